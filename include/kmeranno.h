@@ -1,0 +1,192 @@
+/*
+ * kmeranno.h — C ABI of the MI355X-native signature-kmer annotation library (libkmeranno.so).
+ *
+ * This is the drop-in boundary for the hot path of SEEDtk/kmers.anno (paths relative to the
+ * reference's src/main/java/org/theseed/):
+ *
+ *   - the signature-table load of `apply`
+ *       proteins/kmers/anno/ApplyKmerProcessor.java:100-110   -> kma_table_create*
+ *   - the per-protein extraction + lookup + vote loop of `apply`
+ *       proteins/kmers/anno/ApplyKmerProcessor.java:122-148   -> kma_annotate_proteins*
+ *       (ProteinKmers(...) at :123 is the external org.theseed.sequence extractor)
+ *   - the per-genome role tallies of the APPLY report
+ *       reports/DefaultApplyKmerReporter.java:43-55           -> `tally` outputs
+ *   - the 6-frame contig kmer extractor
+ *       proteins/kmers/KmerReference.java:157-203, KmerPosition.java:50-93
+ *                                                              -> kma_annotate_contigs*
+ *
+ * A Java host would bind these through one JNI class; the C++ CLI under
+ * kmers.anno_amd/host and the Python ctypes module under kmers.anno_amd/python bind them
+ * directly. No HIP or torch types appear here: streams are passed as `void*` (a hipStream_t,
+ * NULL = the legacy default stream) and device buffers as plain pointers.
+ *
+ * Conventions
+ *   - Every function returns an int status: KMA_OK (0) or a negative KMA_E_* code. The message
+ *     of the last failure on the calling thread is available from kma_last_error().
+ *   - "Host" entry points take host buffers owned by the caller and are synchronous.
+ *     "_device" entry points take device buffers on the table's device and are asynchronous
+ *     on the given stream; they never allocate, free or synchronise (graph-capturable).
+ *   - A table is immutable after creation; concurrent annotate calls on one table are
+ *     allowed as long as each uses its own kma_workspace.
+ */
+#ifndef KMERANNO_H
+#define KMERANNO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMA_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------------ */
+#define KMA_OK 0
+#define KMA_E_INVALID (-1)     /* bad argument (usage error; IllegalArgumentException in Java) */
+#define KMA_E_DEVICE (-2)      /* HIP runtime failure / no device                             */
+#define KMA_E_NOMEM (-3)       /* device or host allocation failed                            */
+#define KMA_E_CAPACITY (-4)    /* an output buffer is too small; *needed count is reported    */
+#define KMA_E_ALPHABET (-5)    /* the table needs more than 4 non-[A-Z*] symbols               */
+#define KMA_E_TABLE_FULL (-6)  /* probe chain exhausted during build (load factor too high)    */
+
+/* ---- per-protein call status (out_status) -------------------------------------------------
+ * Mirrors the three outcomes of ApplyKmerProcessor.java:129-147 plus the reporting threshold:
+ *   NONE       no kmer of the protein is in the table            (roleId == null)
+ *   CALLED     all hits agree and count >= min_hits               (recordFeature is called)
+ *   AMBIGUOUS  two different roles hit                            (badPeg == true)
+ *   BELOW_MIN  all hits agree but count < min_hits
+ * out_fid is the role's function id for CALLED / BELOW_MIN and -1 otherwise; out_count is the
+ * number of distinct table kmers hit for CALLED / BELOW_MIN and 0 otherwise.               */
+#define KMA_STATUS_NONE 0
+#define KMA_STATUS_CALLED 1
+#define KMA_STATUS_AMBIGUOUS 2
+#define KMA_STATUS_BELOW_MIN 3
+#define KMA_STATUS_TOO_LONG 4 /* protein beyond the dedupe capacity (> 2^17 windows); fid -1 */
+
+/* ---- extraction flags (kma_annotate_proteins*) ---------------------------------------------
+ * Default (0) is the restatement of org.theseed.sequence.ProteinKmers used by `apply`: the SET
+ * of distinct length-K substrings at window starts i = 0 .. L-K inclusive.
+ *   KMA_F_END_EXCLUSIVE : windows i = 0 .. L-K-1 (the in-repo convention of
+ *                         KmerReference.java:134-136, which skips the last kmer)
+ *   KMA_F_MULTISET      : count every window hit (no within-protein dedupe)                  */
+#define KMA_F_END_EXCLUSIVE 0x1u
+#define KMA_F_MULTISET 0x2u
+
+/* ---- key packing ---------------------------------------------------------------------------
+ * A kmer of K <= 8 residues packs into 5*K bits, first residue most significant:
+ *   key = sum_j code(s[j]) << 5*(K-1-j),  code('A'..'Z') = 1..26, code('*') = 27,
+ *   codes 28..31 are assigned (in byte order) to at most four other bytes that occur in the
+ *   table's kmers; 0 never occurs, so key 0 is the empty-slot sentinel. Packing is injective,
+ *   so key equality is exactly the String.equals of the reference's HashMap lookup.
+ * A table slot is the 64-bit word (key << 24) | fid, so fid < 2^24.                         */
+#define KMA_MAX_K 8
+#define KMA_MAX_FID ((1u << 24) - 1u)
+
+typedef struct kma_table kma_table;         /* opaque: a signature table resident on one GPU */
+typedef struct kma_workspace kma_workspace; /* opaque: per-stream scratch for _device calls  */
+
+typedef struct kma_table_info {
+  uint64_t n_rows;       /* rows passed to create                                          */
+  uint64_t n_skipped;    /* rows whose kmer length != K (can never match; still "loaded")  */
+  uint64_t n_entries;    /* distinct keys stored (duplicates resolved last-wins)           */
+  uint64_t n_buckets;    /* 64-byte buckets of 8 slots                                     */
+  uint64_t bytes;        /* device bytes of the slot array = n_buckets * 64                */
+  int32_t k;             /* kmer length                                                    */
+  int32_t device;        /* HIP device ordinal                                             */
+  uint32_t max_probe;    /* longest bucket chain a stored key needs (1 = home bucket)      */
+  uint32_t n_extra_syms; /* bytes mapped to codes 28..31                                   */
+  uint8_t extra_syms[4];
+} kma_table_info;
+
+/* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
+ * contig `contig` is in the table with function `fid`. Emitted in canonical order
+ * (contig, left, strand '+' before '-').  Location = [left, left + 3K - 1] on the forward
+ * strand, exactly Location.create(contig, dir, left, left + K3) of KmerReference.java:192.  */
+typedef struct kma_hit {
+  uint32_t contig;
+  int32_t left;
+  uint32_t fid;
+  uint8_t strand; /* '+' or '-'                       */
+  uint8_t frame;  /* 1..3 within the strand's sequence */
+  uint16_t pad;
+} kma_hit;
+
+/* ---- library ------------------------------------------------------------------------------ */
+int kma_abi_version(void);
+const char* kma_last_error(void);
+int kma_device_count(int* out_n);
+
+/* Pack n kmers of length K (rows of `text` delimited by offsets[0..n]) with the standard
+ * alphabet + the table's extra symbols. out_keys[r] = 0 for a row that is not of length K or
+ * contains a byte the table cannot encode. Host-side helper; no device needed.             */
+int kma_pack_kmers(const kma_table* table, const char* text, const uint64_t* offsets, uint64_t n,
+                   uint64_t* out_keys);
+
+/* ---- signature table (ApplyKmerProcessor.java:100-110) -------------------------------------
+ * Rows are (kmer text, fid) in file order. Duplicate kmers: the LAST row wins (HashMap.put).
+ * Rows whose kmer is not of length K are counted in n_skipped and never match (apply's
+ * ProteinKmers keeps its own K = 8 whatever KmerReference.setKmerSize(:108) is given).
+ * load_factor <= 0 selects the default 0.5.                                                   */
+int kma_table_create(const char* text, const uint64_t* offsets, const uint32_t* fids, uint64_t n,
+                     int k, int device, double load_factor, kma_table** out);
+/* Same from pre-packed keys (standard alphabet only; key 0 rows are skipped).               */
+int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t n, int k,
+                            int device, double load_factor, kma_table** out);
+int kma_table_info_get(const kma_table* table, kma_table_info* out);
+int kma_table_destroy(kma_table* table);
+
+/* Device-resident construction for hosts that own device memory (e.g. a torch allocation
+ * that is later broadcast over RCCL to the other GPUs of the node).
+ *   kma_table_buckets_for : bucket count for n keys at the load factor
+ *   kma_table_build_device: d_slots (n_buckets*64 bytes) and d_winner (n_buckets*8 u32) are
+ *                           caller scratch; keys/fids are device arrays; builds on `stream`.
+ *   kma_table_wrap_device : adopt an already-built slot array (not owned, not freed).        */
+uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+                           const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
+                           uint32_t* d_status, void* stream);
+int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device,
+                          kma_table** out);
+/* Raw view of the slot array (device pointer) — what an RCCL broadcast moves.               */
+int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes);
+
+/* ---- workspaces ----------------------------------------------------------------------------- */
+int kma_workspace_create(int device, kma_workspace** out);
+int kma_workspace_destroy(kma_workspace* ws);
+
+/* ---- protein annotation (ApplyKmerProcessor.java:118-148) ----------------------------------
+ * residues: raw ASCII proteins concatenated; sequence s is residues[offsets[s]..offsets[s+1]).
+ * min_hits >= 1 (ApplyKmerProcessor.java:91-92). out_tally (optional, length n_fid) receives
+ * += 1 per CALLED protein at its fid (the APPLY report's role counts before column mapping).
+ * Host form: synchronous, host buffers.                                                       */
+int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
+                          const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
+                          int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
+                          uint32_t* out_tally, uint32_t n_fid);
+/* Device form: every pointer is device memory on the table's device; `d_residues` must be
+ * readable for 16 bytes past offsets[n_seq]; d_tally (n_fid u32) is accumulated into, not
+ * cleared. Asynchronous on `stream`.                                                          */
+int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
+                                 const uint8_t* d_residues, const uint64_t* d_offsets,
+                                 uint32_t n_seq, int min_hits, uint32_t flags, int32_t* d_fid,
+                                 int32_t* d_count, uint8_t* d_status, uint32_t* d_tally,
+                                 uint32_t n_fid, void* stream);
+
+/* ---- 6-frame contig annotation (KmerReference.java:157-203 + table probe) -----------------
+ * dna: contigs concatenated (any case; bases other than ACGT translate to 'X'); offsets as
+ * above. genetic_code: NCBI table id (1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 16, 21, 22, 23,
+ * 24, 25). Windows follow processKmers exactly (i < P_f - K end
+ * exclusion, '*'/'X' windows skipped). Every remaining window is probed; hits are written in
+ * canonical order. If cap is too small, returns KMA_E_CAPACITY with *n_hits = needed.
+ * out_tally (optional, n_contig * n_fid u32, row-major by contig) counts hits per function. */
+int kma_annotate_contigs(const kma_table* table, const uint8_t* dna, const uint64_t* offsets,
+                         uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
+                         uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid);
+/* Window count of the 6-frame extractor before the '*'/'X' filter (for throughput metrics).  */
+uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMERANNO_H */

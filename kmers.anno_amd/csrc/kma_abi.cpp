@@ -1,0 +1,557 @@
+// kma_abi.cpp — the C ABI of libkmeranno.so (declared in include/kmeranno.h).
+//
+// Host-side orchestration only: argument checks, key packing, device allocation and copies,
+// and kernel launches (kma_kernels.hip). No compute falls back to the CPU: without a usable
+// HIP device every entry point that needs one returns KMA_E_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/kmeranno.h"
+#include "kma_internal.h"
+
+struct kma_table {
+  int device = 0;
+  int k = 8;
+  uint64_t n_buckets = 0;
+  uint64_t* d_slots = nullptr;
+  bool owned = false;
+  uint8_t* d_lut = nullptr;
+  uint8_t lut[256] = {};
+  kma_table_info info = {};
+};
+
+struct kma_workspace {
+  int device = 0;
+  uint32_t* d_flag = nullptr;
+  uint32_t* d_scratch = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define KMA_HIP(call)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(e_ == hipErrorOutOfMemory ? KMA_E_NOMEM : KMA_E_DEVICE, "%s: %s (%s:%d)", \
+                  #call, hipGetErrorString(e_), __FILE__, __LINE__);                    \
+  } while (0)
+
+// Make `device` current for the scope; restore the caller's device after (torch keeps its own).
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(device);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Device buffers freed on scope exit (host entry points only).
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  template <class T>
+  hipError_t alloc(T** out, size_t bytes) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 1);
+    if (e == hipSuccess) p.push_back(q);
+    *out = static_cast<T*>(q);
+    return e;
+  }
+};
+
+void standard_lut(uint8_t lut[256]) {
+  std::memset(lut, 0, 256);
+  for (int c = 'A'; c <= 'Z'; ++c) lut[c] = (uint8_t)(c - 'A' + 1);
+  lut[(uint8_t)'*'] = 27;
+}
+
+int check_k(int k) {
+  if (k < 1 || k > KMA_MAX_K) return fail(KMA_E_INVALID, "kmer size %d outside 1..%d", k, KMA_MAX_K);
+  return KMA_OK;
+}
+
+// Pack rows [lo, hi) with the LUT; 0 for rows of the wrong length or with unencodable bytes.
+void pack_rows(const uint8_t* lut, const char* text, const uint64_t* off, uint64_t lo, uint64_t hi,
+               int k, uint64_t* keys) {
+  for (uint64_t r = lo; r < hi; ++r) {
+    const uint64_t b = off[r], e = off[r + 1];
+    uint64_t key = 0;
+    if (e - b == (uint64_t)k) {
+      for (int j = 0; j < k; ++j) {
+        const uint8_t c = lut[(uint8_t)text[b + j]];
+        if (!c) {
+          key = 0;
+          break;
+        }
+        key = (key << 5) | c;
+      }
+    }
+    keys[r] = key;
+  }
+}
+
+template <class F>
+void parallel_rows(uint64_t n, F f) {
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < (1u << 16)) nt = 1;
+  std::vector<std::thread> th;
+  const uint64_t chunk = (n + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const uint64_t lo = t * chunk, hi = std::min(n, lo + chunk);
+    if (lo < hi) th.emplace_back(f, lo, hi);
+  }
+  for (auto& x : th) x.join();
+}
+
+// NCBI translation tables, codons in T, C, A, G order.
+const char* ncbi_code(int gc) {
+  switch (gc) {
+    case 1: case 11: return "FFLLSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 2: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSS**VVVVAAAADDEEGGGG";
+    case 3: return "FFLLSSSSYY**CCWWTTTTPPPPHHQQRRRRIIMMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 4: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 5: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSSSSVVVVAAAADDEEGGGG";
+    case 6: return "FFLLSSSSYYQQCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 9: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 10: return "FFLLSSSSYY**CCCWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 12: return "FFLLSSSSYY**CC*WLLLSPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 13: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSSGGVVVVAAAADDEEGGGG";
+    case 14: return "FFLLSSSSYYY*CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 16: return "FFLLSSSSYY*LCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 21: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 22: return "FFLLSS*SYY*LCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 23: return "FF*LSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 24: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSSKVVVVAAAADDEEGGGG";
+    case 25: return "FFLLSSSSYY**CCGWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    default: return nullptr;
+  }
+}
+
+int make_table_object(int device, int k, uint64_t n_buckets, uint64_t* d_slots, bool owned,
+                      const uint8_t lut[256], kma_table** out) {
+  kma_table* t = new kma_table();
+  t->device = device;
+  t->k = k;
+  t->n_buckets = n_buckets;
+  t->d_slots = d_slots;
+  t->owned = owned;
+  std::memcpy(t->lut, lut, 256);
+  hipError_t e = hipMalloc(&t->d_lut, 256);
+  if (e == hipSuccess) e = hipMemcpy(t->d_lut, lut, 256, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (t->d_lut) (void)hipFree(t->d_lut);
+    delete t;
+    return fail(KMA_E_DEVICE, "table LUT upload: %s", hipGetErrorString(e));
+  }
+  t->info.n_buckets = n_buckets;
+  t->info.bytes = n_buckets * 64;
+  t->info.k = k;
+  t->info.device = device;
+  *out = t;
+  return KMA_OK;
+}
+
+int build_on_device(uint64_t* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+                    const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, uint32_t* d_status,
+                    hipStream_t s) {
+  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * 64, s));
+  KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::kSlotsPerBucket * sizeof(uint32_t), s));
+  KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
+  KMA_HIP(kma::launch_build_insert(d_slots, d_winner, n_buckets, d_keys, n, d_status, s));
+  KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, n_buckets, d_status + 1, s));
+  return KMA_OK;
+}
+
+// Shared by both create forms: keys packed on the host with `lut`.
+int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, uint64_t n, int k,
+                     int device, double lf, const uint8_t lut[256], uint64_t n_skipped,
+                     kma_table** out) {
+  if (lf <= 0) lf = 0.5;
+  if (lf > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", lf);
+  for (uint64_t r = 0; r < n; ++r)
+    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^24-1",
+                                            fids[r], (unsigned long long)r);
+  const uint64_t nb = kma_table_buckets_for(n, lf);
+  if (nb * kma::kSlotsPerBucket >= 0xFFFFFFFFull)
+    return fail(KMA_E_INVALID, "table too large: %llu buckets", (unsigned long long)nb);
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  DevBufs tmp;
+  uint64_t* d_keys;
+  uint32_t *d_fids, *d_winner, *d_status;
+  KMA_HIP(tmp.alloc(&d_keys, n * 8));
+  KMA_HIP(tmp.alloc(&d_fids, n * 4));
+  KMA_HIP(tmp.alloc(&d_winner, nb * kma::kSlotsPerBucket * 4));
+  KMA_HIP(tmp.alloc(&d_status, 16));
+  uint64_t* d_slots = nullptr;
+  KMA_HIP(hipMalloc(&d_slots, nb * 64));
+  KMA_HIP(hipMemcpy(d_keys, keys.data(), n * 8, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_fids, fids, n * 4, hipMemcpyHostToDevice));
+  int rc = build_on_device(d_slots, nb, d_winner, d_keys, d_fids, n, d_status, nullptr);
+  uint32_t st[4] = {};
+  if (rc == KMA_OK) {
+    hipError_t e = hipMemcpy(st, d_status, 16, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(KMA_E_DEVICE, "build: %s", hipGetErrorString(e));
+    else if (st[0]) rc = fail(KMA_E_TABLE_FULL, "signature table full");
+  }
+  if (rc == KMA_OK) rc = make_table_object(device, k, nb, d_slots, true, lut, out);
+  if (rc != KMA_OK) {
+    (void)hipFree(d_slots);
+    return rc;
+  }
+  (*out)->info.n_rows = n;
+  (*out)->info.n_skipped = n_skipped;
+  (*out)->info.n_entries = st[1];
+  (*out)->info.max_probe = st[2];
+  int ne = 0;
+  for (int c = 0; c < 256; ++c)
+    if (lut[c] >= 28) (*out)->info.extra_syms[lut[c] - 28] = (uint8_t)c, ++ne;
+  (*out)->info.n_extra_syms = ne;
+  return KMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kma_abi_version(void) { return KMA_ABI_VERSION; }
+
+const char* kma_last_error(void) { return g_err.c_str(); }
+
+int kma_device_count(int* out_n) {
+  if (!out_n) return fail(KMA_E_INVALID, "null out_n");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *out_n = 0;
+    return fail(KMA_E_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *out_n = n;
+  return KMA_OK;
+}
+
+uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor) {
+  if (load_factor <= 0) load_factor = 0.5;
+  const double slots = (double)(n_keys ? n_keys : 1) / load_factor;
+  uint64_t nb = (uint64_t)((slots + kma::kSlotsPerBucket - 1) / kma::kSlotsPerBucket);
+  return nb < 1 ? 1 : nb;
+}
+
+int kma_pack_kmers(const kma_table* table, const char* text, const uint64_t* offsets, uint64_t n,
+                   uint64_t* out_keys) {
+  if (!table || (!text && n) || !offsets || (!out_keys && n))
+    return fail(KMA_E_INVALID, "null argument");
+  pack_rows(table->lut, text, offsets, 0, n, table->k, out_keys);
+  return KMA_OK;
+}
+
+int kma_table_create(const char* text, const uint64_t* offsets, const uint32_t* fids, uint64_t n,
+                     int k, int device, double load_factor, kma_table** out) {
+  if (!out || (n && (!text || !offsets || !fids))) return fail(KMA_E_INVALID, "null argument");
+  if (int rc = check_k(k)) return rc;
+  // Alphabet: standard A-Z and '*', plus up to four other bytes found in K-length rows.
+  bool seen[256] = {};
+  for (uint64_t r = 0; r < n; ++r)
+    if (offsets[r + 1] - offsets[r] == (uint64_t)k)
+      for (uint64_t i = offsets[r]; i < offsets[r + 1]; ++i) seen[(uint8_t)text[i]] = true;
+  uint8_t lut[256];
+  standard_lut(lut);
+  int extra = 0;
+  for (int c = 0; c < 256; ++c)
+    if (seen[c] && !lut[c]) {
+      if (extra == 4) return fail(KMA_E_ALPHABET, "more than 4 kmer symbols outside [A-Z*]");
+      lut[c] = (uint8_t)(28 + extra++);
+    }
+  std::vector<uint64_t> keys(n);
+  parallel_rows(n, [&](uint64_t lo, uint64_t hi) {
+    pack_rows(lut, text, offsets, lo, hi, k, keys.data());
+  });
+  uint64_t skipped = 0;
+  for (uint64_t r = 0; r < n; ++r) skipped += offsets[r + 1] - offsets[r] != (uint64_t)k;
+  return create_from_keys(keys, fids, n, k, device, load_factor, lut, skipped, out);
+}
+
+int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t n, int k,
+                            int device, double load_factor, kma_table** out) {
+  if (!out || (n && (!keys || !fids))) return fail(KMA_E_INVALID, "null argument");
+  if (int rc = check_k(k)) return rc;
+  uint8_t lut[256];
+  standard_lut(lut);
+  std::vector<uint64_t> kv(keys, keys + n);
+  uint64_t skipped = 0;
+  const uint64_t lim = 1ull << (5 * k);
+  for (uint64_t r = 0; r < n; ++r)
+    if (kv[r] == 0 || kv[r] >= lim) kv[r] = 0, ++skipped;
+  return create_from_keys(kv, fids, n, k, device, load_factor, lut, skipped, out);
+}
+
+int kma_table_info_get(const kma_table* table, kma_table_info* out) {
+  if (!table || !out) return fail(KMA_E_INVALID, "null argument");
+  *out = table->info;
+  return KMA_OK;
+}
+
+int kma_table_destroy(kma_table* table) {
+  if (!table) return KMA_OK;
+  DeviceScope ds(table->device);
+  if (table->owned && table->d_slots) (void)hipFree(table->d_slots);
+  if (table->d_lut) (void)hipFree(table->d_lut);
+  delete table;
+  return KMA_OK;
+}
+
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+                           const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
+                           uint32_t* d_status, void* stream) {
+  if (!d_slots || !d_winner || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
+    return fail(KMA_E_INVALID, "null argument");
+  return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, d_winner, d_keys, d_fids, n,
+                         d_status, static_cast<hipStream_t>(stream));
+}
+
+int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device, kma_table** out) {
+  if (!d_slots || !out || !n_buckets) return fail(KMA_E_INVALID, "null argument");
+  if (int rc = check_k(k)) return rc;
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
+  uint8_t lut[256];
+  standard_lut(lut);
+  return make_table_object(device, k, n_buckets, static_cast<uint64_t*>(d_slots), false, lut, out);
+}
+
+int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes) {
+  if (!table || !d_slots || !bytes) return fail(KMA_E_INVALID, "null argument");
+  *d_slots = table->d_slots;
+  *bytes = table->n_buckets * 64;
+  return KMA_OK;
+}
+
+int kma_workspace_create(int device, kma_workspace** out) {
+  if (!out) return fail(KMA_E_INVALID, "null argument");
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
+  kma_workspace* w = new kma_workspace();
+  w->device = device;
+  hipError_t e = hipMalloc(&w->d_flag, 16);
+  if (e == hipSuccess)
+    e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 4);
+  if (e != hipSuccess) {
+    if (w->d_flag) (void)hipFree(w->d_flag);
+    delete w;
+    return fail(KMA_E_NOMEM, "workspace: %s", hipGetErrorString(e));
+  }
+  *out = w;
+  return KMA_OK;
+}
+
+int kma_workspace_destroy(kma_workspace* ws) {
+  if (!ws) return KMA_OK;
+  DeviceScope ds(ws->device);
+  (void)hipFree(ws->d_flag);
+  (void)hipFree(ws->d_scratch);
+  delete ws;
+  return KMA_OK;
+}
+
+int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const uint8_t* d_residues,
+                                 const uint64_t* d_offsets, uint32_t n_seq, int min_hits,
+                                 uint32_t flags, int32_t* d_fid, int32_t* d_count,
+                                 uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
+                                 void* stream) {
+  if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
+  if (ws->device != t->device) return fail(KMA_E_INVALID, "workspace on another device");
+  if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
+  if (flags & ~(KMA_F_END_EXCLUSIVE | KMA_F_MULTISET)) return fail(KMA_E_INVALID, "bad flags");
+  if (n_seq == 0) return KMA_OK;
+  if (!d_residues || !d_offsets || !d_fid || !d_count || !d_status)
+    return fail(KMA_E_INVALID, "null device buffer");
+  if ((uintptr_t)d_residues & 7) return fail(KMA_E_INVALID, "residues must be 8-byte aligned");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DeviceScope ds(t->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  KMA_HIP(hipMemsetAsync(ws->d_flag, 0, 4, s));
+  kma::ProteinArgs a{};
+  a.slots = t->d_slots;
+  a.n_buckets = t->n_buckets;
+  a.lut = t->d_lut;
+  a.residues = d_residues;
+  a.offsets = d_offsets;
+  a.n_seq = n_seq;
+  a.k = t->k;
+  a.min_hits = min_hits;
+  a.flags = flags;
+  a.out_fid = d_fid;
+  a.out_count = d_count;
+  a.out_status = d_status;
+  a.tally = d_tally;
+  a.n_fid = d_tally ? n_fid : 0;
+  a.overflow_flag = ws->d_flag;
+  a.scratch = ws->d_scratch;
+  KMA_HIP(kma::launch_proteins(a, s));
+  return KMA_OK;
+}
+
+int kma_annotate_proteins(const kma_table* t, const uint8_t* residues, const uint64_t* offsets,
+                          uint32_t n_seq, int min_hits, uint32_t flags, int32_t* out_fid,
+                          int32_t* out_count, uint8_t* out_status, uint32_t* out_tally,
+                          uint32_t n_fid) {
+  if (!t) return fail(KMA_E_INVALID, "null table");
+  if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
+  if (n_seq == 0) return KMA_OK;
+  if (!residues || !offsets || !out_fid || !out_count || !out_status)
+    return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t s = 0; s < n_seq; ++s)
+    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
+  DeviceScope ds(t->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  const uint64_t base = offsets[0], nres = offsets[n_seq] - base;
+  std::vector<uint64_t> rel(offsets, offsets + n_seq + 1);
+  for (auto& o : rel) o -= base;
+  DevBufs b;
+  uint8_t *d_res, *d_st;
+  uint64_t* d_off;
+  int32_t *d_fid, *d_cnt;
+  uint32_t* d_tally = nullptr;
+  KMA_HIP(b.alloc(&d_res, nres + 16));
+  KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_fid, n_seq * 4ull));
+  KMA_HIP(b.alloc(&d_cnt, n_seq * 4ull));
+  KMA_HIP(b.alloc(&d_st, n_seq));
+  KMA_HIP(hipMemcpy(d_res, residues + base, nres, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_res + nres, 0, 16));
+  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_seq + 1) * 8ull, hipMemcpyHostToDevice));
+  if (out_tally && n_fid) {
+    KMA_HIP(b.alloc(&d_tally, n_fid * 4ull));
+    KMA_HIP(hipMemcpy(d_tally, out_tally, n_fid * 4ull, hipMemcpyHostToDevice));
+  }
+  kma_workspace* ws = nullptr;
+  if (int rc = kma_workspace_create(t->device, &ws)) return rc;
+  int rc = kma_annotate_proteins_device(t, ws, d_res, d_off, n_seq, min_hits, flags, d_fid, d_cnt,
+                                        d_st, d_tally, d_tally ? n_fid : 0, nullptr);
+  hipError_t e = rc == KMA_OK ? hipDeviceSynchronize() : hipSuccess;
+  kma_workspace_destroy(ws);
+  if (rc != KMA_OK) return rc;
+  if (e != hipSuccess) return fail(KMA_E_DEVICE, "annotate: %s", hipGetErrorString(e));
+  KMA_HIP(hipMemcpy(out_fid, d_fid, n_seq * 4ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(out_count, d_cnt, n_seq * 4ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(out_status, d_st, n_seq, hipMemcpyDeviceToHost));
+  if (d_tally) KMA_HIP(hipMemcpy(out_tally, d_tally, n_fid * 4ull, hipMemcpyDeviceToHost));
+  return KMA_OK;
+}
+
+uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k) {
+  uint64_t n = 0;
+  for (uint32_t c = 0; c < n_contig; ++c) {
+    const int64_t len = (int64_t)(offsets[c + 1] - offsets[c]);
+    const int64_t per = len - 3 * k - 2;  // sum over frames of max(0, P_f - K), per strand
+    if (per > 0) n += 2 * (uint64_t)per;
+  }
+  return n;
+}
+
+int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
+                         uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
+                         uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid) {
+  if (!t || !n_hits) return fail(KMA_E_INVALID, "null argument");
+  const char* code = ncbi_code(genetic_code);
+  if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
+  *n_hits = 0;
+  if (n_contig == 0) return KMA_OK;
+  if (!dna || !offsets) return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t c = 0; c < n_contig; ++c)
+    if (offsets[c + 1] < offsets[c]) return fail(KMA_E_INVALID, "offsets decrease at %u", c);
+  const uint64_t base = offsets[0], total = offsets[n_contig] - base;
+  if (total >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
+  std::vector<uint64_t> rel(offsets, offsets + n_contig + 1);
+  for (auto& o : rel) o -= base;
+  uint8_t codes[64];
+  for (int i = 0; i < 64; ++i)
+    codes[i] = (code[i] == '*' || code[i] == 'X') ? 0 : (uint8_t)(code[i] - 'A' + 1);
+  DeviceScope ds(t->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  const uint64_t n_blocks = std::max<uint64_t>(1, (total + kma::kContigTile - 1) / kma::kContigTile);
+  DevBufs b;
+  uint8_t *d_dna, *d_codes;
+  uint64_t *d_off, *d_staging, *d_prefix;
+  uint32_t *d_counts, *d_tally = nullptr;
+  KMA_HIP(b.alloc(&d_dna, total + 64));
+  KMA_HIP(b.alloc(&d_off, (n_contig + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_codes, 64));
+  KMA_HIP(b.alloc(&d_staging, n_blocks * 2 * kma::kContigTile * 8));
+  KMA_HIP(b.alloc(&d_counts, n_blocks * 4));
+  KMA_HIP(b.alloc(&d_prefix, n_blocks * 8));
+  KMA_HIP(hipMemcpy(d_dna, dna + base, total, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_dna + total, 0, 64));
+  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_contig + 1) * 8ull, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_codes, codes, 64, hipMemcpyHostToDevice));
+  if (out_tally && n_fid) {
+    const uint64_t tb = (uint64_t)n_contig * n_fid * 4;
+    KMA_HIP(b.alloc(&d_tally, tb));
+    KMA_HIP(hipMemcpy(d_tally, out_tally, tb, hipMemcpyHostToDevice));
+  }
+  kma::ContigArgs a{};
+  a.slots = t->d_slots;
+  a.n_buckets = t->n_buckets;
+  a.dna = d_dna;
+  a.offsets = d_off;
+  a.n_contig = n_contig;
+  a.total_bases = total;
+  a.k = t->k;
+  a.codon_codes = d_codes;
+  a.staging = d_staging;
+  a.block_counts = d_counts;
+  a.tally = d_tally;
+  a.n_fid = d_tally ? n_fid : 0;
+  KMA_HIP(kma::launch_contigs_probe(a, n_blocks, nullptr));
+  size_t temp_bytes = 0;
+  KMA_HIP(kma::launch_contig_scan(d_counts, d_prefix, n_blocks, nullptr, &temp_bytes, nullptr));
+  void* d_temp;
+  KMA_HIP(b.alloc(&d_temp, temp_bytes));
+  KMA_HIP(kma::launch_contig_scan(d_counts, d_prefix, n_blocks, d_temp, &temp_bytes, nullptr));
+  uint64_t last_prefix = 0;
+  uint32_t last_count = 0;
+  KMA_HIP(hipMemcpy(&last_prefix, d_prefix + n_blocks - 1, 8, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(&last_count, d_counts + n_blocks - 1, 4, hipMemcpyDeviceToHost));
+  const uint64_t nh = last_prefix + last_count;
+  *n_hits = nh;
+  // On KMA_E_CAPACITY nothing is written (the tally neither), so the caller can retry.
+  if (nh > cap) return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
+                            (unsigned long long)cap);
+  if (d_tally)
+    KMA_HIP(hipMemcpy(out_tally, d_tally, (uint64_t)n_contig * n_fid * 4, hipMemcpyDeviceToHost));
+  if (nh == 0) return KMA_OK;
+  if (!out_hits) return fail(KMA_E_INVALID, "null out_hits");
+  uint8_t* d_out;
+  KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
+  KMA_HIP(kma::launch_contigs(a, n_blocks, d_prefix, d_out, nullptr));
+  KMA_HIP(hipMemcpy(out_hits, d_out, nh * sizeof(kma_hit), hipMemcpyDeviceToHost));
+  return KMA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,271 @@
+"""ctypes binding of libkmeranno.so (include/kmeranno.h) for tests and bench.py.
+
+The library is the product; this module only marshals numpy buffers (host entry points) or
+raw device pointers (the ``*_device`` entry points, e.g. torch tensors' ``data_ptr()``).
+There is no CPU fallback: if the shared library is missing or no HIP device is usable,
+calls raise ``KmerAnnoError``.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(PKG_ROOT, "build", "libkmeranno.so")
+
+OK = 0
+E_INVALID, E_DEVICE, E_NOMEM, E_CAPACITY, E_ALPHABET, E_TABLE_FULL = -1, -2, -3, -4, -5, -6
+STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN, STATUS_TOO_LONG = 0, 1, 2, 3, 4
+F_END_EXCLUSIVE, F_MULTISET = 0x1, 0x2
+MAX_K = 8
+
+# Every symbol include/kmeranno.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "kma_abi_version", "kma_last_error", "kma_device_count", "kma_pack_kmers",
+    "kma_table_create", "kma_table_create_packed", "kma_table_info_get", "kma_table_destroy",
+    "kma_table_buckets_for", "kma_table_build_device", "kma_table_wrap_device",
+    "kma_table_device_ptr", "kma_workspace_create", "kma_workspace_destroy",
+    "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
+    "kma_contig_window_count",
+)
+
+
+class KmerAnnoError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"kmeranno error {code}: {msg}")
+        self.code = code
+
+
+class TableInfo(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_skipped", C.c_uint64), ("n_entries", C.c_uint64),
+                ("n_buckets", C.c_uint64), ("bytes", C.c_uint64), ("k", C.c_int32),
+                ("device", C.c_int32), ("max_probe", C.c_uint32), ("n_extra_syms", C.c_uint32),
+                ("extra_syms", C.c_uint8 * 4)]
+
+
+HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
+                      ("frame", "u1"), ("pad", "<u2")])
+
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C")
+_u64p = np.ctypeslib.ndpointer(np.uint64, flags="C")
+_vp, _u64, _u32, _int = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libkmeranno.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise KmerAnnoError(E_DEVICE, f"{p} not built (run `make -C kmers.anno_amd`)")
+        L = C.CDLL(p)
+        L.kma_last_error.restype = C.c_char_p
+        L.kma_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.kma_pack_kmers.argtypes = [_vp, C.c_char_p, _u64p, _u64, _u64p]
+        L.kma_table_create.argtypes = [C.c_char_p, _u64p, _u32p, _u64, _int, _int, C.c_double,
+                                       C.POINTER(_vp)]
+        L.kma_table_create_packed.argtypes = [_u64p, _u32p, _u64, _int, _int, C.c_double,
+                                              C.POINTER(_vp)]
+        L.kma_table_info_get.argtypes = [_vp, C.POINTER(TableInfo)]
+        L.kma_table_destroy.argtypes = [_vp]
+        L.kma_table_buckets_for.restype = _u64
+        L.kma_table_buckets_for.argtypes = [_u64, C.c_double]
+        L.kma_table_build_device.argtypes = [_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]
+        L.kma_table_wrap_device.argtypes = [_vp, _u64, _int, _int, C.POINTER(_vp)]
+        L.kma_table_device_ptr.argtypes = [_vp, C.POINTER(_vp), C.POINTER(_u64)]
+        L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
+        L.kma_workspace_destroy.argtypes = [_vp]
+        L.kma_annotate_proteins.argtypes = [_vp, _u8p, _u64p, _u32, _int, _u32, _i32p, _i32p,
+                                            _u8p, _vp, _u32]
+        L.kma_annotate_proteins_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _int, _u32, _vp,
+                                                   _vp, _vp, _vp, _u32, _vp]
+        L.kma_annotate_contigs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _vp, _u64,
+                                           C.POINTER(_u64), _vp, _u32]
+        L.kma_contig_window_count.restype = _u64
+        L.kma_contig_window_count.argtypes = [_u64p, _u32, _int]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc != OK:
+        raise KmerAnnoError(rc, load().kma_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(load().kma_device_count(C.byref(n)))
+    return n.value
+
+
+def pack_strings(strs):
+    """Concatenate strings -> (uint8 buffer padded by 16 bytes, uint64 offsets)."""
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
+    offsets = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        offsets[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 16, dtype=np.uint8).copy()
+    return buf, offsets
+
+
+def std_codes(ascii_bytes: np.ndarray) -> np.ndarray:
+    """Standard 5-bit residue codes ('A'..'Z' -> 1..26, '*' -> 27, other -> 0)."""
+    b = ascii_bytes.astype(np.int64)
+    c = np.where((b >= 65) & (b <= 90), b - 64, 0)
+    return np.where(b == 42, 27, c).astype(np.uint64)
+
+
+def pack_std(kmers_u8: np.ndarray) -> np.ndarray:
+    """Pack an (n, k) uint8 array of ASCII kmers into keys (standard alphabet, 0 if invalid)."""
+    codes = std_codes(kmers_u8)
+    k = kmers_u8.shape[1]
+    keys = np.zeros(len(kmers_u8), np.uint64)
+    for j in range(k):
+        keys = (keys << np.uint64(5)) | codes[:, j]
+    keys[(codes == 0).any(axis=1)] = 0
+    return keys
+
+
+class SignatureTable:
+    """A signature table resident on one GPU (ApplyKmerProcessor.java:100-110)."""
+
+    def __init__(self, handle, owner=True):
+        self._h = handle
+        self._owner = owner
+
+    @classmethod
+    def from_rows(cls, kmers, fids, k: int = 8, device: int = 0, load_factor: float = 0.5):
+        buf, off = pack_strings(kmers)
+        h = _vp()
+        _check(load().kma_table_create(buf.tobytes(), off, np.ascontiguousarray(fids, np.uint32),
+                                       len(off) - 1, k, device, load_factor, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_packed(cls, keys, fids, k: int = 8, device: int = 0, load_factor: float = 0.5):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        h = _vp()
+        _check(load().kma_table_create_packed(keys, np.ascontiguousarray(fids, np.uint32),
+                                              len(keys), k, device, load_factor, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def wrap_device(cls, d_slots: int, n_buckets: int, k: int = 8, device: int = 0):
+        h = _vp()
+        _check(load().kma_table_wrap_device(d_slots, n_buckets, k, device, C.byref(h)))
+        return cls(h)
+
+    @property
+    def info(self) -> TableInfo:
+        i = TableInfo()
+        _check(load().kma_table_info_get(self._h, C.byref(i)))
+        return i
+
+    def device_ptr(self):
+        p, n = _vp(), _u64()
+        _check(load().kma_table_device_ptr(self._h, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def pack(self, kmers) -> np.ndarray:
+        buf, off = pack_strings(kmers)
+        out = np.zeros(len(off) - 1, np.uint64)
+        _check(load().kma_pack_kmers(self._h, buf.tobytes(), off, len(off) - 1, out))
+        return out
+
+    def close(self):
+        if self._h:
+            load().kma_table_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class Workspace:
+    def __init__(self, device: int = 0):
+        self._h = _vp()
+        _check(load().kma_workspace_create(device, C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            load().kma_workspace_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def buckets_for(n_keys: int, load_factor: float = 0.5) -> int:
+    return int(load().kma_table_buckets_for(n_keys, load_factor))
+
+
+def build_device(d_slots: int, n_buckets: int, d_winner: int, d_keys: int, d_fids: int, n: int,
+                 d_status: int, stream: int = 0):
+    _check(load().kma_table_build_device(d_slots, n_buckets, d_winner, d_keys, d_fids, n,
+                                         d_status, stream or None))
+
+
+def annotate_proteins(table: SignatureTable, residues: np.ndarray, offsets: np.ndarray,
+                      min_hits: int = 5, flags: int = 0, n_fid: int = 0):
+    """Host form of the apply loop: returns (fid, count, status, tally-or-None)."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets) - 1
+    fid, cnt, st = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint8)
+    tally = np.zeros(n_fid, np.uint32) if n_fid else None
+    _check(load().kma_annotate_proteins(table._h, residues, offsets, n, min_hits, flags, fid, cnt,
+                                        st, tally.ctypes.data if n_fid else None, n_fid))
+    return fid, cnt, st, tally
+
+
+def annotate_proteins_device(table: SignatureTable, ws: Workspace, d_residues: int,
+                             d_offsets: int, n_seq: int, min_hits: int, flags: int, d_fid: int,
+                             d_count: int, d_status: int, d_tally: int = 0, n_fid: int = 0,
+                             stream: int = 0):
+    _check(load().kma_annotate_proteins_device(table._h, ws._h, d_residues, d_offsets, n_seq,
+                                               min_hits, flags, d_fid, d_count, d_status,
+                                               d_tally or None, n_fid, stream or None))
+
+
+def annotate_contigs(table: SignatureTable, dna: np.ndarray, offsets: np.ndarray,
+                     genetic_code: int = 11, n_fid: int = 0):
+    """6-frame annotation: returns (hits structured array, tally[n_contig, n_fid] or None)."""
+    dna = np.ascontiguousarray(dna, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n_contig = len(offsets) - 1
+    cap = max(1024, int(load().kma_contig_window_count(offsets, n_contig, table.info.k)) // 8)
+    while True:
+        hits = np.empty(cap, HIT_DTYPE)
+        tally = np.zeros((n_contig, n_fid), np.uint32) if n_fid else None
+        nh = _u64()
+        rc = load().kma_annotate_contigs(table._h, dna, offsets, n_contig, genetic_code,
+                                         hits.ctypes.data, cap, C.byref(nh),
+                                         tally.ctypes.data if n_fid else None, n_fid)
+        if rc == E_CAPACITY:
+            cap = nh.value
+            continue
+        _check(rc)
+        return hits[:nh.value], tally
+
+
+def contig_window_count(offsets: np.ndarray, k: int = 8) -> int:
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    return int(load().kma_contig_window_count(offsets, len(offsets) - 1, k))

@@ -1,0 +1,170 @@
+"""Seeded synthetic workloads for the BASELINE.json configs (SURVEY.md §8(d) generator).
+
+- protein lengths resampled from the 712 CDS lengths of the reference fixture small.gto
+  (data/small_gto_cds_lengths.txt: min 35, median 264, mean 310.5, max 2955);
+- residues iid uniform over the 20 standard amino acids;
+- F functions, one prototype protein each; the signature table holds prototype 8-mers that are
+  unique to one function (BuildKmerProcessor.java:157-208's rule), at most T // F per function,
+  padded with random decoy 8-mers up to T rows, rows shuffled;
+- queries: 50% prototype copies with 10% per-residue substitution, 40% random proteins,
+  10% chimeras (first half of one prototype + second half of another, both mutated);
+- role string of fid i is ROLE%07d.
+Keys use the standard 5-bit packing of include/kmeranno.h.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+AA = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", dtype=np.uint8)
+AA_CODES = (AA.astype(np.uint64) - 64)  # 'A' -> 1 ... 'Y' -> 25
+_LEN_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                         "small_gto_cds_lengths.txt")
+
+
+def cds_lengths() -> np.ndarray:
+    return np.loadtxt(_LEN_FILE, dtype=np.int64, comments="#")
+
+
+def window_keys(res: np.ndarray, k: int = 8) -> np.ndarray:
+    """Packed keys of every window of one ASCII protein (standard alphabet)."""
+    codes = res.astype(np.uint64) - 64
+    n = len(res) - k + 1
+    if n <= 0:
+        return np.zeros(0, np.uint64)
+    key = np.zeros(n, np.uint64)
+    for j in range(k):
+        key = (key << np.uint64(5)) | codes[j:j + n]
+    return key
+
+
+def unpack_key(key: int, k: int = 8) -> str:
+    return "".join(chr(64 + ((int(key) >> (5 * (k - 1 - j))) & 31)) for j in range(k))
+
+
+@dataclass
+class Workload:
+    keys: np.ndarray       # uint64 [T] packed table kmers (file order)
+    fids: np.ndarray       # uint32 [T]
+    n_fid: int
+    residues: np.ndarray   # uint8 ASCII, padded by 16 zero bytes
+    offsets: np.ndarray    # uint64 [n_seq + 1]
+    kinds: np.ndarray      # uint8 [n_seq]: 0 copy, 1 random, 2 chimera
+    true_fid: np.ndarray   # int32 [n_seq]: source function (-1 random)
+
+    @property
+    def n_seq(self) -> int:
+        return len(self.offsets) - 1
+
+    @property
+    def n_windows(self) -> int:
+        L = np.diff(self.offsets).astype(np.int64)
+        return int(np.maximum(L - 7, 0).sum())
+
+
+def _mutate(rng, prot: np.ndarray, rate: float) -> np.ndarray:
+    out = prot.copy()
+    m = rng.random(len(out)) < rate
+    out[m] = AA[rng.integers(0, 20, int(m.sum()))]
+    return out
+
+
+@dataclass
+class SignatureSet:
+    protos: list           # prototype proteins (uint8 ASCII), one per function
+    keys: np.ndarray       # uint64 [T] packed table kmers (file order)
+    fids: np.ndarray       # uint32 [T]
+    n_fid: int
+
+
+def make_table(table_size: int, n_fid: int, seed: int, k: int = 8) -> SignatureSet:
+    rng = np.random.default_rng(seed)
+    lens = cds_lengths()
+    plen = rng.choice(lens, n_fid)
+    protos = [AA[rng.integers(0, 20, int(L))] for L in plen]
+    pk = [np.unique(window_keys(p, k)) for p in protos]
+    all_k = np.concatenate(pk)
+    all_f = np.repeat(np.arange(n_fid, dtype=np.uint32), [len(x) for x in pk])
+    _, inv, cnt = np.unique(all_k, return_inverse=True, return_counts=True)
+    unique_mask = cnt[inv] == 1  # kmer occurs in exactly one function's prototype
+    all_k, all_f = all_k[unique_mask], all_f[unique_mask]
+    per_fn = max(1, table_size // n_fid)
+    # At most per_fn kmers per function (random subset), then decoys up to table_size.
+    order = rng.permutation(len(all_k))
+    all_k, all_f = all_k[order], all_f[order]
+    srt = np.argsort(all_f, kind="stable")
+    starts = np.searchsorted(all_f[srt], np.arange(n_fid))
+    rank = np.empty(len(all_k), np.int64)
+    rank[srt] = np.arange(len(all_k)) - starts[all_f[srt]]
+    keep = rank < per_fn
+    sig_k, sig_f = all_k[keep][:table_size], all_f[keep][:table_size]
+    n_decoy = table_size - len(sig_k)
+    dec = np.zeros(n_decoy, np.uint64)
+    for _ in range(k):
+        dec = (dec << np.uint64(5)) | AA_CODES[rng.integers(0, 20, n_decoy)]
+    dec_f = rng.integers(0, n_fid, n_decoy).astype(np.uint32)
+    keys = np.concatenate([sig_k, dec])
+    fids = np.concatenate([sig_f, dec_f]).astype(np.uint32)
+    perm = rng.permutation(len(keys))
+    return SignatureSet(protos, keys[perm], fids[perm], n_fid)
+
+
+def make_queries(sig: SignatureSet, n_seq: int, seed: int, mutation: float = 0.10):
+    """(residues padded by 16 bytes, offsets, kinds, true_fid) for one batch."""
+    rng = np.random.default_rng(seed)
+    lens = cds_lengths()
+    protos, n_fid = sig.protos, sig.n_fid
+    kinds = rng.choice(np.array([0, 1, 2], np.uint8), n_seq, p=[0.5, 0.4, 0.1])
+    true_fid = np.full(n_seq, -1, np.int32)
+    seqs = []
+    for i in range(n_seq):
+        if kinds[i] == 0:
+            f = int(rng.integers(0, n_fid))
+            true_fid[i] = f
+            seqs.append(_mutate(rng, protos[f], mutation))
+        elif kinds[i] == 1:
+            seqs.append(AA[rng.integers(0, 20, int(rng.choice(lens)))])
+        else:
+            a, b = rng.integers(0, n_fid, 2)
+            pa, pb = protos[int(a)], protos[int(b)]
+            true_fid[i] = int(a)
+            seqs.append(_mutate(rng, np.concatenate([pa[:len(pa) // 2], pb[len(pb) // 2:]]),
+                                mutation))
+    offsets = np.zeros(n_seq + 1, np.uint64)
+    offsets[1:] = np.cumsum([len(s) for s in seqs])
+    residues = np.concatenate(seqs + [np.zeros(16, np.uint8)])
+    return residues, offsets, kinds, true_fid
+
+
+def make_workload(n_seq: int, table_size: int, n_fid: int, seed: int, k: int = 8,
+                  mutation: float = 0.10, query_seed: int | None = None) -> Workload:
+    sig = make_table(table_size, n_fid, seed, k)
+    qs = seed * 1_000_003 + 17 if query_seed is None else query_seed
+    residues, offsets, kinds, true_fid = make_queries(sig, n_seq, qs, mutation)
+    return Workload(sig.keys, sig.fids, n_fid, residues, offsets, kinds, true_fid)
+
+
+# BASELINE.json configs -> (n_seq, table_size, n_fid, seed)
+CONFIGS = {
+    "c1": (100, 1_000, 100, 1),
+    "c2": (10_000, 10_000_000, 10_000, 2),
+    "c4": (1_000_000, 10_000_000, 10_000, 4),
+    "c5": (1_000_000, 100_000_000, 100_000, 5),
+}
+
+
+def random_contigs(total_bp: int, n_contig: int, seed: int, n_rate: float = 0.0005):
+    """Config 3 DNA: contig lengths log-uniform 50 kb..1 Mbp scaled to total_bp, GC 0.5,
+    n_rate ambiguous 'n' bases; lower-case like GTO contigs."""
+    rng = np.random.default_rng(seed)
+    raw = np.exp(rng.uniform(np.log(5e4), np.log(1e6), n_contig))
+    lens = np.maximum((raw / raw.sum() * total_bp).astype(np.int64), 100)
+    bases = np.frombuffer(b"acgt", np.uint8)
+    dna = bases[rng.integers(0, 4, int(lens.sum()))]
+    dna[rng.random(len(dna)) < n_rate] = ord("n")
+    offsets = np.zeros(n_contig + 1, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    return np.concatenate([dna, np.zeros(64, np.uint8)]), offsets

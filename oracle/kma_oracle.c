@@ -1,0 +1,400 @@
+/*
+ * kma_oracle.c — ORACLE (test infrastructure only; never shipped, never measured as the product).
+ *
+ * A scalar CPU restatement of the SEEDtk/kmers.anno signature-kmer annotation path, written
+ * from the Java sources (paths relative to /root/reference/src/main/java/org/theseed/) with
+ * String semantics kept literally: kmers are byte strings compared with memcmp, the signature
+ * table is a chained hash map with last-wins put, and a protein's kmers are a set of distinct
+ * substrings. It deliberately shares NO code with the product (no 5-bit packing, no bucketed
+ * table): it is the checker. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it.
+ *
+ * Parity status
+ *   - 6-frame extraction (orc_contig_kmers), peg kmers (orc_peg_kmers), Location math:
+ *     pinned against the reference's own test properties on src/test/small.gto
+ *     (test/.../anno/AppTest.java:69-161), re-expressed in tests/test_oracle_golden.py.
+ *   - apply vote (orc_apply) and ProteinKmers window semantics: PARITY UNPINNED. The Java
+ *     reference cannot run here (no JDK, no org.theseed jars) and no reference test exercises
+ *     ApplyKmerProcessor or ProteinKmers. This restatement is cross-checked against an
+ *     independent pure-Python restatement (oracle/oracle_py.py) and hand-built edge cases.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_F_END_EXCLUSIVE 0x1u
+#define ORC_F_MULTISET 0x2u
+
+/* ------------------------------------------------------------------------------------------ */
+/* HashMap<String,String> restated: chained buckets, Java String.hashCode + HashMap.hash spread */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct orc_node {
+  struct orc_node* next;
+  uint32_t hash;
+  int32_t value;
+  int32_t len;
+  char key[]; /* len bytes */
+} orc_node;
+
+typedef struct orc_table {
+  orc_node** buckets;
+  uint64_t mask;
+  uint64_t size;
+} orc_table;
+
+static uint32_t java_string_hash(const char* s, int len) {
+  uint32_t h = 0; /* String.hashCode: s[0]*31^(n-1) + ... */
+  for (int i = 0; i < len; i++) h = 31u * h + (uint8_t)s[i];
+  return h ^ (h >> 16); /* HashMap.hash spread */
+}
+
+static void orc_table_grow(orc_table* t) {
+  uint64_t nb = (t->mask + 1) * 2;
+  orc_node** b = (orc_node**)calloc(nb, sizeof(orc_node*));
+  for (uint64_t i = 0; i <= t->mask; i++) {
+    orc_node* n = t->buckets[i];
+    while (n) {
+      orc_node* nx = n->next;
+      uint64_t j = n->hash & (nb - 1);
+      n->next = b[j];
+      b[j] = n;
+      n = nx;
+    }
+  }
+  free(t->buckets);
+  t->buckets = b;
+  t->mask = nb - 1;
+}
+
+static void orc_table_put(orc_table* t, const char* key, int len, int32_t value) {
+  uint32_t h = java_string_hash(key, len);
+  for (orc_node* n = t->buckets[h & t->mask]; n; n = n->next)
+    if (n->hash == h && n->len == len && memcmp(n->key, key, (size_t)len) == 0) {
+      n->value = value; /* ApplyKmerProcessor.java:106: put -> the last row wins */
+      return;
+    }
+  orc_node* n = (orc_node*)malloc(sizeof(orc_node) + (size_t)len);
+  n->hash = h;
+  n->value = value;
+  n->len = len;
+  memcpy(n->key, key, (size_t)len);
+  n->next = t->buckets[h & t->mask];
+  t->buckets[h & t->mask] = n;
+  if (++t->size > (t->mask + 1) / 4 * 3) orc_table_grow(t);
+}
+
+/* Returns the value or -1 when absent (HashMap.get -> null). */
+int32_t orc_table_get(const orc_table* t, const char* key, int len) {
+  uint32_t h = java_string_hash(key, len);
+  for (orc_node* n = t->buckets[h & t->mask]; n; n = n->next)
+    if (n->hash == h && n->len == len && memcmp(n->key, key, (size_t)len) == 0) return n->value;
+  return -1;
+}
+
+/* ApplyKmerProcessor.java:101-107: every row of the headerless 2-column file is put, in file
+ * order; rows of any length are loaded (they simply never match a K-window). */
+orc_table* orc_table_new(const char* text, const uint64_t* offsets, const int32_t* values,
+                         uint64_t n) {
+  orc_table* t = (orc_table*)calloc(1, sizeof(orc_table));
+  uint64_t nb = 16;
+  while (nb < n / 2) nb <<= 1;
+  t->buckets = (orc_node**)calloc(nb, sizeof(orc_node*));
+  t->mask = nb - 1;
+  for (uint64_t r = 0; r < n; r++)
+    orc_table_put(t, text + offsets[r], (int)(offsets[r + 1] - offsets[r]), values[r]);
+  return t;
+}
+
+uint64_t orc_table_size(const orc_table* t) { return t->size; }
+
+void orc_table_free(orc_table* t) {
+  if (!t) return;
+  for (uint64_t i = 0; i <= t->mask; i++) {
+    orc_node* n = t->buckets[i];
+    while (n) {
+      orc_node* nx = n->next;
+      free(n);
+      n = nx;
+    }
+  }
+  free(t->buckets);
+  free(t);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* ProteinKmers(String) restated (external org.theseed.sequence, UNVERIFIED semantics):       */
+/* the set of distinct substrings s[i, i+K) for i = 0..L-K (inclusive end by default).        */
+/* Set elements are kept as window start indices in first-insertion order.                   */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int32_t* slots; /* open addressing over window starts, -1 empty */
+  uint32_t cap;
+  int32_t* order; /* distinct window starts, insertion order */
+  uint32_t n;
+} kmer_set;
+
+static void kmer_set_build(kmer_set* s, const char* p, int64_t L, int K, uint32_t flags) {
+  int64_t nwin = L - K + ((flags & ORC_F_END_EXCLUSIVE) ? 0 : 1);
+  s->n = 0;
+  if (nwin <= 0) return;
+  uint32_t cap = 16;
+  while (cap < (uint64_t)nwin * 2) cap <<= 1;
+  if (cap > s->cap) {
+    free(s->slots);
+    free(s->order);
+    s->slots = (int32_t*)malloc(sizeof(int32_t) * cap);
+    s->order = (int32_t*)malloc(sizeof(int32_t) * cap);
+    s->cap = cap;
+  }
+  for (uint32_t i = 0; i < cap; i++) s->slots[i] = -1;
+  for (int64_t i = 0; i < nwin; i++) {
+    if (flags & ORC_F_MULTISET) { /* every window counts: no set semantics */
+      s->order[s->n++] = (int32_t)i;
+      continue;
+    }
+    uint32_t h = java_string_hash(p + i, K) & (cap - 1);
+    for (;;) {
+      int32_t j = s->slots[h];
+      if (j < 0) {
+        s->slots[h] = (int32_t)i;
+        s->order[s->n++] = (int32_t)i;
+        break;
+      }
+      if (memcmp(p + j, p + i, (size_t)K) == 0) break; /* HashSet.add of an equal String */
+      h = (h + 1) & (cap - 1);
+    }
+  }
+}
+
+#define ORC_STATUS_NONE 0
+#define ORC_STATUS_CALLED 1
+#define ORC_STATUS_AMBIGUOUS 2
+#define ORC_STATUS_BELOW_MIN 3
+
+/* ApplyKmerProcessor.runCommand :122-147, literally: iterate the kmer set, probe the table,
+ * first hit sets the role, a confirming hit counts, a different role marks the peg bad and
+ * stops the loop; the feature is recorded iff role != null && !bad && count >= minHits. */
+void orc_apply(const orc_table* t, const uint8_t* residues, const uint64_t* offsets,
+               uint32_t n_seq, int K, int min_hits, uint32_t flags, int32_t* out_fid,
+               int32_t* out_count, uint8_t* out_status) {
+  kmer_set set = {0};
+  for (uint32_t s = 0; s < n_seq; s++) {
+    const char* p = (const char*)residues + offsets[s];
+    int64_t L = (int64_t)(offsets[s + 1] - offsets[s]);
+    kmer_set_build(&set, p, L, K, flags);
+    int32_t role = -1, count = 0;
+    int bad = 0;
+    for (uint32_t k = 0; k < set.n && !bad; k++) {
+      int32_t possible = orc_table_get(t, p + set.order[k], K);
+      if (possible >= 0) {
+        if (role < 0) {
+          role = possible;
+          count = 1;
+        } else if (possible == role) {
+          count++;
+        } else {
+          bad = 1;
+        }
+      }
+    }
+    if (role < 0) {
+      out_fid[s] = -1, out_count[s] = 0, out_status[s] = ORC_STATUS_NONE;
+    } else if (bad) {
+      out_fid[s] = -1, out_count[s] = 0, out_status[s] = ORC_STATUS_AMBIGUOUS;
+    } else {
+      out_fid[s] = role, out_count[s] = count;
+      out_status[s] = count >= min_hits ? ORC_STATUS_CALLED : ORC_STATUS_BELOW_MIN;
+    }
+  }
+  free(set.slots);
+  free(set.order);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* DnaTranslator restated (external org.theseed.proteins): codon -> amino acid by NCBI table,  */
+/* case-insensitive ACGT, any other base makes the codon 'X'.                                 */
+/* ------------------------------------------------------------------------------------------ */
+static int base_index(char c) { /* NCBI tables enumerate codons in T, C, A, G order */
+  switch (c) {
+    case 't': case 'T': case 'u': case 'U': return 0;
+    case 'c': case 'C': return 1;
+    case 'a': case 'A': return 2;
+    case 'g': case 'G': return 3;
+    default: return -1;
+  }
+}
+
+static const char* ncbi_table(int gcode) {
+  switch (gcode) {
+    case 1: case 11: return "FFLLSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 2: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSS**VVVVAAAADDEEGGGG";
+    case 3: return "FFLLSSSSYY**CCWWTTTTPPPPHHQQRRRRIIMMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 4: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 5: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSSSSVVVVAAAADDEEGGGG";
+    case 6: return "FFLLSSSSYYQQCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 9: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 10: return "FFLLSSSSYY**CCCWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 12: return "FFLLSSSSYY**CC*WLLLSPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 13: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNKKSSGGVVVVAAAADDEEGGGG";
+    case 14: return "FFLLSSSSYYY*CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 16: return "FFLLSSSSYY*LCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 21: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIMMTTTTNNNKSSSSVVVVAAAADDEEGGGG";
+    case 22: return "FFLLSS*SYY*LCC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 23: return "FF*LSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    case 24: return "FFLLSSSSYY**CCWWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSSKVVVVAAAADDEEGGGG";
+    case 25: return "FFLLSSSSYY**CCGWLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+    default: return 0;
+  }
+}
+
+/* translate(seq, frame, len): codons starting at 1-based `frame`, floor((len-frame+1)/3) aa. */
+int64_t orc_translate(const char* dna, int64_t len, int frame, int gcode, char* out) {
+  const char* tab = ncbi_table(gcode);
+  if (!tab) return -1;
+  int64_t n = 0;
+  for (int64_t p = frame - 1; p + 3 <= len; p += 3) {
+    int a = base_index(dna[p]), b = base_index(dna[p + 1]), c = base_index(dna[p + 2]);
+    out[n++] = (a < 0 || b < 0 || c < 0) ? 'X' : tab[a * 16 + b * 4 + c];
+  }
+  return n;
+}
+
+/* Contig.getRSequence restated: reverse complement (case kept, other bytes -> 'n'). */
+void orc_reverse_complement(const char* dna, int64_t len, char* out) {
+  for (int64_t i = 0; i < len; i++) {
+    char c = dna[len - 1 - i], r;
+    switch (c) {
+      case 'a': r = 't'; break; case 'c': r = 'g'; break;
+      case 'g': r = 'c'; break; case 't': r = 'a'; break;
+      case 'A': r = 'T'; break; case 'C': r = 'G'; break;
+      case 'G': r = 'C'; break; case 'T': r = 'A'; break;
+      default: r = 'n';
+    }
+    out[i] = r;
+  }
+}
+
+/* KmerReference.processKmers :180-203 for one strand, with KmerPosition.calcLeft :60-62 /
+ * :78-86. Records are appended while n < cap; the needed count is always returned. */
+static uint64_t process_strand(const char* seq, int64_t len, int minus, uint32_t contig,
+                               int gcode, int K, char* prot, char* out_kmers,
+                               uint32_t* out_contig, int32_t* out_left, uint8_t* out_strand,
+                               uint8_t* out_frame, uint64_t n, uint64_t cap) {
+  int64_t base = len - 3 * K + 2; /* KmerPosition.Minus: contigLen - kmerLen + 2 */
+  for (int frame = 1; frame <= 3; frame++) {
+    int64_t P = orc_translate(seq, len, frame, gcode, prot);
+    int64_t end = P - K; /* :186-187 the point past the last legal kmer start (exclusive) */
+    for (int64_t i = 0; i < end; i++) {
+      const char* km = prot + i;
+      int ok = 1;
+      for (int j = 0; j < K; j++)
+        if (km[j] == '*' || km[j] == 'X') { ok = 0; break; } /* :190 containsNone('*','X') */
+      if (!ok) continue;
+      int64_t left = minus ? base - (i * 3 + frame) : i * 3 + frame;
+      if (n < cap) {
+        if (out_kmers) memcpy(out_kmers + n * K, km, (size_t)K);
+        out_contig[n] = contig;
+        out_left[n] = (int32_t)left;
+        out_strand[n] = minus ? '-' : '+';
+        out_frame[n] = (uint8_t)frame;
+      }
+      n++;
+    }
+  }
+  return n;
+}
+
+/* KmerReference.getContigKmers :157-169 flattened to records (kmer, contig, left, strand,
+ * frame) in the reference's own visiting order: contig, + strand then - strand, frame 1..3,
+ * window i ascending. */
+uint64_t orc_contig_kmers(const uint8_t* dna, const uint64_t* offsets, uint32_t n_contig,
+                          int gcode, int K, char* out_kmers, uint32_t* out_contig,
+                          int32_t* out_left, uint8_t* out_strand, uint8_t* out_frame,
+                          uint64_t cap) {
+  uint64_t n = 0;
+  if (!ncbi_table(gcode)) return (uint64_t)-1;
+  for (uint32_t c = 0; c < n_contig; c++) {
+    const char* seq = (const char*)dna + offsets[c];
+    int64_t len = (int64_t)(offsets[c + 1] - offsets[c]);
+    char* rseq = (char*)malloc((size_t)len + 1);
+    char* prot = (char*)malloc((size_t)len / 3 + 2);
+    orc_reverse_complement(seq, len, rseq);
+    n = process_strand(seq, len, 0, c, gcode, K, prot, out_kmers, out_contig, out_left,
+                       out_strand, out_frame, n, cap);
+    n = process_strand(rseq, len, 1, c, gcode, K, prot, out_kmers, out_contig, out_left,
+                       out_strand, out_frame, n, cap);
+    free(rseq);
+    free(prot);
+  }
+  return n;
+}
+
+/* Signature-table probe of every 6-frame window (the DNA form of the apply lookup): returns
+ * (contig, left, strand, frame, fid) for windows whose kmer is in the table, sorted by
+ * (contig, left, strand '+' first). */
+typedef struct {
+  uint32_t contig;
+  int32_t left;
+  uint32_t fid;
+  uint8_t strand, frame;
+} orc_hit;
+
+static int hit_cmp(const void* a, const void* b) {
+  const orc_hit *x = (const orc_hit*)a, *y = (const orc_hit*)b;
+  if (x->contig != y->contig) return x->contig < y->contig ? -1 : 1;
+  if (x->left != y->left) return x->left < y->left ? -1 : 1;
+  return (int)x->strand - (int)y->strand; /* '+' (43) < '-' (45) */
+}
+
+uint64_t orc_annotate_contigs(const orc_table* t, const uint8_t* dna, const uint64_t* offsets,
+                              uint32_t n_contig, int gcode, int K, uint32_t* out_contig,
+                              int32_t* out_left, uint8_t* out_strand, uint8_t* out_frame,
+                              uint32_t* out_fid, uint64_t cap) {
+  uint64_t total = orc_contig_kmers(dna, offsets, n_contig, gcode, K, 0, 0, 0, 0, 0, 0);
+  if (total == (uint64_t)-1) return total;
+  char* km = (char*)malloc(total * (uint64_t)K + 1);
+  uint32_t* ct = (uint32_t*)malloc(sizeof(uint32_t) * (total + 1));
+  int32_t* lf = (int32_t*)malloc(sizeof(int32_t) * (total + 1));
+  uint8_t* st = (uint8_t*)malloc(total + 1);
+  uint8_t* fr = (uint8_t*)malloc(total + 1);
+  orc_contig_kmers(dna, offsets, n_contig, gcode, K, km, ct, lf, st, fr, total);
+  orc_hit* hits = (orc_hit*)malloc(sizeof(orc_hit) * (total + 1));
+  uint64_t nh = 0;
+  for (uint64_t r = 0; r < total; r++) {
+    int32_t v = orc_table_get(t, km + r * K, K);
+    if (v < 0) continue;
+    orc_hit h = {ct[r], lf[r], (uint32_t)v, st[r], fr[r]};
+    hits[nh++] = h;
+  }
+  qsort(hits, nh, sizeof(orc_hit), hit_cmp);
+  for (uint64_t i = 0; i < nh && i < cap; i++) {
+    out_contig[i] = hits[i].contig;
+    out_left[i] = hits[i].left;
+    out_strand[i] = hits[i].strand;
+    out_frame[i] = hits[i].frame;
+    out_fid[i] = hits[i].fid;
+  }
+  free(km), free(ct), free(lf), free(st), free(fr), free(hits);
+  return nh;
+}
+
+/* KmerReference.countPegKmers :124-147: windows i < L-K (end exclusive), skipping kmers that
+ * contain 'X'; location begin = i + 1 on the peg. Records in visiting order. */
+uint64_t orc_peg_kmers(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq, int K,
+                       char* out_kmers, uint32_t* out_peg, int32_t* out_left, uint64_t cap) {
+  uint64_t n = 0;
+  for (uint32_t s = 0; s < n_seq; s++) {
+    const char* p = (const char*)residues + offsets[s];
+    int64_t end = (int64_t)(offsets[s + 1] - offsets[s]) - K;
+    for (int64_t i = 0; i < end; i++) {
+      if (memchr(p + i, 'X', (size_t)K)) continue;
+      if (n < cap) {
+        if (out_kmers) memcpy(out_kmers + n * K, p + i, (size_t)K);
+        out_peg[n] = s;
+        out_left[n] = (int32_t)(i + 1);
+      }
+      n++;
+    }
+  }
+  return n;
+}

@@ -1,0 +1,121 @@
+"""ORACLE twin (test infrastructure only): a pure-Python restatement of the reference path.
+
+Written independently of oracle/kma_oracle.c to cross-check it: Python ``str`` / ``dict`` /
+``set`` stand in for Java ``String`` / ``HashMap`` / ``HashSet``, and the genetic code is built
+from an amino-acid -> codons listing rather than the NCBI 64-character strings the C oracle
+uses. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import it.
+Use it on small inputs only (pure-Python loops).
+
+Citations are relative to /root/reference/src/main/java/org/theseed/.
+Parity status: see oracle/kma_oracle.c (6-frame + peg extraction pinned by AppTest
+properties on small.gto; the apply vote and ProteinKmers semantics are parity unpinned).
+"""
+
+from __future__ import annotations
+
+STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN = 0, 1, 2, 3
+
+# Standard code by amino acid (NCBI table 1 / 11).
+_STANDARD = {
+    "A": "GCT GCC GCA GCG", "R": "CGT CGC CGA CGG AGA AGG", "N": "AAT AAC",
+    "D": "GAT GAC", "C": "TGT TGC", "Q": "CAA CAG", "E": "GAA GAG",
+    "G": "GGT GGC GGA GGG", "H": "CAT CAC", "I": "ATT ATC ATA", "L": "TTA TTG CTT CTC CTA CTG",
+    "K": "AAA AAG", "M": "ATG", "F": "TTT TTC", "P": "CCT CCC CCA CCG",
+    "S": "TCT TCC TCA TCG AGT AGC", "T": "ACT ACC ACA ACG", "W": "TGG", "Y": "TAT TAC",
+    "V": "GTT GTC GTA GTG", "*": "TAA TAG TGA",
+}
+_DIFFS = {1: {}, 11: {}, 4: {"TGA": "W"}, 25: {"TGA": "G"}}
+
+
+def codon_table(gcode: int) -> dict:
+    if gcode not in _DIFFS:
+        raise ValueError(f"genetic code {gcode} not in the Python twin")
+    tab = {c: aa for aa, cs in _STANDARD.items() for c in cs.split()}
+    tab.update(_DIFFS[gcode])
+    return tab
+
+
+def translate(dna: str, frame: int, gcode: int) -> str:
+    """DnaTranslator.translate(seq, frame, len(seq)) (external; KmerReference.java:184)."""
+    tab = codon_table(gcode)
+    up = dna.upper().replace("U", "T")
+    return "".join(tab.get(up[p:p + 3], "X") for p in range(frame - 1, len(up) - 2, 3))
+
+
+def reverse_complement(dna: str) -> str:
+    """Contig.getRSequence (external; KmerReference.java:166)."""
+    comp = {"a": "t", "c": "g", "g": "c", "t": "a", "A": "T", "C": "G", "G": "C", "T": "A"}
+    return "".join(comp.get(c, "n") for c in reversed(dna))
+
+
+def protein_kmers(prot: str, k: int = 8, end_exclusive: bool = False, multiset: bool = False):
+    """ProteinKmers(String) (external; ApplyKmerProcessor.java:123), UNVERIFIED semantics:
+    distinct substrings prot[i:i+k] for i in 0..len-k (inclusive unless end_exclusive)."""
+    n = len(prot) - k + (0 if end_exclusive else 1)
+    wins = [prot[i:i + k] for i in range(max(n, 0))]
+    return wins if multiset else list(dict.fromkeys(wins))
+
+
+def load_table(rows):
+    """ApplyKmerProcessor.java:101-107: HashMap.put per row, the last row wins."""
+    table = {}
+    for kmer, role in rows:
+        table[kmer] = role
+    return table
+
+
+def apply_protein(table: dict, prot: str, min_hits: int = 5, k: int = 8,
+                  end_exclusive: bool = False, multiset: bool = False):
+    """ApplyKmerProcessor.java:122-147 -> (status, role or None, count)."""
+    role, count, bad = None, 0, False
+    for kmer in protein_kmers(prot, k, end_exclusive, multiset):
+        possible = table.get(kmer)
+        if possible is None:
+            continue
+        if role is None:
+            role, count = possible, 1
+        elif possible == role:
+            count += 1
+        else:
+            bad = True
+            break
+    if role is None:
+        return STATUS_NONE, None, 0
+    if bad:
+        return STATUS_AMBIGUOUS, None, 0
+    return (STATUS_CALLED if count >= min_hits else STATUS_BELOW_MIN), role, count
+
+
+def contig_kmers(contigs, gcode: int = 11, k: int = 8):
+    """KmerReference.getContigKmers / processKmers (KmerReference.java:157-203) with
+    KmerPosition.calcLeft (KmerPosition.java:60-62, 78-86). Yields
+    (kmer, contig_index, left, strand, frame) in the reference's visiting order."""
+    for ci, seq in enumerate(contigs):
+        n = len(seq)
+        for strand, s in (("+", seq), ("-", reverse_complement(seq))):
+            base = n - 3 * k + 2
+            for frame in (1, 2, 3):
+                prot = translate(s, frame, gcode)
+                for i in range(len(prot) - k):
+                    km = prot[i:i + k]
+                    if "*" in km or "X" in km:
+                        continue
+                    left = i * 3 + frame if strand == "+" else base - (i * 3 + frame)
+                    yield km, ci, left, strand, frame
+
+
+def annotate_contigs(table: dict, contigs, gcode: int = 11, k: int = 8):
+    """Every 6-frame window probed in the table; hits sorted (contig, left, '+' first)."""
+    hits = [(ci, left, strand, frame, table[km])
+            for km, ci, left, strand, frame in contig_kmers(contigs, gcode, k) if km in table]
+    hits.sort(key=lambda h: (h[0], h[1], h[2]))
+    return hits
+
+
+def peg_kmers(prots, k: int = 8):
+    """KmerReference.countPegKmers (KmerReference.java:124-147): windows i < len-k, no 'X'."""
+    for pi, p in enumerate(prots):
+        for i in range(len(p) - k):
+            km = p[i:i + k]
+            if "X" not in km:
+                yield km, pi, i + 1

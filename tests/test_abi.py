@@ -1,0 +1,48 @@
+"""The C-ABI library loads and exports every symbol include/kmeranno.h declares (CPU only:
+no compute calls; only the pure host helpers are exercised)."""
+import os
+import re
+
+import numpy as np
+
+from conftest import ROOT
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "kmeranno.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kma_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    import kmeranno
+    assert header_functions() == sorted(kmeranno.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(native_lib):
+    for name in header_functions():
+        assert hasattr(native_lib, name), name
+
+
+def test_abi_version_and_error_string(native_lib):
+    assert native_lib.kma_abi_version() == 1
+    assert isinstance(native_lib.kma_last_error(), bytes)
+
+
+def test_bucket_sizing_host_helper(native_lib):
+    import kmeranno
+    assert kmeranno.buckets_for(1000, 0.5) == 250        # 2000 slots / 8
+    assert kmeranno.buckets_for(10**8, 0.75) * 8 >= 10**8 / 0.75
+    assert kmeranno.buckets_for(0, 0.5) == 1
+
+
+def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
+    """kma_contig_window_count = sum over strands/frames of max(0, P_f - K) (processKmers)."""
+    import kmeranno
+    contigs = [c["dna"] for c in small_gto["contigs"]]
+    _, off = kmeranno.pack_strings(contigs)
+    assert kmeranno.contig_window_count(off, 8) == 1_537_176
+    for L in range(0, 40):
+        o = np.array([0, L], np.uint64)
+        expect = sum(2 * max(0, (L - f + 1) // 3 - 8) for f in (1, 2, 3))
+        assert kmeranno.contig_window_count(o, 8) == expect, L
