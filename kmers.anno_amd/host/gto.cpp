@@ -1,0 +1,329 @@
+// gto.cpp — see gto.h.
+#include "gto.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <unordered_map>
+
+namespace kma_host {
+
+const Json* Json::get(const std::string& key) const {
+  if (kind != Object) return nullptr;
+  for (const auto& kv : obj)
+    if (kv.first == key) return &kv.second;
+  return nullptr;
+}
+
+std::string Json::as_string(const std::string& dflt) const {
+  if (kind == String) return str;
+  if (kind == Number) {
+    std::ostringstream o;
+    o << (long long)num;
+    return o.str();
+  }
+  return dflt;
+}
+
+long long Json::as_int(long long dflt) const {
+  if (kind == Number) return (long long)num;
+  if (kind == String && !str.empty()) return std::strtoll(str.c_str(), nullptr, 10);
+  return dflt;
+}
+
+namespace {
+
+struct Parser {
+  const char* p;
+  const char* begin;
+  const char* end;
+  [[noreturn]] void error(const char* what) {
+    throw std::runtime_error(std::string("JSON parse error at byte ") +
+                             std::to_string(p - begin) + ": " + what);
+  }
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  static void put_utf8(std::string& s, uint32_t cp) {
+    if (cp < 0x80) {
+      s += (char)cp;
+    } else if (cp < 0x800) {
+      s += (char)(0xC0 | (cp >> 6));
+      s += (char)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      s += (char)(0xE0 | (cp >> 12));
+      s += (char)(0x80 | ((cp >> 6) & 0x3F));
+      s += (char)(0x80 | (cp & 0x3F));
+    } else {
+      s += (char)(0xF0 | (cp >> 18));
+      s += (char)(0x80 | ((cp >> 12) & 0x3F));
+      s += (char)(0x80 | ((cp >> 6) & 0x3F));
+      s += (char)(0x80 | (cp & 0x3F));
+    }
+  }
+  uint32_t hex4() {
+    if (end - p < 4) error("short \\u escape");
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+      char c = *p++;
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else error("bad \\u escape");
+    }
+    return v;
+  }
+  std::string string() {
+    if (*p != '"') error("expected string");
+    ++p;
+    std::string s;
+    for (;;) {
+      const char* q = p;
+      while (q < end && *q != '"' && *q != '\\') ++q;
+      s.append(p, q);
+      p = q;
+      if (p >= end) error("unterminated string");
+      if (*p == '"') {
+        ++p;
+        return s;
+      }
+      ++p;  // backslash
+      if (p >= end) error("bad escape");
+      char c = *p++;
+      switch (c) {
+        case '"': s += '"'; break;
+        case '\\': s += '\\'; break;
+        case '/': s += '/'; break;
+        case 'b': s += '\b'; break;
+        case 'f': s += '\f'; break;
+        case 'n': s += '\n'; break;
+        case 'r': s += '\r'; break;
+        case 't': s += '\t'; break;
+        case 'u': {
+          uint32_t cp = hex4();
+          if (cp >= 0xD800 && cp < 0xDC00 && end - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            p += 2;
+            uint32_t lo = hex4();
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          }
+          put_utf8(s, cp);
+          break;
+        }
+        default: error("bad escape");
+      }
+    }
+  }
+  Json value() {
+    ws();
+    if (p >= end) error("unexpected end");
+    Json v;
+    switch (*p) {
+      case '{': {
+        ++p;
+        v.kind = Json::Object;
+        ws();
+        if (p < end && *p == '}') {
+          ++p;
+          return v;
+        }
+        for (;;) {
+          ws();
+          std::string k = string();
+          ws();
+          if (p >= end || *p != ':') error("expected ':'");
+          ++p;
+          v.obj.emplace_back(std::move(k), value());
+          ws();
+          if (p < end && *p == ',') {
+            ++p;
+            continue;
+          }
+          if (p < end && *p == '}') {
+            ++p;
+            return v;
+          }
+          error("expected ',' or '}'");
+        }
+      }
+      case '[': {
+        ++p;
+        v.kind = Json::Array;
+        ws();
+        if (p < end && *p == ']') {
+          ++p;
+          return v;
+        }
+        for (;;) {
+          v.arr.push_back(value());
+          ws();
+          if (p < end && *p == ',') {
+            ++p;
+            continue;
+          }
+          if (p < end && *p == ']') {
+            ++p;
+            return v;
+          }
+          error("expected ',' or ']'");
+        }
+      }
+      case '"':
+        v.kind = Json::String;
+        v.str = string();
+        return v;
+      case 't':
+        if (end - p >= 4 && !std::strncmp(p, "true", 4)) {
+          p += 4;
+          v.kind = Json::Bool;
+          v.b = true;
+          return v;
+        }
+        error("bad literal");
+      case 'f':
+        if (end - p >= 5 && !std::strncmp(p, "false", 5)) {
+          p += 5;
+          v.kind = Json::Bool;
+          return v;
+        }
+        error("bad literal");
+      case 'n':
+        if (end - p >= 4 && !std::strncmp(p, "null", 4)) {
+          p += 4;
+          return v;
+        }
+        error("bad literal");
+      default: {
+        char* q = nullptr;
+        v.num = std::strtod(p, &q);
+        if (q == p) error("bad value");
+        p = q;
+        v.kind = Json::Number;
+        return v;
+      }
+    }
+  }
+};
+
+std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  std::ostringstream o;
+  o << f.rdbuf();
+  return o.str();
+}
+
+}  // namespace
+
+Json parse_json(const std::string& text) {
+  Parser ps{text.data(), text.data(), text.data() + text.size()};
+  Json v = ps.value();
+  ps.ws();
+  if (ps.p != ps.end) ps.error("trailing characters");
+  return v;
+}
+
+std::vector<const Feature*> Genome::pegs() const {
+  std::vector<const Feature*> out;
+  for (const auto& f : features)
+    if (f.is_peg()) out.push_back(&f);
+  return out;
+}
+
+Genome load_genome(const std::string& path) {
+  Json j = parse_json(slurp(path));
+  Genome g;
+  if (const Json* v = j.get("id")) g.id = v->as_string();
+  if (const Json* v = j.get("scientific_name")) g.name = v->as_string();
+  if (const Json* v = j.get("genetic_code")) g.genetic_code = (int)v->as_int(11);
+  if (const Json* cs = j.get("contigs"))
+    for (const Json& c : cs->arr) {
+      Contig ct;
+      if (const Json* v = c.get("id")) ct.id = v->as_string();
+      if (const Json* v = c.get("dna")) ct.dna = v->as_string();
+      g.contigs.push_back(std::move(ct));
+    }
+  if (const Json* fs = j.get("features"))
+    for (const Json& f : fs->arr) {
+      Feature ft;
+      if (const Json* v = f.get("id")) ft.id = v->as_string();
+      if (const Json* v = f.get("type")) ft.type = v->as_string();
+      if (const Json* v = f.get("function")) ft.function = v->as_string();
+      if (const Json* v = f.get("protein_translation")) ft.protein = v->as_string();
+      g.features.push_back(std::move(ft));
+    }
+  return g;
+}
+
+std::vector<std::string> genome_files(const std::string& dir) {
+  std::vector<std::string> out;
+  DIR* d = opendir(dir.c_str());
+  if (!d) throw std::runtime_error("cannot list " + dir);
+  while (dirent* e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n.size() > 4 && n.compare(n.size() - 4, 4, ".gto") == 0) out.push_back(dir + "/" + n);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+KmerRows read_kmer_db(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  KmerRows r;
+  r.offsets.push_back(0);
+  std::unordered_map<std::string, uint32_t> role_ids;
+  std::string line;
+  while (std::getline(f, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    const size_t tab = line.find('\t');
+    const std::string kmer = line.substr(0, tab);
+    std::string role;
+    if (tab != std::string::npos) {
+      const size_t tab2 = line.find('\t', tab + 1);
+      role = line.substr(tab + 1, tab2 == std::string::npos ? std::string::npos : tab2 - tab - 1);
+    }
+    auto it = role_ids.find(role);
+    if (it == role_ids.end()) {
+      it = role_ids.emplace(role, (uint32_t)r.roles.size()).first;
+      r.roles.push_back(role);
+    }
+    r.text += kmer;
+    r.offsets.push_back(r.text.size());
+    r.fids.push_back(it->second);
+    r.last_kmer = kmer;
+  }
+  return r;
+}
+
+std::map<std::string, int> read_roles(const std::string& path, int* n_lines) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  std::map<std::string, int> idx;
+  std::string line;
+  int i = 1;
+  while (std::getline(f, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    idx[line.substr(0, line.find('\t'))] = i++;  // StringUtils.substringBefore(line, "\t")
+  }
+  if (n_lines) *n_lines = i - 1;
+  return idx;
+}
+
+bool is_directory(const std::string& path) {
+  struct stat st;
+  return stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+bool can_read(const std::string& path) {
+  struct stat st;
+  return stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode) && access(path.c_str(), R_OK) == 0;
+}
+
+}  // namespace kma_host
