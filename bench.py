@@ -28,6 +28,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "kmers.anno_amd", "python")]
 import kmeranno  # noqa: E402
+from kmeranno import dist as kdist  # noqa: E402
 from kmeranno import synth  # noqa: E402
 
 K = 8
@@ -138,10 +139,11 @@ def main():
             f"max probe {st[2]}, built in {tb.elapsed_time(te):.1f} ms")
         del winner, keys, fids
     if world > 1:
-        dist.broadcast(slots, src=0)
+        kdist.broadcast_table(slots, src=0)  # RCCL over xGMI
         torch.cuda.synchronize()
     table = kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, local)
-    ws = kmeranno.Workspace(local)
+    n_res = int(offsets[-1] - offsets[0])
+    ws = kmeranno.Workspace(local, n_res)
 
     d_res = torch.from_numpy(residues).to(dev)
     d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
@@ -152,7 +154,7 @@ def main():
 
     def step():
         kmeranno.annotate_proteins_device(table, ws, d_res.data_ptr(), d_off.data_ptr(), n_seq,
-                                          MIN_HITS, 0, d_fid.data_ptr(), d_cnt.data_ptr(),
+                                          n_res, MIN_HITS, 0, d_fid.data_ptr(), d_cnt.data_ptr(),
                                           d_st.data_ptr(), d_tally.data_ptr(), n_fid, sp)
 
     for _ in range(args.warmup):
@@ -170,7 +172,7 @@ def main():
         step()
         ev[i][1].record(stream)
     if world > 1:
-        dist.reduce(d_tally, dst=0)  # per-function tallies of the whole job -> rank 0
+        kdist.reduce_tallies(d_tally, dst=0)  # per-function tallies of the whole job -> rank 0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -151,8 +151,11 @@ int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device,
 /* Raw view of the slot array (device pointer) — what an RCCL broadcast moves.               */
 int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes);
 
-/* ---- workspaces ----------------------------------------------------------------------------- */
+/* ---- workspaces -----------------------------------------------------------------------------
+ * Per-stream scratch of the _device entry points. kma_workspace_reserve sizes it for calls of
+ * up to n_residues residues (4 bytes per residue of HBM); it is the only call that allocates. */
 int kma_workspace_create(int device, kma_workspace** out);
+int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_destroy(kma_workspace* ws);
 
 /* ---- protein annotation (ApplyKmerProcessor.java:118-148) ----------------------------------
@@ -164,14 +167,16 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                           uint32_t* out_tally, uint32_t n_fid);
-/* Device form: every pointer is device memory on the table's device; `d_residues` must be
- * readable for 16 bytes past offsets[n_seq]; d_tally (n_fid u32) is accumulated into, not
+/* Device form: every pointer is device memory on the table's device; `d_residues` is 8-byte
+ * aligned and readable for 16 bytes past offsets[n_seq]; n_residues = offsets[n_seq] -
+ * offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is accumulated into, not
  * cleared. Asynchronous on `stream`.                                                          */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
-                                 uint32_t n_seq, int min_hits, uint32_t flags, int32_t* d_fid,
-                                 int32_t* d_count, uint8_t* d_status, uint32_t* d_tally,
-                                 uint32_t n_fid, void* stream);
+                                 uint32_t n_seq, uint64_t n_residues, int min_hits,
+                                 uint32_t flags, int32_t* d_fid, int32_t* d_count,
+                                 uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
+                                 void* stream);
 
 /* ---- 6-frame contig annotation (KmerReference.java:157-203 + table probe) -----------------
  * dna: contigs concatenated (any case; bases other than ACGT translate to 'X'); offsets as

@@ -29,8 +29,11 @@ struct kma_table {
 
 struct kma_workspace {
   int device = 0;
+  int n_cu = 256;
   uint32_t* d_flag = nullptr;
-  uint32_t* d_scratch = nullptr;
+  uint64_t* d_scratch = nullptr;
+  uint32_t* d_hits = nullptr;  // K1 words: one u32 per residue position
+  uint64_t hits_cap = 0;
 };
 
 namespace {
@@ -176,14 +179,19 @@ int make_table_object(int device, int k, uint64_t n_buckets, uint64_t* d_slots, 
   return KMA_OK;
 }
 
+constexpr uint64_t kMaxBuckets = 1ull << 29;  // slot index and bucket index stay 32-bit
+
 int build_on_device(uint64_t* d_slots, uint64_t n_buckets, uint32_t* d_winner,
                     const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, uint32_t* d_status,
                     hipStream_t s) {
+  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than 2^29 buckets");
   KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * 64, s));
   KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::kSlotsPerBucket * sizeof(uint32_t), s));
   KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
-  KMA_HIP(kma::launch_build_insert(d_slots, d_winner, n_buckets, d_keys, n, d_status, s));
-  KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, n_buckets, d_status + 1, s));
+  KMA_HIP(kma::launch_build_insert(d_slots, d_winner, (uint32_t)n_buckets, d_keys, n, d_status,
+                                   s));
+  KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, (uint32_t)n_buckets,
+                                     d_status + 1, s));
   return KMA_OK;
 }
 
@@ -197,7 +205,7 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
     if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^24-1",
                                             fids[r], (unsigned long long)r);
   const uint64_t nb = kma_table_buckets_for(n, lf);
-  if (nb * kma::kSlotsPerBucket >= 0xFFFFFFFFull)
+  if (nb > kMaxBuckets)
     return fail(KMA_E_INVALID, "table too large: %llu buckets", (unsigned long long)nb);
   DeviceScope ds(device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
@@ -337,6 +345,7 @@ int kma_table_build_device(void* d_slots, uint64_t n_buckets, uint32_t* d_winner
 
 int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device, kma_table** out) {
   if (!d_slots || !out || !n_buckets) return fail(KMA_E_INVALID, "null argument");
+  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than 2^29 buckets");
   if (int rc = check_k(k)) return rc;
   DeviceScope ds(device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
@@ -358,9 +367,13 @@ int kma_workspace_create(int device, kma_workspace** out) {
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
   kma_workspace* w = new kma_workspace();
   w->device = device;
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      n_cu > 0)
+    w->n_cu = n_cu;
   hipError_t e = hipMalloc(&w->d_flag, 16);
   if (e == hipSuccess)
-    e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 4);
+    e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 8);
   if (e != hipSuccess) {
     if (w->d_flag) (void)hipFree(w->d_flag);
     delete w;
@@ -370,18 +383,32 @@ int kma_workspace_create(int device, kma_workspace** out) {
   return KMA_OK;
 }
 
+int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  if (n_residues <= ws->hits_cap) return KMA_OK;
+  DeviceScope ds(ws->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
+  if (ws->d_hits) (void)hipFree(ws->d_hits);
+  ws->d_hits = nullptr;
+  ws->hits_cap = 0;
+  KMA_HIP(hipMalloc(&ws->d_hits, n_residues * 4));
+  ws->hits_cap = n_residues;
+  return KMA_OK;
+}
+
 int kma_workspace_destroy(kma_workspace* ws) {
   if (!ws) return KMA_OK;
   DeviceScope ds(ws->device);
   (void)hipFree(ws->d_flag);
   (void)hipFree(ws->d_scratch);
+  if (ws->d_hits) (void)hipFree(ws->d_hits);
   delete ws;
   return KMA_OK;
 }
 
 int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const uint8_t* d_residues,
-                                 const uint64_t* d_offsets, uint32_t n_seq, int min_hits,
-                                 uint32_t flags, int32_t* d_fid, int32_t* d_count,
+                                 const uint64_t* d_offsets, uint32_t n_seq, uint64_t n_residues,
+                                 int min_hits, uint32_t flags, int32_t* d_fid, int32_t* d_count,
                                  uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
                                  void* stream) {
   if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
@@ -392,17 +419,21 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   if (!d_residues || !d_offsets || !d_fid || !d_count || !d_status)
     return fail(KMA_E_INVALID, "null device buffer");
   if ((uintptr_t)d_residues & 7) return fail(KMA_E_INVALID, "residues must be 8-byte aligned");
+  if (n_residues > ws->hits_cap)
+    return fail(KMA_E_CAPACITY, "workspace reserved for %llu residues, call needs %llu",
+                (unsigned long long)ws->hits_cap, (unsigned long long)n_residues);
   hipStream_t s = static_cast<hipStream_t>(stream);
   DeviceScope ds(t->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
   KMA_HIP(hipMemsetAsync(ws->d_flag, 0, 4, s));
   kma::ProteinArgs a{};
   a.slots = t->d_slots;
-  a.n_buckets = t->n_buckets;
+  a.n_buckets = (uint32_t)t->n_buckets;
   a.lut = t->d_lut;
   a.residues = d_residues;
   a.offsets = d_offsets;
   a.n_seq = n_seq;
+  a.n_residues = n_residues;
   a.k = t->k;
   a.min_hits = min_hits;
   a.flags = flags;
@@ -411,9 +442,10 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   a.out_status = d_status;
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
+  a.hits = ws->d_hits;
   a.overflow_flag = ws->d_flag;
   a.scratch = ws->d_scratch;
-  KMA_HIP(kma::launch_proteins(a, s));
+  KMA_HIP(kma::launch_proteins(a, ws->n_cu, s));
   return KMA_OK;
 }
 
@@ -452,8 +484,10 @@ int kma_annotate_proteins(const kma_table* t, const uint8_t* residues, const uin
   }
   kma_workspace* ws = nullptr;
   if (int rc = kma_workspace_create(t->device, &ws)) return rc;
-  int rc = kma_annotate_proteins_device(t, ws, d_res, d_off, n_seq, min_hits, flags, d_fid, d_cnt,
-                                        d_st, d_tally, d_tally ? n_fid : 0, nullptr);
+  int rc = kma_workspace_reserve(ws, nres);
+  if (rc == KMA_OK)
+    rc = kma_annotate_proteins_device(t, ws, d_res, d_off, n_seq, nres, min_hits, flags, d_fid,
+                                      d_cnt, d_st, d_tally, d_tally ? n_fid : 0, nullptr);
   hipError_t e = rc == KMA_OK ? hipDeviceSynchronize() : hipSuccess;
   kma_workspace_destroy(ws);
   if (rc != KMA_OK) return rc;
@@ -517,7 +551,7 @@ int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t*
   }
   kma::ContigArgs a{};
   a.slots = t->d_slots;
-  a.n_buckets = t->n_buckets;
+  a.n_buckets = (uint32_t)t->n_buckets;
   a.dna = d_dna;
   a.offsets = d_off;
   a.n_contig = n_contig;

@@ -8,39 +8,43 @@
 namespace kma {
 
 // ---- signature-table layout in HBM ------------------------------------------------------------
-// n_buckets x 64-byte buckets; each bucket = 8 slots of u64 (key << 24 | fid); slot 0 = empty.
-// A key lives in its home bucket or, if that is full, in the next buckets (linear bucket probing,
-// wrapping). Lookups stop at the first bucket holding the key or an empty slot.
+// n_buckets x 64-byte buckets (n_buckets < 2^29); each bucket = 8 slots of one u64:
+//   low dword  = key bits 0..31            (never 0 for a valid key: codes are 1..31)
+//   high dword = key bits 32..39 << 24 | fid (24 bits)
+// An all-zero slot is empty. A key lives in its home bucket or, if that is full, in the next
+// buckets (linear bucket probing, wrapping). Lookups stop at the first bucket holding the key or
+// an empty slot. Every compare is a 32-bit operation.
 constexpr int kSlotsPerBucket = 8;
-constexpr int kFidBits = 24;
-constexpr uint64_t kFidMask = (1ull << kFidBits) - 1;
+constexpr uint32_t kFidMask = (1u << 24) - 1;
 
-__host__ __device__ inline uint64_t mix64(uint64_t k) {  // murmur3 fmix64 finaliser
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdull;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ull;
-  k ^= k >> 33;
-  return k;
+__host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
+  return ((uint64_t)((uint32_t)(key >> 32) << 24 | (fid & kFidMask)) << 32) | (uint32_t)key;
+}
+__host__ __device__ inline uint64_t slot_key(uint64_t slot) {
+  return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
 }
 
-__host__ __device__ inline uint64_t home_bucket(uint64_t key, uint64_t n_buckets) {
-  // Lemire fast range: high 64 bits of mix(key) * n_buckets, any n_buckets (no power of two).
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __umul64hi(mix64(key), n_buckets);
-#else
-  return (uint64_t)(((unsigned __int128)mix64(key) * n_buckets) >> 64);
-#endif
+// Home bucket: a 32-bit mix of the <= 40-bit key (murmur3 fmix32 over both halves), mapped to
+// [0, n_buckets) by a multiply-high (Lemire fast range).
+__host__ __device__ inline uint32_t home_bucket(uint64_t key, uint32_t n_buckets) {
+  uint32_t h = (uint32_t)key * 0x9E3779B1u ^ ((uint32_t)(key >> 32) + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
 }
 
 // ---- kernel parameter blocks ------------------------------------------------------------------
 struct ProteinArgs {
   const uint64_t* slots;
-  uint64_t n_buckets;
+  uint32_t n_buckets;
   const uint8_t* lut;  // 256-byte residue -> 5-bit code table (device)
   const uint8_t* residues;
   const uint64_t* offsets;
   uint32_t n_seq;
+  uint64_t n_residues;  // offsets[n_seq] - offsets[0]
   int32_t k;
   int32_t min_hits;
   uint32_t flags;
@@ -49,23 +53,31 @@ struct ProteinArgs {
   uint8_t* out_status;
   uint32_t* tally;  // may be null
   uint32_t n_fid;
+  uint32_t* hits;           // workspace: fid + 1 (0 = miss) per residue position
   uint32_t* overflow_flag;  // workspace: set when a protein needs the global dedupe pass
-  uint32_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u32
+  uint64_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u64
 };
 
-// Per-wave LDS dedupe set of hit slot ids (u32, 0 = empty): capacity and the distinct-hit
-// count at which a protein is deferred to the global-memory pass.
+// K1 probe kernel: kProbeWin windows per thread per step, all first-bucket loads in flight.
+constexpr int kProbeWin = 4;
+constexpr int kProbeBlocksPerCU = 8;
+// K2 vote kernel: one wave per protein, kVoteWin words per lane per step, kVoteWaves waves per
+// block sharing an LDS pool of kVotePool u64 set entries. Proteins whose set does not fit are
+// finished by vote_long_kernel: one block each, an LDS set of kLongSet keys, else kFallbackCap
+// keys of workspace scratch per block.
 constexpr int kWavesPerBlock = 4;
-constexpr int kSetCap = 2048;
-constexpr int kSetLimit = 1536;
+constexpr int kVoteWin = 4;
+constexpr int kVoteWaves = 8;
+constexpr int kVotePool = 4096;
+constexpr int kLongSet = 8192;
 constexpr uint8_t kStatusPending = 0xFF;
-// Global-memory dedupe pass for proteins with more than kSetLimit distinct hits.
+constexpr int kLongBlocksPerCU = 4;
 constexpr int kFallbackBlocks = 64;
-constexpr uint32_t kFallbackCap = 1u << 18;  // u32 entries per block (1 MiB)
+constexpr uint32_t kFallbackCap = 1u << 17;  // u64 entries per block (1 MiB)
 
 struct ContigArgs {
   const uint64_t* slots;
-  uint64_t n_buckets;
+  uint32_t n_buckets;
   const uint8_t* dna;
   const uint64_t* offsets;
   uint32_t n_contig;
@@ -80,12 +92,12 @@ struct ContigArgs {
 constexpr int kContigTile = 256;  // forward positions per block
 
 // ---- launchers (kma_kernels.hip) --------------------------------------------------------------
-hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint64_t n_buckets,
+hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets,
                                const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream);
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
-                                 uint64_t n_buckets, uint32_t* stats, hipStream_t stream);
-hipError_t launch_proteins(const ProteinArgs& a, hipStream_t stream);
+                                 uint32_t n_buckets, uint32_t* stats, hipStream_t stream);
+hipError_t launch_proteins(const ProteinArgs& a, int n_cu, hipStream_t stream);
 hipError_t launch_contigs(const ContigArgs& a, uint64_t n_blocks, const uint64_t* d_prefix,
                           uint8_t* out_hits, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,

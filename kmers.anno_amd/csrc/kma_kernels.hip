@@ -1,18 +1,22 @@
 // kma_kernels.hip — CDNA4 (gfx950) kernels of the signature-kmer annotation hot path.
 //
 //   build_insert / build_finalize  signature-table construction (ApplyKmerProcessor.java:100-110)
-//   proteins_kernel                ProteinKmers extraction + table probe + vote, one wave per
-//                                  protein (ApplyKmerProcessor.java:122-147)
-//   proteins_fallback_kernel       the same vote with a global-memory dedupe set for proteins
-//                                  whose distinct hits overflow the per-wave LDS set
-//   contigs_probe_kernel           6-frame translation + window + probe
-//                                  (KmerReference.java:157-203, KmerPosition.java:50-93)
-//   contigs_emit_kernel            canonical-order hit emission after a block-count scan
+//   probe_kernel       K1: every residue position's K-window packed and probed in the table
+//                      (the HashMap.get of ApplyKmerProcessor.java:130 for every kmer of every
+//                      protein); writes fid + 1 (0 = miss) per position. HBM random access.
+//   vote_kernel        K2: one wave per protein: ProteinKmers set semantics (distinct kmers,
+//                      org.theseed.sequence.ProteinKmers at :123) + the first/confirm/conflict
+//                      vote and min-hits threshold (:129-147) over K1's words.
+//   vote_long_kernel   K2 for long proteins: one block per protein.
+//   contigs_probe_kernel  6-frame translation + window + probe
+//                      (KmerReference.java:157-203, KmerPosition.java:50-93)
+//   contigs_emit_kernel   canonical-order hit emission after a block-count scan
 //
 // Integer / byte work only: the bound is HBM (or Infinity-Cache) random access to 64-byte
-// buckets, not MFMA. Every wave keeps one bucket load per lane in flight per chunk of 64
-// windows; all per-protein state lives in registers and a wave-private LDS set.
+// buckets, not MFMA.
 #include <hipcub/hipcub.hpp>
+
+#include <cstdlib>
 
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
@@ -41,52 +45,79 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// The K residues of the window starting at absolute byte `pos`, as one little-endian u64
-// (byte j = residue j). Two aligned 8-byte loads + a funnel shift: consecutive lanes read
-// consecutive words, so a wave's 64 windows coalesce into two or three 64-byte lines.
+// The residues of the window starting at byte `pos` as one little-endian u64 (byte j = residue
+// j). Two aligned 8-byte loads + a funnel shift: consecutive lanes read consecutive words.
+__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
+  return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+}
 __device__ __forceinline__ uint64_t window_bytes(const uint8_t* __restrict__ res, uint64_t pos) {
   const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
-  const uint64_t lo = src[0], hi = src[1];
-  const uint32_t sh = (uint32_t)(pos & 7) * 8u;
-  return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+  return funnel(src[0], src[1], (uint32_t)(pos & 7) * 8u);
+}
+// The two aligned words of a window, combined later (funnel) so that the load is not consumed
+// in the step that issues it.
+struct WinWords {
+  uint64_t lo, hi;
+  uint32_t sh;
+};
+__device__ __forceinline__ WinWords window_words(const uint8_t* __restrict__ res, uint64_t pos) {
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
+  return WinWords{src[0], src[1], (uint32_t)(pos & 7) * 8u};
 }
 
 // 5-bit packing through the table's residue LUT (LDS); false if a byte is not encodable.
-__device__ __forceinline__ bool pack_window(const uint8_t* lut, uint64_t bytes, int k,
-                                           uint64_t& key) {
-  bool ok = true;
+template <int K>
+__device__ __forceinline__ bool pack_window(const uint8_t* lut, uint64_t bytes, uint64_t& key) {
+  uint32_t c[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) c[j] = lut[(uint32_t)(bytes >> (8 * j)) & 0xFFu];
   uint64_t v = 0;
-  for (int j = 0; j < k; ++j) {
-    const uint32_t c = lut[(bytes >> (8 * j)) & 0xFFu];
-    ok = ok && (c != 0u);
-    v = (v << 5) | c;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    ok = ok && c[j] != 0u;
+    v = (v << 5) | c[j];
   }
   key = v;
   return ok;
 }
 
-// Probe the bucketized table. Returns true on a hit with the fid and the global slot id.
-__device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint64_t n_buckets,
-                                      uint64_t key, uint32_t& fid, uint32_t& sid) {
-  uint64_t b = home_bucket(key, n_buckets);
-  for (uint64_t step = 0; step < n_buckets; ++step) {  // bounded even for a full foreign table
-    const uint4* bp = reinterpret_cast<const uint4*>(slots + b * kSlotsPerBucket);
-    const uint4 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
-    const uint64_t s[8] = {
-        ((uint64_t)q0.y << 32) | q0.x, ((uint64_t)q0.w << 32) | q0.z,
-        ((uint64_t)q1.y << 32) | q1.x, ((uint64_t)q1.w << 32) | q1.z,
-        ((uint64_t)q2.y << 32) | q2.x, ((uint64_t)q2.w << 32) | q2.z,
-        ((uint64_t)q3.y << 32) | q3.x, ((uint64_t)q3.w << 32) | q3.z};
-    bool hit = false, empty = false;
+// Scan one 64-byte bucket held in registers for `key`: hit (+ fid, slot index) / empty slot seen.
+__device__ __forceinline__ void scan_bucket(const uint4 (&q)[4], uint64_t key, bool& hit,
+                                            bool& empty, uint32_t& fid, uint32_t& slot) {
+  const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32) << 24;
+  const uint32_t lo[8] = {q[0].x, q[0].z, q[1].x, q[1].z, q[2].x, q[2].z, q[3].x, q[3].z};
+  const uint32_t hi[8] = {q[0].y, q[0].w, q[1].y, q[1].w, q[2].y, q[2].w, q[3].y, q[3].w};
+  hit = false;
+  empty = false;
 #pragma unroll
-    for (int j = 0; j < kSlotsPerBucket; ++j) {
-      if ((s[j] >> kFidBits) == key) {
-        hit = true;
-        fid = (uint32_t)(s[j] & kFidMask);
-        sid = (uint32_t)(b * kSlotsPerBucket + j);
-      }
-      empty |= (s[j] == 0);
-    }
+  for (int j = 0; j < kSlotsPerBucket; ++j) {
+    const bool m = lo[j] == klo && (hi[j] & ~kFidMask) == khi;
+    fid = m ? (hi[j] & kFidMask) : fid;
+    slot = m ? (uint32_t)j : slot;
+    hit = hit || m;
+    empty = empty || lo[j] == 0u;
+  }
+}
+
+__device__ __forceinline__ void load_bucket(const uint64_t* __restrict__ slots, uint32_t b,
+                                            uint4 (&q)[4]) {
+  const uint4* bp = reinterpret_cast<const uint4*>(slots + (uint64_t)b * kSlotsPerBucket);
+  q[0] = bp[0];
+  q[1] = bp[1];
+  q[2] = bp[2];
+  q[3] = bp[3];
+}
+
+// Full probe from the home bucket (chains included). Returns true on a hit.
+__device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint32_t n_buckets,
+                                      uint64_t key, uint32_t& fid) {
+  uint32_t b = home_bucket(key, n_buckets), slot = 0;
+  for (uint32_t step = 0; step < n_buckets; ++step) {  // bounded even for a full foreign table
+    uint4 q[4];
+    load_bucket(slots, b, q);
+    bool hit, empty;
+    scan_bucket(q, key, hit, empty, fid, slot);
     if (hit) return true;
     if (empty) return false;
     b = (b + 1 == n_buckets) ? 0 : b + 1;
@@ -96,31 +127,31 @@ __device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint64
 
 // ---------------------------------------------------------------------------------------------
 // Table construction. Insert: claim the first empty slot of the probe chain with a 64-bit CAS
-// (slot = key << 24, fid still 0) or find the key already there; either way record the row
-// index with atomicMax so the LAST row of a duplicate key wins (HashMap.put semantics).
+// (slot key bits, fid still 0) or find the key already there; either way record the row index
+// with atomicMax so the LAST row of a duplicate key wins (HashMap.put semantics).
 // Finalize: write the winning row's fid into the slot; collect entry count and max probe.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint32_t* winner,
-                                                           uint64_t n_buckets,
+                                                           uint32_t n_buckets,
                                                            const uint64_t* __restrict__ keys,
                                                            uint64_t n, uint32_t* status) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     if (key == 0) continue;
-    const uint64_t want = key << kFidBits;
-    uint64_t b = home_bucket(key, n_buckets);
+    const uint64_t want = slot_make(key, 0);
+    uint32_t b = home_bucket(key, n_buckets);
     bool done = false;
-    for (uint64_t p = 0; p < n_buckets && !done; ++p) {
+    for (uint32_t p = 0; p < n_buckets && !done; ++p) {
       for (int j = 0; j < kSlotsPerBucket; ++j) {
-        uint64_t* sp = slots + b * kSlotsPerBucket + j;
+        uint64_t* sp = slots + (uint64_t)b * kSlotsPerBucket + j;
         uint64_t v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v == 0) {
           const uint64_t old = atomicCAS((unsigned long long*)sp, 0ull, want);
           v = old == 0 ? want : old;
         }
-        if ((v >> kFidBits) == key) {
-          atomicMax(winner + b * kSlotsPerBucket + j, (uint32_t)(i + 1));
+        if (slot_key(v) == key) {
+          atomicMax(winner + (uint64_t)b * kSlotsPerBucket + j, (uint32_t)(i + 1));
           done = true;
           break;
         }
@@ -134,17 +165,17 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
 __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
                                                              const uint32_t* __restrict__ winner,
                                                              const uint32_t* __restrict__ fids,
-                                                             uint64_t n_buckets, uint32_t* stats) {
-  const uint64_t n_slots = n_buckets * kSlotsPerBucket;
+                                                             uint32_t n_buckets, uint32_t* stats) {
+  const uint64_t n_slots = (uint64_t)n_buckets * kSlotsPerBucket;
   uint32_t entries = 0, max_probe = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_slots;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t w = winner[i];
     if (w == 0) continue;
     const uint64_t v = slots[i];
-    slots[i] = v | ((uint64_t)fids[w - 1] & kFidMask);
-    const uint64_t b = i / kSlotsPerBucket, h = home_bucket(v >> kFidBits, n_buckets);
-    const uint32_t d = (uint32_t)((b + n_buckets - h) % n_buckets) + 1u;
+    slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
+    const uint32_t b = (uint32_t)(i / kSlotsPerBucket), h = home_bucket(slot_key(v), n_buckets);
+    const uint32_t d = (b >= h ? b - h : b + n_buckets - h) + 1u;
     entries++;
     max_probe = max(max_probe, d);
   }
@@ -157,94 +188,342 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Protein annotation: one wave per protein, 64 windows per step (lane = window).
-// Vote state per lane: min fid, max fid, distinct-hit count; the protein is CALLED iff the
-// wave-wide min == max (one role only) and the distinct count >= min_hits. Distinct counting
-// (ProteinKmers is a set) inserts each hit's slot id into a wave-private LDS open-addressing
-// set; a protein whose distinct hits would exceed kSetLimit is marked pending and finished by
-// proteins_fallback_kernel with a global-memory set.
+// K1 — probe. Residue positions g of [offsets[0], offsets[n_seq]) in grid-stride steps of
+// 256 x U; each thread issues its U windows' residue loads, then packs and issues all U
+// first-bucket loads (U x 64 B in flight per lane) before consuming any; overflow chains (a full
+// home bucket) are walked afterwards. Windows that straddle two proteins are probed too (their
+// words are never read): K1 needs no protein boundaries, no LDS set and no barrier.
+// Residue loads are unconditional (a lane past the end re-reads position 0) so that no loaded
+// register is merged on a branch join, which would force a vmcnt(0) per load.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void proteins_kernel(ProteinArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t set_mem[kWavesPerBlock * kSetCap];
+template <int K, int U>
+__global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  lut[tid] = a.lut[tid];
-  uint32_t* set = set_mem + wave * kSetCap;
-  uint4* set4 = reinterpret_cast<uint4*>(set);
-#pragma unroll
-  for (int i = lane; i < kSetCap / 4; i += 64) set4[i] = make_uint4(0u, 0u, 0u, 0u);
+  const int t = threadIdx.x;
+  lut[t] = a.lut[t];
   __syncthreads();
-
-  const uint32_t s = blockIdx.x * kWavesPerBlock + wave;
-  if (s >= a.n_seq) return;
-  const uint64_t beg = a.offsets[s];
-  const int64_t len = (int64_t)(a.offsets[s + 1] - beg);
-  const int k = a.k;
-  const int64_t n_win = len - k + ((a.flags & KMA_F_END_EXCLUSIVE) ? 0 : 1);
-  const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
-
-  uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, cnt = 0u;
-  uint32_t total = 0u;  // wave-uniform: distinct entries in the LDS set
-  bool ambiguous = false, overflow = false;
-  for (int64_t w0 = 0; w0 < n_win; w0 += 64) {
-    if (!multiset && !ambiguous && total + 64u > (uint32_t)kSetLimit) {
-      overflow = true;
-      break;
+  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint8_t* __restrict__ res = a.residues + a.offsets[0];
+  const uint64_t* __restrict__ slots = a.slots;
+  const uint32_t nb = a.n_buckets;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * (256 * U); g0 < n_pos;
+       g0 += (uint64_t)gridDim.x * (256 * U)) {
+    uint64_t bytes[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t g = g0 + j * 256 + t;
+      bytes[j] = window_bytes(res, g < n_pos ? g : 0);
     }
-    const int64_t w = w0 + lane;
-    uint64_t key = 0;
-    bool ok = w < n_win;
-    if (ok) ok = pack_window(lut, window_bytes(a.residues, beg + (uint64_t)w), k, key);
-    uint32_t fid = 0u, sid = 0u;
-    const bool hit = ok && probe(a.slots, a.n_buckets, key, fid, sid);
-    if (hit) {
-      fmin = min(fmin, fid);
-      fmax = max(fmax, fid);
+    uint64_t key[U];
+    uint32_t bk[U];
+    bool ok[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      ok[j] = pack_window<K>(lut, bytes[j], key[j]) && g0 + j * 256 + t < n_pos;
+      bk[j] = home_bucket(key[j], nb);
     }
-    if (multiset) {
-      cnt += hit ? 1u : 0u;
-    } else if (!ambiguous) {
-      bool fresh = false;
-      if (hit) {
-        const uint32_t id = sid + 1u;
-        uint32_t h = (id * 0x9E3779B1u) >> (32 - 11);  // kSetCap = 2^11
-        for (;;) {
-          const uint32_t old = atomicCAS(set + h, 0u, id);
-          if (old == 0u) {
-            fresh = true;
-            break;
-          }
-          if (old == id) break;
-          h = (h + 1u) & (kSetCap - 1);
+    uint4 q[U][4];  // undefined on lanes that do not probe: consumed unconditionally below
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (ok[j]) load_bucket(slots, bk[j], q[j]);
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      bool hit, empty;
+      uint32_t fid = 0, slot = 0;
+      scan_bucket(q[j], key[j], hit, empty, fid, slot);
+      hit = ok[j] && hit;
+      if (ok[j] && !hit && !empty) {  // rare: walk the chain past a full home bucket
+        uint32_t b = bk[j];
+        for (uint32_t step = 1; step < nb && !hit && !empty; ++step) {
+          b = (b + 1 == nb) ? 0 : b + 1;
+          uint4 qq[4];
+          load_bucket(slots, b, qq);
+          scan_bucket(qq, key[j], hit, empty, fid, slot);
         }
       }
-      cnt += fresh ? 1u : 0u;
-      total += (uint32_t)__popcll(__ballot(fresh));
-      const uint32_t wmin = wave_min(fmin), wmax = wave_max(fmax);
-      ambiguous = wmin != 0xFFFFFFFFu && wmin != wmax;
+      const uint64_t g = g0 + j * 256 + t;
+      if (g < n_pos) a.hits[g] = hit ? fid + 1u : 0u;
     }
   }
-  const uint32_t wmin = wave_min(fmin), wmax = wave_max(fmax), wcnt = wave_sum(cnt);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1, quad-cooperative form. Each lane packs the key of its own windows, then the four lanes
+// of a quad probe their four windows' buckets together: for the window of quad lane r, lane p
+// loads bytes [16p, 16p + 16) of the bucket (one dwordx4), so one wave instruction reads 16
+// whole 64-byte lines (the access shape with the higher measured random-gather rate, and 4x
+// fewer VGPRs per probe than a lane reading a whole bucket). Matches are combined with DPP
+// quad reductions and kept by the window's owner lane. Overflow chains (rare) are walked by
+// the owner lane alone.
+// ---------------------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, R * 0x55, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t quad_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  return max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+}
+
+template <int K, int U>
+__global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
+  __shared__ uint8_t lut[256];
+  const int t = threadIdx.x, part = t & 3;
+  lut[t] = a.lut[t];
+  __syncthreads();
+  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint8_t* __restrict__ res = a.residues + a.offsets[0];
+  const uint64_t* __restrict__ slots = a.slots;
+  const uint32_t nb = a.n_buckets;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const uint64_t stride = (uint64_t)gridDim.x * (256 * U);
+  // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
+  // flight, so a wave's only exposed latency per step is the bucket gather.
+  uint64_t g0 = (uint64_t)blockIdx.x * (256 * U);
+  WinWords ww[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t g = g0 + j * 256 + t;
+    ww[j] = window_words(res, g < n_pos ? g : 0);
+  }
+  for (; g0 < n_pos; g0 += stride) {
+    uint32_t klo[U], khi[U], bk[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      uint64_t key;
+      const bool ok = pack_window<K>(lut, funnel(ww[j].lo, ww[j].hi, ww[j].sh), key) &&
+                      g0 + j * 256 + t < n_pos;
+      klo[j] = (uint32_t)key;
+      khi[j] = (uint32_t)(key >> 32) << 24;
+      bk[j] = ok ? home_bucket(key, nb) : kNone;
+    }
+    // Cooperative loads: all 4U dwordx4 of the lane in flight before any compare. A window
+    // that does not probe reads bucket 0 (its result is discarded): no branch-merged loads.
+    uint4 q[U][4];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint32_t b0 = quad_bcast<0>(bk[j]), b1 = quad_bcast<1>(bk[j]);
+      const uint32_t b2 = quad_bcast<2>(bk[j]), b3 = quad_bcast<3>(bk[j]);
+      const uint4* base = reinterpret_cast<const uint4*>(slots) + part;
+      q[j][0] = base[(uint64_t)(b0 == kNone ? 0u : b0) * 4];
+      q[j][1] = base[(uint64_t)(b1 == kNone ? 0u : b1) * 4];
+      q[j][2] = base[(uint64_t)(b2 == kNone ? 0u : b2) * 4];
+      q[j][3] = base[(uint64_t)(b3 == kNone ? 0u : b3) * 4];
+    }
+    // Next step's residues (issued after the bucket loads: waiting for those leaves these in
+    // flight, vmcnt counts in order).
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t g = g0 + stride + j * 256 + t;
+      ww[j] = window_words(res, g < n_pos ? g : 0);
+    }
+    uint32_t word[U], full[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      word[j] = 0;
+      full[j] = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t kl = r == 0 ? quad_bcast<0>(klo[j]) : r == 1 ? quad_bcast<1>(klo[j])
+                          : r == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
+        const uint32_t kh = r == 0 ? quad_bcast<0>(khi[j]) : r == 1 ? quad_bcast<1>(khi[j])
+                          : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
+        // Branch-free on purpose: a short-circuit here lets the compiler split the 16-byte
+        // load into a lazily loaded tail behind a branch and a vmcnt(0).
+        const uint4 v = q[j][r];
+        const uint32_t m0 = (uint32_t)(v.x == kl) & (uint32_t)((v.y & ~kFidMask) == kh);
+        const uint32_t m1 = (uint32_t)(v.z == kl) & (uint32_t)((v.w & ~kFidMask) == kh);
+        uint32_t w = (m0 * ((v.y & kFidMask) + 1u)) | (m1 * ((v.w & kFidMask) + 1u));
+        uint32_t f = (uint32_t)(v.x != 0u) & (uint32_t)(v.z != 0u);  // no empty slot here
+        w = quad_max(w);
+        f = 1u - quad_max(1u - f);  // quad min: 1 iff the whole bucket is full
+        word[j] = part == r ? w : word[j];
+        full[j] = part == r ? f : full[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t g = g0 + j * 256 + t;
+      if (bk[j] != kNone && word[j] == 0u && full[j]) {  // rare: chain past a full home bucket
+        const uint64_t key = ((uint64_t)(khi[j] >> 24) << 32) | klo[j];
+        uint32_t b = bk[j], fid = 0, slot = 0;
+        bool hit = false, empty = false;
+        for (uint32_t step = 1; step < nb && !hit && !empty; ++step) {
+          b = (b + 1 == nb) ? 0 : b + 1;
+          uint4 qq[4];
+          load_bucket(slots, b, qq);
+          scan_bucket(qq, key, hit, empty, fid, slot);
+        }
+        word[j] = hit ? fid + 1u : 0u;
+      }
+      if (g < n_pos) a.hits[g] = bk[j] != kNone ? word[j] : 0u;
+    }
+  }
+}
+
+// Open-addressing set of distinct hit keys (u64, 0 = empty) in LDS or global memory, capacity a
+// power of two at least twice the keys it can receive. Returns true if newly inserted.
+__device__ __forceinline__ uint32_t set_hash(uint64_t key) {
+  return (uint32_t)key * 0x9E3779B1u ^ (uint32_t)(key >> 32) * 0x85EBCA77u;
+}
+__device__ __forceinline__ bool set_insert(unsigned long long* set, uint32_t mask, uint64_t key) {
+  uint32_t h = set_hash(key) & mask;
+  for (;;) {
+    const unsigned long long old = atomicCAS(set + h, 0ull, (unsigned long long)key);
+    if (old == 0ull) return true;
+    if (old == key) return false;
+    h = (h + 1u) & mask;
+  }
+}
+
+__device__ __forceinline__ void write_vote(const ProteinArgs& a, uint32_t s, uint32_t mn,
+                                           uint32_t mx, uint32_t cnt) {
+  int32_t fid_out = -1, cnt_out = 0;
+  uint8_t st;
+  if (mn == 0xFFFFFFFFu) {
+    st = KMA_STATUS_NONE;  // roleId == null
+  } else if (mn != mx) {
+    st = KMA_STATUS_AMBIGUOUS;  // badPeg
+  } else {
+    fid_out = (int32_t)mn;
+    cnt_out = (int32_t)cnt;
+    st = cnt >= (uint32_t)a.min_hits ? KMA_STATUS_CALLED : KMA_STATUS_BELOW_MIN;
+    if (st == KMA_STATUS_CALLED && a.tally && mn < a.n_fid) atomicAdd(a.tally + mn, 1u);
+  }
+  a.out_fid[s] = fid_out;
+  a.out_count[s] = cnt_out;
+  a.out_status[s] = st;
+}
+
+__device__ __forceinline__ int64_t n_windows(const ProteinArgs& a, uint32_t s, int k) {
+  return (int64_t)(a.offsets[s + 1] - a.offsets[s]) - k +
+         ((a.flags & KMA_F_END_EXCLUSIVE) ? 0 : 1);
+}
+
+// The vote over a window range held by one thread group: V words and V residue windows per
+// lane per step, all loaded before any is consumed (clamped addresses, no branch-merged loads).
+// Hit keys are re-packed from the residues and inserted in `set` unless multiset.
+template <int K, int V, int STRIDE>
+__device__ __forceinline__ void vote_range(const ProteinArgs& a, const uint8_t* lut,
+                                           const uint32_t* __restrict__ words,
+                                           const uint8_t* __restrict__ res, int64_t n_win,
+                                           int64_t first, unsigned long long* set, uint32_t mask,
+                                           bool multiset, uint32_t& fmin, uint32_t& fmax,
+                                           uint32_t& cnt) {
+  for (int64_t w0 = first; w0 < n_win; w0 += (int64_t)STRIDE * V) {
+    uint32_t h[V];
+    uint64_t bytes[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int64_t w = w0 + v * STRIDE;
+      const int64_t wc = w < n_win ? w : n_win - 1;
+      const uint32_t x = words[wc];
+      bytes[v] = window_bytes(res, (uint64_t)wc);
+      h[v] = w < n_win ? x : 0u;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (h[v]) {
+        fmin = min(fmin, h[v] - 1u);
+        fmax = max(fmax, h[v] - 1u);
+        if (multiset) {
+          cnt++;
+        } else {
+          uint64_t key;
+          pack_window<K>(lut, bytes[v], key);
+          cnt += set_insert(set, mask, key) ? 1u : 0u;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 — vote. One wave per protein; kVoteWaves waves per block share an LDS pool of kVotePool
+// u64 set entries (small static LDS per wave keeps 32 waves per CU resident).
+//   pass 1: the protein's K1 words (kVoteWin per lane per step) -> min fid, max fid, hits H.
+//           No hit -> NONE; two roles -> AMBIGUOUS (badPeg): no set needed; multiset -> H.
+//   pass 2: one role and H >= 2: a set of >= 2H entries taken from the pool; each hit window's
+//           key is re-packed from the residues and inserted, so a kmer occurring twice in one
+//           protein counts once (ProteinKmers is a set). The residues and words of a protein
+//           that fits one step are still in registers from pass 1.
+// A protein whose set does not fit the pool's free space is marked pending for
+// vote_long_kernel.
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(64 * kVoteWaves, 8) void vote_kernel(ProteinArgs a) {
+  constexpr int V = kVoteWin;
+  __shared__ __attribute__((aligned(16))) unsigned long long pool[kVotePool];
+  __shared__ uint32_t pool_top;
+  __shared__ uint8_t lut[256];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < 256) lut[tid] = a.lut[tid];
+  if (tid == 0) pool_top = 0;
+  __syncthreads();
+  const uint32_t s = blockIdx.x * kVoteWaves + wave;
+  if (s >= a.n_seq) return;
+  const int64_t n_win = n_windows(a, s, K);
+  const uint64_t beg = a.offsets[s];
+  const uint32_t* __restrict__ words = a.hits + (beg - a.offsets[0]);
+  const uint8_t* __restrict__ res = a.residues + beg;
+  const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  // ---- pass 1 ----------------------------------------------------------------------------------
+  uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, hits = 0u;
+  uint32_t h[V];
+  uint64_t bytes[V];
+  for (int64_t w0 = 0; w0 < n_win; w0 += 64 * V) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int64_t w = w0 + v * 64 + lane;
+      const int64_t wc = w < n_win ? w : n_win - 1;
+      const uint32_t x = words[wc];
+      bytes[v] = window_bytes(res, (uint64_t)wc);
+      h[v] = w < n_win ? x : 0u;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      if (h[v]) {
+        fmin = min(fmin, h[v] - 1u);
+        fmax = max(fmax, h[v] - 1u);
+        hits++;
+      }
+  }
+  const uint32_t wmin = wave_min(fmin), wmax = wave_max(fmax), wh = wave_sum(hits);
+  if (wmin == 0xFFFFFFFFu || wmin != wmax || multiset || wh < 2) {
+    if (lane == 0) write_vote(a, s, wmin, wmax, wh);
+    return;
+  }
+  // ---- pass 2: distinct hit keys -----------------------------------------------------------
+  uint32_t cap = 64;
+  while (cap < 2 * wh) cap <<= 1;
+  uint32_t base = 0;
   if (lane == 0) {
-    int32_t fid_out = -1, cnt_out = 0;
-    uint8_t st;
-    if (wmin == 0xFFFFFFFFu) {
-      st = KMA_STATUS_NONE;
-    } else if (wmin != wmax) {
-      st = KMA_STATUS_AMBIGUOUS;
-    } else if (overflow) {
-      st = kStatusPending;
+    base = atomicAdd(&pool_top, cap);
+    if (base + cap > (uint32_t)kVotePool) {
+      a.out_status[s] = kStatusPending;
       atomicOr(a.overflow_flag, 1u);
-    } else {
-      fid_out = (int32_t)wmin;
-      cnt_out = (int32_t)wcnt;
-      st = wcnt >= (uint32_t)a.min_hits ? KMA_STATUS_CALLED : KMA_STATUS_BELOW_MIN;
-      if (st == KMA_STATUS_CALLED && a.tally && wmin < a.n_fid) atomicAdd(a.tally + wmin, 1u);
     }
-    a.out_fid[s] = fid_out;
-    a.out_count[s] = cnt_out;
-    a.out_status[s] = st;
   }
+  base = __shfl(base, 0, 64);
+  if (base + cap > (uint32_t)kVotePool) return;  // wave-uniform
+  unsigned long long* set = pool + base;
+  uint4* s4 = reinterpret_cast<uint4*>(set);
+  for (uint32_t i = lane; i < cap / 2; i += 64) s4[i] = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t cnt = 0;
+  if (n_win <= 64 * V) {  // single step: words and residues still in registers
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      if (h[v]) {
+        uint64_t key;
+        pack_window<K>(lut, bytes[v], key);
+        cnt += set_insert(set, cap - 1, key) ? 1u : 0u;
+      }
+  } else {
+    uint32_t m0 = 0xFFFFFFFFu, m1 = 0u;
+    vote_range<K, V, 64>(a, lut, words, res, n_win, lane, set, cap - 1, false, m0, m1, cnt);
+  }
+  cnt = wave_sum(cnt);
+  if (lane == 0) write_vote(a, s, wmin, wmax, cnt);
 }
 
 __device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* red, int op) {
@@ -260,70 +539,95 @@ __device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* red, int 
   return r;
 }
 
-__global__ __launch_bounds__(256) void proteins_fallback_kernel(ProteinArgs a) {
+// K2 for the pending (long) proteins: one block per protein, grid-striding over the statuses.
+// Proteins of up to kLongSet / 2 windows keep their distinct-key set in LDS; longer ones are
+// taken by the first kFallbackBlocks blocks with a set in their slice of workspace scratch
+// (kFallbackCap u64); longer still are TOO_LONG.
+template <int K>
+__device__ void vote_long_one(const ProteinArgs& a, const uint8_t* lut, uint32_t s, int64_t n_win,
+                              unsigned long long* set, uint32_t cap, uint32_t* red) {
+  const int tid = threadIdx.x;
+  const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  if (!multiset)
+    for (uint32_t i = tid; i < cap; i += blockDim.x) set[i] = 0ull;
+  __syncthreads();
+  const uint64_t beg = a.offsets[s];
+  uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, cnt = 0u;
+  vote_range<K, kVoteWin, 256>(a, lut, a.hits + (beg - a.offsets[0]), a.residues + beg, n_win,
+                               tid, set, cap - 1, multiset, fmin, fmax, cnt);
+  fmin = block_reduce(fmin, red, 0);
+  fmax = block_reduce(fmax, red, 1);
+  cnt = block_reduce(cnt, red, 2);
+  if (tid == 0) write_vote(a, s, fmin, fmax, cnt);
+  __syncthreads();  // the set is reused by the next protein
+}
+
+// Block-cooperative scan of statuses [s0, s0 + 256): the pending proteins whose window count
+// satisfies `want`, compacted into `list` (returns their number). One status load per thread.
+template <class Want>
+__device__ __forceinline__ uint32_t scan_pending(const ProteinArgs& a, uint32_t s0, Want want,
+                                                 uint32_t* list, uint32_t* wave_cnt) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const uint32_t s = s0 + tid;
+  const bool p = s < a.n_seq && a.out_status[s] == kStatusPending && want(s);
+  const uint64_t m = __ballot(p);
+  __syncthreads();  // list / wave_cnt are reused across chunks
+  if ((tid & 63) == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t base = 0, total = 0;
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    base += w < wave ? wave_cnt[w] : 0u;
+    total += wave_cnt[w];
+  }
+  if (p) list[base + popc_below(m)] = s;
+  __syncthreads();
+  return total;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void vote_long_kernel(ProteinArgs a) {
   if (__hip_atomic_load(a.overflow_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     return;
+  __shared__ __attribute__((aligned(16))) unsigned long long lds_set[kLongSet];
   __shared__ uint8_t lut[256];
-  __shared__ uint32_t red[kWavesPerBlock];
+  __shared__ uint32_t red[kWavesPerBlock], wave_cnt[kWavesPerBlock], list[256];
   const int tid = threadIdx.x;
   lut[tid] = a.lut[tid];
   __syncthreads();
-  uint32_t* set = a.scratch + (uint64_t)blockIdx.x * kFallbackCap;
-  const int k = a.k;
-  for (uint32_t s = blockIdx.x; s < a.n_seq; s += gridDim.x) {
-    if (a.out_status[s] != kStatusPending) continue;  // block-uniform
-    const uint64_t beg = a.offsets[s];
-    const int64_t len = (int64_t)(a.offsets[s + 1] - beg);
-    const int64_t n_win = len - k + ((a.flags & KMA_F_END_EXCLUSIVE) ? 0 : 1);
-    if (n_win > (int64_t)(kFallbackCap / 2)) {
-      if (tid == 0) {
-        a.out_fid[s] = -1;
-        a.out_count[s] = 0;
-        a.out_status[s] = KMA_STATUS_TOO_LONG;
-      }
-      continue;
+  // Proteins of up to kLongSet / 2 windows: LDS set; chunks of 256 statuses per block.
+  for (uint32_t s0 = blockIdx.x * 256u; s0 < a.n_seq; s0 += gridDim.x * 256u) {
+    const uint32_t n = scan_pending(a, s0, [&](uint32_t s) {
+      return n_windows(a, s, K) <= kLongSet / 2; }, list, wave_cnt);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t s = list[i];
+      const int64_t n_win = n_windows(a, s, K);
+      uint32_t cap = 64;
+      while (cap < 2 * (uint32_t)n_win) cap <<= 1;
+      vote_long_one<K>(a, lut, s, n_win, lds_set, cap, red);
     }
-    uint32_t cap = 64;
-    while (cap < 2 * (uint32_t)n_win) cap <<= 1;
-    for (uint32_t i = tid; i < cap; i += blockDim.x) set[i] = 0u;
-    __syncthreads();
-    uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, cnt = 0u;
-    for (int64_t w = tid; w < n_win; w += blockDim.x) {
-      uint64_t key;
-      if (!pack_window(lut, window_bytes(a.residues, beg + (uint64_t)w), k, key)) continue;
-      uint32_t fid, sid;
-      if (!probe(a.slots, a.n_buckets, key, fid, sid)) continue;
-      fmin = min(fmin, fid);
-      fmax = max(fmax, fid);
-      const uint32_t id = sid + 1u;
-      uint32_t h = (id * 0x9E3779B1u) & (cap - 1u);
-      for (;;) {
-        const uint32_t old = atomicCAS(set + h, 0u, id);
-        if (old == 0u) {
-          cnt++;
-          break;
+  }
+  if (blockIdx.x >= kFallbackBlocks) return;
+  // Longer proteins: the first kFallbackBlocks blocks, a set in workspace scratch.
+  unsigned long long* gset =
+      reinterpret_cast<unsigned long long*>(a.scratch) + (uint64_t)blockIdx.x * kFallbackCap;
+  for (uint32_t s0 = blockIdx.x * 256u; s0 < a.n_seq; s0 += kFallbackBlocks * 256u) {
+    const uint32_t n = scan_pending(a, s0, [&](uint32_t s) {
+      return n_windows(a, s, K) > kLongSet / 2; }, list, wave_cnt);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t s = list[i];
+      const int64_t n_win = n_windows(a, s, K);
+      if (n_win > (int64_t)(kFallbackCap / 2)) {
+        if (tid == 0) {
+          a.out_fid[s] = -1;
+          a.out_count[s] = 0;
+          a.out_status[s] = KMA_STATUS_TOO_LONG;
         }
-        if (old == id) break;
-        h = (h + 1u) & (cap - 1u);
+        continue;
       }
+      uint32_t cap = 64;
+      while (cap < 2 * (uint32_t)n_win) cap <<= 1;
+      vote_long_one<K>(a, lut, s, n_win, gset, cap, red);
     }
-    fmin = block_reduce(fmin, red, 0);
-    fmax = block_reduce(fmax, red, 1);
-    cnt = block_reduce(cnt, red, 2);
-    if (tid == 0) {
-      if (fmin != fmax) {  // cannot be NONE: the main kernel only defers proteins with hits
-        a.out_fid[s] = -1;
-        a.out_count[s] = 0;
-        a.out_status[s] = KMA_STATUS_AMBIGUOUS;
-      } else {
-        a.out_fid[s] = (int32_t)fmin;
-        a.out_count[s] = (int32_t)cnt;
-        const bool called = cnt >= (uint32_t)a.min_hits;
-        a.out_status[s] = called ? KMA_STATUS_CALLED : KMA_STATUS_BELOW_MIN;
-        if (called && a.tally && fmin < a.n_fid) atomicAdd(a.tally + fmin, 1u);
-      }
-    }
-    __syncthreads();  // the set is reused by the next protein
   }
 }
 
@@ -397,9 +701,8 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
       kp = (kp << 5) | cp;
       km |= (uint64_t)cm << (5 * j);
     }
-    uint32_t sid;
-    hp = pv && probe(a.slots, a.n_buckets, kp, fp, sid);
-    hm = mv && probe(a.slots, a.n_buckets, km, fm, sid);
+    hp = pv && probe(a.slots, a.n_buckets, kp, fp);
+    hm = mv && probe(a.slots, a.n_buckets, km, fm);
     if (a.tally) {
       if (hp && fp < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fp, 1u);
       if (hm && fm < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fm, 1u);
@@ -436,7 +739,7 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a,
     kma_hit h;
     h.contig = c;
     h.left = (int32_t)(x + 1);
-    h.fid = (uint32_t)(v & kFidMask);
+    h.fid = (uint32_t)v & kFidMask;
     h.strand = minus ? '-' : '+';
     h.frame = (uint8_t)((minus ? (len - 3 * a.k - x) : x) % 3 + 1);
     h.pad = 0;
@@ -452,7 +755,7 @@ static unsigned grid_for(uint64_t n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
-hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint64_t n_buckets,
+hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets,
                                const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream) {
   hipLaunchKernelGGL(build_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream, slots, winner,
@@ -461,20 +764,58 @@ hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint64_t n_buc
 }
 
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
-                                 uint64_t n_buckets, uint32_t* stats, hipStream_t stream) {
-  hipLaunchKernelGGL(build_finalize_kernel, dim3(grid_for(n_buckets * kSlotsPerBucket)),
-                     dim3(256), 0, stream, slots, winner, fids, n_buckets, stats);
+                                 uint32_t n_buckets, uint32_t* stats, hipStream_t stream) {
+  hipLaunchKernelGGL(build_finalize_kernel,
+                     dim3(grid_for((uint64_t)n_buckets * kSlotsPerBucket)), dim3(256), 0, stream,
+                     slots, winner, fids, n_buckets, stats);
   return hipGetLastError();
 }
 
-hipError_t launch_proteins(const ProteinArgs& a, hipStream_t stream) {
-  if (a.n_seq == 0) return hipSuccess;
-  const unsigned blocks = (a.n_seq + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(proteins_kernel, dim3(blocks), dim3(256), 0, stream, a);
+// K1 access shape: quad-cooperative (default) or one lane per bucket (KMA_PROBE=lane).
+static bool probe_lane_shape() {
+  static const bool lane = [] {
+    const char* e = getenv("KMA_PROBE");
+    return e && e[0] == 'l';
+  }();
+  return lane;
+}
+
+template <int K>
+static hipError_t launch_proteins_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint64_t per_block = 256ull * kProbeWin;
+  const uint64_t want = (n_pos + per_block - 1) / per_block;
+  const uint64_t cap = (uint64_t)n_cu * kProbeBlocksPerCU;
+  if (want) {
+    const dim3 grid((unsigned)(want < cap ? want : cap));
+    if (probe_lane_shape())
+      hipLaunchKernelGGL((probe_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((probe_quad_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const unsigned blocks = (a.n_seq + kVoteWaves - 1) / kVoteWaves;
+  hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(proteins_fallback_kernel, dim3(kFallbackBlocks), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(vote_long_kernel<K>, dim3(n_cu * kLongBlocksPerCU), dim3(256), 0, stream, a);
   return hipGetLastError();
+}
+
+hipError_t launch_proteins(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  if (a.n_seq == 0) return hipSuccess;
+  switch (a.k) {
+    case 1: return launch_proteins_k<1>(a, n_cu, stream);
+    case 2: return launch_proteins_k<2>(a, n_cu, stream);
+    case 3: return launch_proteins_k<3>(a, n_cu, stream);
+    case 4: return launch_proteins_k<4>(a, n_cu, stream);
+    case 5: return launch_proteins_k<5>(a, n_cu, stream);
+    case 6: return launch_proteins_k<6>(a, n_cu, stream);
+    case 7: return launch_proteins_k<7>(a, n_cu, stream);
+    case 8: return launch_proteins_k<8>(a, n_cu, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {

@@ -27,7 +27,8 @@ EXPORTS = (
     "kma_abi_version", "kma_last_error", "kma_device_count", "kma_pack_kmers",
     "kma_table_create", "kma_table_create_packed", "kma_table_info_get", "kma_table_destroy",
     "kma_table_buckets_for", "kma_table_build_device", "kma_table_wrap_device",
-    "kma_table_device_ptr", "kma_workspace_create", "kma_workspace_destroy",
+    "kma_table_device_ptr", "kma_workspace_create", "kma_workspace_reserve",
+    "kma_workspace_destroy",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_contig_window_count",
 )
@@ -81,10 +82,11 @@ def load(path: str | None = None):
         L.kma_table_device_ptr.argtypes = [_vp, C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
         L.kma_workspace_destroy.argtypes = [_vp]
+        L.kma_workspace_reserve.argtypes = [_vp, _u64]
         L.kma_annotate_proteins.argtypes = [_vp, _u8p, _u64p, _u32, _int, _u32, _i32p, _i32p,
                                             _u8p, _vp, _u32]
-        L.kma_annotate_proteins_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _int, _u32, _vp,
-                                                   _vp, _vp, _vp, _u32, _vp]
+        L.kma_annotate_proteins_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _u32,
+                                                   _vp, _vp, _vp, _vp, _u32, _vp]
         L.kma_annotate_contigs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _vp, _u64,
                                            C.POINTER(_u64), _vp, _u32]
         L.kma_contig_window_count.restype = _u64
@@ -197,9 +199,14 @@ class SignatureTable:
 
 
 class Workspace:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, n_residues: int = 0):
         self._h = _vp()
         _check(load().kma_workspace_create(device, C.byref(self._h)))
+        if n_residues:
+            self.reserve(n_residues)
+
+    def reserve(self, n_residues: int):
+        _check(load().kma_workspace_reserve(self._h, n_residues))
 
     def close(self):
         if self._h:
@@ -237,12 +244,12 @@ def annotate_proteins(table: SignatureTable, residues: np.ndarray, offsets: np.n
 
 
 def annotate_proteins_device(table: SignatureTable, ws: Workspace, d_residues: int,
-                             d_offsets: int, n_seq: int, min_hits: int, flags: int, d_fid: int,
-                             d_count: int, d_status: int, d_tally: int = 0, n_fid: int = 0,
-                             stream: int = 0):
+                             d_offsets: int, n_seq: int, n_residues: int, min_hits: int,
+                             flags: int, d_fid: int, d_count: int, d_status: int, d_tally: int = 0,
+                             n_fid: int = 0, stream: int = 0):
     _check(load().kma_annotate_proteins_device(table._h, ws._h, d_residues, d_offsets, n_seq,
-                                               min_hits, flags, d_fid, d_count, d_status,
-                                               d_tally or None, n_fid, stream or None))
+                                               n_residues, min_hits, flags, d_fid, d_count,
+                                               d_status, d_tally or None, n_fid, stream or None))
 
 
 def annotate_contigs(table: SignatureTable, dna: np.ndarray, offsets: np.ndarray,

@@ -23,5 +23,14 @@ for s in $STEPS; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
             -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench5) run bench_c5 900 python bench.py --steps 10 --warmup 2 --workload c5 --no-cpu-baseline ;;
+    lf) for lf in 0.25 0.35 0.5; do
+          run prof_c5_lf$lf 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5_lf$lf -o run \
+            -- python3 bench.py --steps 5 --warmup 1 --workload c5 --no-cpu-baseline --load-factor $lf || exit $?; done ;;
+    prof5) run prof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof5 -o run \
+            -- python3 bench.py --steps 5 --warmup 1 --workload c5 --no-cpu-baseline ;;
+    gather) for cfg in ${GATHER_CFGS:-"16 lane 4" "150 lane 1" "150 lane 2" "150 lane 4" "150 quad 2" "150 quad 4" "150 quad 8" "1536 lane 1" "1536 lane 2" "1536 lane 4" "1536 quad 2" "1536 quad 4" "1536 quad 8" "1536 quad 4 1" "1536 lane 2 1" "6144 quad 4" "6144 lane 2"}; do
+              run gather 300 kmers.anno_amd/build/kma_gather_bench $cfg || exit $?
+              cat $OUT/gather.log >> $OUT/gather_all.log; done ;;
   esac
 done

@@ -204,7 +204,8 @@ def test_device_api_with_torch_buffers(kma):
     torch.cuda.synchronize()
     assert status[0].item() == 0
     t = kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0)
-    ws = kma.Workspace(0)
+    n_res = int(wl.offsets[-1])
+    ws = kma.Workspace(0, n_res)
     res = torch.from_numpy(wl.residues).to(dev)
     off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
     n = wl.n_seq
@@ -212,8 +213,9 @@ def test_device_api_with_torch_buffers(kma):
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
     st = torch.empty(n, dtype=torch.uint8, device=dev)
     tally = torch.zeros(1000, dtype=torch.int32, device=dev)
-    kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, 5, 0, fid.data_ptr(),
-                                 cnt.data_ptr(), st.data_ptr(), tally.data_ptr(), 1000, stream)
+    kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
+                                 fid.data_ptr(), cnt.data_ptr(), st.data_ptr(), tally.data_ptr(),
+                                 1000, stream)
     torch.cuda.synchronize()
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as th:
         hf, hc, hs, ht = kma.annotate_proteins(th, wl.residues, wl.offsets, 5, 0, n_fid=1000)
