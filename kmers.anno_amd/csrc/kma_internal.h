@@ -61,12 +61,13 @@ struct ProteinArgs {
 // K1 probe kernel: kProbeWin windows per thread per step, all first-bucket loads in flight.
 constexpr int kProbeWin = 4;
 constexpr int kProbeBlocksPerCU = 8;
-// K2 vote kernel: one wave per protein, kVoteWin words per lane per step, kVoteWaves waves per
-// block sharing an LDS pool of kVotePool u64 set entries. Proteins whose set does not fit are
-// finished by vote_long_kernel: one block each, an LDS set of kLongSet keys, else kFallbackCap
-// keys of workspace scratch per block.
+// K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteWaves
+// proteins (kVoteWin words per lane per chunk) and an LDS pool of kVotePool u64 set entries.
+// Proteins whose set does not fit are finished by vote_long_kernel: one block each, an LDS set
+// of kLongSet keys, else kFallbackCap keys of workspace scratch per block.
 constexpr int kWavesPerBlock = 4;
 constexpr int kVoteWin = 4;
+constexpr int kChunk = 64 * kVoteWin;
 constexpr int kVoteWaves = 8;
 constexpr int kVotePool = 4096;
 constexpr int kLongSet = 8192;

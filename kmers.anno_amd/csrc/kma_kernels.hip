@@ -439,47 +439,75 @@ __device__ __forceinline__ void vote_range(const ProteinArgs& a, const uint8_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2 — vote. One wave per protein; kVoteWaves waves per block share an LDS pool of kVotePool
-// u64 set entries (small static LDS per wave keeps 32 waves per CU resident).
-//   pass 1: the protein's K1 words (kVoteWin per lane per step) -> min fid, max fid, hits H.
-//           No hit -> NONE; two roles -> AMBIGUOUS (badPeg): no set needed; multiset -> H.
-//   pass 2: one role and H >= 2: a set of >= 2H entries taken from the pool; each hit window's
-//           key is re-packed from the residues and inserted, so a kmer occurring twice in one
-//           protein counts once (ProteinKmers is a set). The residues and words of a protein
-//           that fits one step are still in registers from pass 1.
-// A protein whose set does not fit the pool's free space is marked pending for
-// vote_long_kernel.
+// K2 — vote. A block of kVoteWaves waves owns kVoteWaves consecutive proteins; their windows are
+// cut into chunks of kChunk windows and the waves share the chunks of all the block's proteins,
+// so a long protein is spread over the block instead of one wave (no serial tail).
+//   pass 1: per chunk, the K1 words (kVoteWin per lane, all in flight) -> per-protein min fid,
+//           max fid, hits H in LDS. No hit -> NONE; two roles -> AMBIGUOUS (badPeg); multiset
+//           -> count H; H < 2 -> count H. These need no set.
+//   pass 2: a protein with one role and H >= 2 gets a set of >= 2H u64 keys from the block's
+//           LDS pool; each hit window's key is re-packed from the residues and inserted, so a
+//           kmer occurring twice in one protein counts once (ProteinKmers is a set).
+// A protein whose set does not fit the pool is marked pending for vote_long_kernel.
 // ---------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__(64 * kVoteWaves, 8) void vote_kernel(ProteinArgs a) {
+__global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   constexpr int V = kVoteWin;
+  constexpr int P = kVoteWaves;
   __shared__ __attribute__((aligned(16))) unsigned long long pool[kVotePool];
+  __shared__ uint64_t pbeg[P];
+  __shared__ uint32_t pwin[P], chunk0[P + 1], pmin[P], pmax[P], phits[P], pcnt[P], pbase[P],
+      pcap[P];
   __shared__ uint32_t pool_top;
   __shared__ uint8_t lut[256];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (tid < 256) lut[tid] = a.lut[tid];
-  if (tid == 0) pool_top = 0;
-  __syncthreads();
-  const uint32_t s = blockIdx.x * kVoteWaves + wave;
-  if (s >= a.n_seq) return;
-  const int64_t n_win = n_windows(a, s, K);
-  const uint64_t beg = a.offsets[s];
-  const uint32_t* __restrict__ words = a.hits + (beg - a.offsets[0]);
-  const uint8_t* __restrict__ res = a.residues + beg;
+  const uint32_t p0 = blockIdx.x * P;
+  const int np = (int)min<uint32_t>(P, a.n_seq - p0);
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  if (tid < 256) lut[tid] = a.lut[tid];
+  if (tid < P) {
+    uint32_t w = 0;
+    pbeg[tid] = 0;
+    if (tid < np) {
+      const int64_t n = n_windows(a, p0 + tid, K);
+      w = n > 0 ? (uint32_t)n : 0u;
+      pbeg[tid] = a.offsets[p0 + tid];
+    }
+    pwin[tid] = w;
+    pmin[tid] = 0xFFFFFFFFu;
+    pmax[tid] = 0u;
+    phits[tid] = 0u;
+    pcnt[tid] = 0u;
+    pcap[tid] = 0u;
+  }
+  if (tid == 0) {
+    uint32_t c = 0;
+    for (int i = 0; i < P; ++i) {
+      chunk0[i] = c;
+      c += (pwin[i] + kChunk - 1) / kChunk;
+    }
+    chunk0[P] = c;
+    pool_top = 0;
+  }
+  __syncthreads();
+  const uint64_t o0 = a.offsets[0];
+  const uint32_t n_chunks = chunk0[P];
   // ---- pass 1 ----------------------------------------------------------------------------------
-  uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, hits = 0u;
-  uint32_t h[V];
-  uint64_t bytes[V];
-  for (int64_t w0 = 0; w0 < n_win; w0 += 64 * V) {
+  for (uint32_t c = wave; c < n_chunks; c += P) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 1; i < P; ++i) p += c >= chunk0[i] ? 1u : 0u;
+    const int64_t n_win = pwin[p];
+    const int64_t w0 = (int64_t)(c - chunk0[p]) * kChunk;
+    const uint32_t* __restrict__ words = a.hits + (pbeg[p] - o0);
+    uint32_t h[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const int64_t w = w0 + v * 64 + lane;
-      const int64_t wc = w < n_win ? w : n_win - 1;
-      const uint32_t x = words[wc];
-      bytes[v] = window_bytes(res, (uint64_t)wc);
+      const uint32_t x = words[w < n_win ? w : n_win - 1];
       h[v] = w < n_win ? x : 0u;
     }
+    uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, hits = 0u;
 #pragma unroll
     for (int v = 0; v < V; ++v)
       if (h[v]) {
@@ -487,43 +515,75 @@ __global__ __launch_bounds__(64 * kVoteWaves, 8) void vote_kernel(ProteinArgs a)
         fmax = max(fmax, h[v] - 1u);
         hits++;
       }
-  }
-  const uint32_t wmin = wave_min(fmin), wmax = wave_max(fmax), wh = wave_sum(hits);
-  if (wmin == 0xFFFFFFFFu || wmin != wmax || multiset || wh < 2) {
-    if (lane == 0) write_vote(a, s, wmin, wmax, wh);
-    return;
-  }
-  // ---- pass 2: distinct hit keys -----------------------------------------------------------
-  uint32_t cap = 64;
-  while (cap < 2 * wh) cap <<= 1;
-  uint32_t base = 0;
-  if (lane == 0) {
-    base = atomicAdd(&pool_top, cap);
-    if (base + cap > (uint32_t)kVotePool) {
-      a.out_status[s] = kStatusPending;
-      atomicOr(a.overflow_flag, 1u);
+    fmin = wave_min(fmin);
+    fmax = wave_max(fmax);
+    hits = wave_sum(hits);
+    if (lane == 0 && hits) {
+      atomicMin(pmin + p, fmin);
+      atomicMax(pmax + p, fmax);
+      atomicAdd(phits + p, hits);
     }
   }
-  base = __shfl(base, 0, 64);
-  if (base + cap > (uint32_t)kVotePool) return;  // wave-uniform
-  unsigned long long* set = pool + base;
-  uint4* s4 = reinterpret_cast<uint4*>(set);
-  for (uint32_t i = lane; i < cap / 2; i += 64) s4[i] = make_uint4(0u, 0u, 0u, 0u);
-  uint32_t cnt = 0;
-  if (n_win <= 64 * V) {  // single step: words and residues still in registers
+  __syncthreads();
+  // ---- decide; take sets from the pool -------------------------------------------------------
+  if (tid < np) {
+    const uint32_t mn = pmin[tid], mx = pmax[tid], h = phits[tid];
+    if (mn == 0xFFFFFFFFu || mn != mx || multiset || h < 2) {
+      write_vote(a, p0 + tid, mn, mx, h);
+    } else {
+      uint32_t cap = 64;
+      while (cap < 2 * h) cap <<= 1;
+      const uint32_t base = atomicAdd(&pool_top, cap);
+      if (base + cap <= (uint32_t)kVotePool) {
+        pbase[tid] = base;
+        pcap[tid] = cap;
+      } else {
+        a.out_status[p0 + tid] = kStatusPending;
+        atomicOr(a.overflow_flag, 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t used = min(pool_top, (uint32_t)kVotePool);
+  if (used == 0) return;  // block-uniform: no protein needs a set
+  uint4* pool4 = reinterpret_cast<uint4*>(pool);
+  for (uint32_t i = tid; i < used / 2; i += 64 * P) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  // ---- pass 2: distinct hit keys ----------------------------------------------------------------
+  for (uint32_t c = wave; c < n_chunks; c += P) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 1; i < P; ++i) p += c >= chunk0[i] ? 1u : 0u;
+    const uint32_t cap = pcap[p];
+    if (cap == 0) continue;  // wave-uniform
+    const int64_t n_win = pwin[p];
+    const int64_t w0 = (int64_t)(c - chunk0[p]) * kChunk;
+    const uint32_t* __restrict__ words = a.hits + (pbeg[p] - o0);
+    const uint8_t* __restrict__ res = a.residues + pbeg[p];
+    uint32_t h[V];
+    WinWords ww[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int64_t w = w0 + v * 64 + lane;
+      const int64_t wc = w < n_win ? w : n_win - 1;
+      const uint32_t x = words[wc];
+      ww[v] = window_words(res, (uint64_t)wc);
+      h[v] = w < n_win ? x : 0u;
+    }
+    unsigned long long* set = pool + pbase[p];
+    uint32_t fresh = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v)
       if (h[v]) {
         uint64_t key;
-        pack_window<K>(lut, bytes[v], key);
-        cnt += set_insert(set, cap - 1, key) ? 1u : 0u;
+        pack_window<K>(lut, funnel(ww[v].lo, ww[v].hi, ww[v].sh), key);
+        fresh += set_insert(set, cap - 1, key) ? 1u : 0u;
       }
-  } else {
-    uint32_t m0 = 0xFFFFFFFFu, m1 = 0u;
-    vote_range<K, V, 64>(a, lut, words, res, n_win, lane, set, cap - 1, false, m0, m1, cnt);
+    fresh = wave_sum(fresh);
+    if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
   }
-  cnt = wave_sum(cnt);
-  if (lane == 0) write_vote(a, s, wmin, wmax, cnt);
+  __syncthreads();
+  if (tid < np && pcap[tid]) write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
 }
 
 __device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* red, int op) {
