@@ -35,6 +35,9 @@ K = 8
 MIN_HITS = 5
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probe
+# kma_gather_bench, 1.5 GiB buffer, quad shape (profiles/r01_gather_bench.jsonl): random 64-B
+# lines beyond L2 are served at ~5.5e10/s on MI355X.
+GATHER_CEILING_GBS = 3544.2
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
           "8-mer signature table, 1 MI355X per rank",
@@ -161,27 +164,35 @@ def main():
         step()
     torch.cuda.synchronize()
     d_tally.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        ev[i][1].record(stream)
     if world > 1:
         kdist.reduce_tallies(d_tally, dst=0)  # per-function tallies of the whole job -> rank 0
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    call_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    stats = torch.tensor([elapsed, call_ms], dtype=torch.float64, device=dev)
+    gpu_ms = ev0.elapsed_time(ev1)
+    # Per-phase device time of the same calls (hipEvents recorded by the library on the call's
+    # stream around the probe kernel K1 and the vote kernels K2), in a second loop so that the
+    # timed loop above carries no per-step events.
+    ws.timing(True)
+    for _ in range(args.steps):
+        step()
+    n_t, probe_ms, vote_ms = ws.timing_read()
+    ws.timing(False)
+    stats = torch.tensor([elapsed, gpu_ms, probe_ms / max(n_t, 1), vote_ms / max(n_t, 1)],
+                         dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, call_ms = stats.tolist()
+    elapsed, gpu_ms, k1_ms, k2_ms = stats.tolist()
 
     st = d_st.cpu().numpy()
     called = int((st == kmeranno.STATUS_CALLED).sum())
@@ -189,8 +200,11 @@ def main():
         total_lookups = n_win * args.steps * world
         value = total_lookups / elapsed
         seqs_per_s = n_seq * args.steps * world / elapsed
-        alg_bytes = n_win * BYTES_PER_LOOKUP + int(lens.sum())
-        achieved = alg_bytes / (call_ms * 1e-3) / 1e9
+        n_pos = max(n_res - K + 1, 0)
+        # K1 algorithmic bytes per launch: one 64-B bucket line + the 4-B result word per residue
+        # position probed, + 1 B per residue streamed in.
+        alg_bytes = n_pos * (BYTES_PER_LOOKUP + 4) + n_res
+        achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
         out = {
             "metric": "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs "
                       "roofline",
@@ -213,11 +227,13 @@ def main():
                                       "tally reduce (RCCL)"},
             "seqs_per_s": seqs_per_s,
             "called_per_batch": called,
+            "gpu_ms_per_step": gpu_ms / args.steps,
+            "phases_ms": {"probe_K1": k1_ms, "vote_K2": k2_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "proteins_kernel (+ its no-op fallback launch)",
-                         "call_ms": call_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "kernel": "probe_quad_kernel<8,4> (K1: every window's bucket gather)",
+                         "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
+                         "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sig, residues, offsets)

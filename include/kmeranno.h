@@ -157,6 +157,14 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_destroy(kma_workspace* ws);
+/* Per-phase device timing of the _device calls made with this workspace: with enable = 1 each
+ * call records hipEvents on its stream around the probe phase (every window's table lookup)
+ * and the vote phase (set semantics + vote). Not for graph capture. _read synchronises on
+ * the recorded events (the last 256 calls), returns their count and summed milliseconds, and
+ * clears the accumulators.                                                                  */
+int kma_workspace_timing(kma_workspace* ws, int enable);
+int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* probe_ms,
+                              double* vote_ms);
 
 /* ---- protein annotation (ApplyKmerProcessor.java:118-148) ----------------------------------
  * residues: raw ASCII proteins concatenated; sequence s is residues[offsets[s]..offsets[s+1]).

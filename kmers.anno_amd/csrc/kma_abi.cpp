@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -34,7 +35,29 @@ struct kma_workspace {
   uint64_t* d_scratch = nullptr;
   uint32_t* d_hits = nullptr;  // K1 words: one u32 per residue position
   uint64_t hits_cap = 0;
+  // Segmented overlap: K2 of segment i on `side` while K1 of segment i + 1 runs on the call's
+  // stream (fork/join through events, graph-capturable).
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> seg_ev;  // fork, per-segment K1 done, join
+  // Per-phase timing (kma_workspace_timing): a ring of (start, after K1, end) event triples.
+  bool timing = false;
+  std::vector<hipEvent_t> events;
+  uint32_t n_timed = 0;
 };
+constexpr uint32_t kTimingRing = 256;
+constexpr int kMaxSegments = 8;
+
+// Segments per call (K2 of a segment may run beside K1 of the next); KMA_SEGMENTS overrides.
+int segments_for(uint32_t n_seq) {
+  static const int forced = [] {
+    const char* e = getenv("KMA_SEGMENTS");
+    return e ? atoi(e) : 0;
+  }();
+  // Measured on MI355X (r01): K1 fills every CU, so K2 on the side stream does not overlap it
+  // and each extra segment adds a K1 ramp; default 1.
+  int s = forced > 0 ? forced : 1;
+  return std::max(1, std::min(s, std::min<int>(kMaxSegments, (int)std::max<uint32_t>(1, n_seq))));
+}
 
 namespace {
 
@@ -372,6 +395,11 @@ int kma_workspace_create(int device, kma_workspace** out) {
       n_cu > 0)
     w->n_cu = n_cu;
   hipError_t e = hipMalloc(&w->d_flag, 16);
+  if (e == hipSuccess) e = hipMemset(w->d_flag, 0, 16);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+  w->seg_ev.assign(kMaxSegments + 2, nullptr);
+  for (auto& ev : w->seg_ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 8);
   if (e != hipSuccess) {
@@ -396,9 +424,47 @@ int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
   return KMA_OK;
 }
 
+int kma_workspace_timing(kma_workspace* ws, int enable) {
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  DeviceScope ds(ws->device);
+  if (enable && ws->events.empty()) {
+    ws->events.resize(3 * kTimingRing);
+    for (auto& e : ws->events) KMA_HIP(hipEventCreate(&e));
+  }
+  ws->timing = enable != 0;
+  ws->n_timed = 0;
+  return KMA_OK;
+}
+
+int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* probe_ms,
+                              double* vote_ms) {
+  if (!ws || !n_calls || !probe_ms || !vote_ms) return fail(KMA_E_INVALID, "null argument");
+  DeviceScope ds(ws->device);
+  const uint32_t n = std::min(ws->n_timed, kTimingRing);
+  double p = 0, v = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    hipEvent_t* e = &ws->events[3 * i];
+    KMA_HIP(hipEventSynchronize(e[2]));
+    float a = 0, b = 0;
+    KMA_HIP(hipEventElapsedTime(&a, e[0], e[1]));
+    KMA_HIP(hipEventElapsedTime(&b, e[1], e[2]));
+    p += a;
+    v += b;
+  }
+  *n_calls = n;
+  *probe_ms = p;
+  *vote_ms = v;
+  ws->n_timed = 0;
+  return KMA_OK;
+}
+
 int kma_workspace_destroy(kma_workspace* ws) {
   if (!ws) return KMA_OK;
   DeviceScope ds(ws->device);
+  for (auto& e : ws->events) (void)hipEventDestroy(e);
+  for (auto& e : ws->seg_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ws->side) (void)hipStreamDestroy(ws->side);
   (void)hipFree(ws->d_flag);
   (void)hipFree(ws->d_scratch);
   if (ws->d_hits) (void)hipFree(ws->d_hits);
@@ -425,7 +491,6 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   hipStream_t s = static_cast<hipStream_t>(stream);
   DeviceScope ds(t->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  KMA_HIP(hipMemsetAsync(ws->d_flag, 0, 4, s));
   kma::ProteinArgs a{};
   a.slots = t->d_slots;
   a.n_buckets = (uint32_t)t->n_buckets;
@@ -445,7 +510,48 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   a.hits = ws->d_hits;
   a.overflow_flag = ws->d_flag;
   a.scratch = ws->d_scratch;
-  KMA_HIP(kma::launch_proteins(a, ws->n_cu, s));
+  hipEvent_t* ev = nullptr;
+  if (ws->timing) {
+    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
+    KMA_HIP(hipEventRecord(ev[0], s));
+  }
+  if (ev) {
+    // Timing mode: the phases back to back on the call's stream, so their events bracket them.
+    a.seq_lo = 0;
+    a.seq_hi = n_seq;
+    a.reset_flag = 1;
+    KMA_HIP(kma::launch_probe(a, ws->n_cu, s));
+    KMA_HIP(hipEventRecord(ev[1], s));
+    KMA_HIP(kma::launch_vote(a, ws->n_cu, s));
+    KMA_HIP(kma::launch_long(a, ws->n_cu, s));
+    KMA_HIP(hipEventRecord(ev[2], s));
+    return KMA_OK;
+  }
+  const int S = segments_for(n_seq);
+  if (S > 1) {
+    KMA_HIP(hipEventRecord(ws->seg_ev[0], s));  // fork: the side stream sees prior work
+    KMA_HIP(hipStreamWaitEvent(ws->side, ws->seg_ev[0], 0));
+  }
+  for (int i = 0; i < S; ++i) {
+    a.seq_lo = (uint32_t)((uint64_t)n_seq * i / S);
+    a.seq_hi = (uint32_t)((uint64_t)n_seq * (i + 1) / S);
+    a.reset_flag = i == 0;
+    KMA_HIP(kma::launch_probe(a, ws->n_cu, s));
+    if (S > 1) {
+      KMA_HIP(hipEventRecord(ws->seg_ev[1 + i], s));
+      KMA_HIP(hipStreamWaitEvent(ws->side, ws->seg_ev[1 + i], 0));
+      KMA_HIP(kma::launch_vote(a, ws->n_cu, ws->side));
+    } else {
+      KMA_HIP(kma::launch_vote(a, ws->n_cu, s));
+    }
+  }
+  if (S > 1) {
+    KMA_HIP(hipEventRecord(ws->seg_ev[kMaxSegments + 1], ws->side));  // join
+    KMA_HIP(hipStreamWaitEvent(s, ws->seg_ev[kMaxSegments + 1], 0));
+  }
+  a.seq_lo = 0;
+  a.seq_hi = n_seq;
+  KMA_HIP(kma::launch_long(a, ws->n_cu, s));
   return KMA_OK;
 }
 

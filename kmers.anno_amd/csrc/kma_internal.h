@@ -56,6 +56,8 @@ struct ProteinArgs {
   uint32_t* hits;           // workspace: fid + 1 (0 = miss) per residue position
   uint32_t* overflow_flag;  // workspace: set when a protein needs the global dedupe pass
   uint64_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u64
+  uint32_t seq_lo, seq_hi;  // the segment [seq_lo, seq_hi) of proteins this launch covers
+  uint32_t reset_flag;      // K1 of the first segment clears overflow_flag
 };
 
 // K1 probe kernel: kProbeWin windows per thread per step, all first-bucket loads in flight.
@@ -72,6 +74,7 @@ constexpr int kVoteWaves = 8;
 constexpr int kVotePool = 4096;
 constexpr int kLongSet = 8192;
 constexpr uint8_t kStatusPending = 0xFF;
+constexpr uint32_t kDeferred = 1u << 31;  // K2: set taken from the whole pool in phase 3
 constexpr int kLongBlocksPerCU = 4;
 constexpr int kFallbackBlocks = 64;
 constexpr uint32_t kFallbackCap = 1u << 17;  // u64 entries per block (1 MiB)
@@ -98,7 +101,9 @@ hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buc
                                hipStream_t stream);
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
                                  uint32_t n_buckets, uint32_t* stats, hipStream_t stream);
-hipError_t launch_proteins(const ProteinArgs& a, int n_cu, hipStream_t stream);
+hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K1
+hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream);   // K2 (segment)
+hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream);   // long proteins
 hipError_t launch_contigs(const ContigArgs& a, uint64_t n_blocks, const uint64_t* d_prefix,
                           uint8_t* out_hits, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,

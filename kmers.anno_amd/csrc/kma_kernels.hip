@@ -200,13 +200,17 @@ template <int K, int U>
 __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
   const int t = threadIdx.x;
+  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
-  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
-  const uint8_t* __restrict__ res = a.residues + a.offsets[0];
+  const uint64_t o0 = a.offsets[0];
+  const uint64_t n_all = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint64_t seg_hi = a.offsets[a.seq_hi] - o0;
+  const uint64_t n_pos = seg_hi < n_all ? seg_hi : n_all;
+  const uint8_t* __restrict__ res = a.residues + o0;
   const uint64_t* __restrict__ slots = a.slots;
   const uint32_t nb = a.n_buckets;
-  for (uint64_t g0 = (uint64_t)blockIdx.x * (256 * U); g0 < n_pos;
+  for (uint64_t g0 = (a.offsets[a.seq_lo] - o0) + (uint64_t)blockIdx.x * (256 * U); g0 < n_pos;
        g0 += (uint64_t)gridDim.x * (256 * U)) {
     uint64_t bytes[U];
 #pragma unroll
@@ -269,17 +273,23 @@ template <int K, int U>
 __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
   const int t = threadIdx.x, part = t & 3;
+  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
-  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
-  const uint8_t* __restrict__ res = a.residues + a.offsets[0];
+  // This segment's positions: [offsets[seq_lo], offsets[seq_hi]) relative to offsets[0],
+  // clipped to the last full window of the batch.
+  const uint64_t o0 = a.offsets[0];
+  const uint64_t n_all = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint64_t seg_hi = a.offsets[a.seq_hi] - o0;
+  const uint64_t n_pos = seg_hi < n_all ? seg_hi : n_all;
+  const uint8_t* __restrict__ res = a.residues + o0;
   const uint64_t* __restrict__ slots = a.slots;
   const uint32_t nb = a.n_buckets;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   const uint64_t stride = (uint64_t)gridDim.x * (256 * U);
   // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
   // flight, so a wave's only exposed latency per step is the bucket gather.
-  uint64_t g0 = (uint64_t)blockIdx.x * (256 * U);
+  uint64_t g0 = (a.offsets[a.seq_lo] - o0) + (uint64_t)blockIdx.x * (256 * U);
   WinWords ww[U];
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -438,6 +448,38 @@ __device__ __forceinline__ void vote_range(const ProteinArgs& a, const uint8_t* 
   }
 }
 
+// One chunk of kChunk windows of a protein (a wave, kVoteWin per lane, all loads in flight):
+// every hit window's key is re-packed from the residues and inserted in `set`; returns the
+// wave's number of new keys.
+template <int K>
+__device__ __forceinline__ uint32_t dedupe_chunk(const ProteinArgs& a, const uint8_t* lut,
+                                                 unsigned long long* set, uint32_t mask,
+                                                 uint64_t beg, int64_t n_win, int64_t w0,
+                                                 int lane) {
+  constexpr int V = kVoteWin;
+  const uint32_t* __restrict__ words = a.hits + (beg - a.offsets[0]);
+  const uint8_t* __restrict__ res = a.residues + beg;
+  uint32_t h[V];
+  WinWords ww[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int64_t w = w0 + v * 64 + lane;
+    const int64_t wc = w < n_win ? w : n_win - 1;
+    const uint32_t x = words[wc];
+    ww[v] = window_words(res, (uint64_t)wc);
+    h[v] = w < n_win ? x : 0u;
+  }
+  uint32_t fresh = 0;
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+    if (h[v]) {
+      uint64_t key;
+      pack_window<K>(lut, funnel(ww[v].lo, ww[v].hi, ww[v].sh), key);
+      fresh += set_insert(set, mask, key) ? 1u : 0u;
+    }
+  return wave_sum(fresh);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2 — vote. A block of kVoteWaves waves owns kVoteWaves consecutive proteins; their windows are
 // cut into chunks of kChunk windows and the waves share the chunks of all the block's proteins,
@@ -461,8 +503,8 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   __shared__ uint32_t pool_top;
   __shared__ uint8_t lut[256];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t p0 = blockIdx.x * P;
-  const int np = (int)min<uint32_t>(P, a.n_seq - p0);
+  const uint32_t p0 = a.seq_lo + blockIdx.x * P;
+  const int np = (int)min<uint32_t>(P, a.seq_hi - p0);
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
   if (tid < 256) lut[tid] = a.lut[tid];
   if (tid < P) {
@@ -537,15 +579,17 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
       if (base + cap <= (uint32_t)kVotePool) {
         pbase[tid] = base;
         pcap[tid] = cap;
+      } else if (cap <= (uint32_t)kVotePool) {
+        pcap[tid] = cap | kDeferred;  // phase 3: the whole pool, after pass 2
       } else {
-        a.out_status[p0 + tid] = kStatusPending;
+        a.out_status[p0 + tid] = kStatusPending;  // vote_long_kernel, global-memory set
         atomicOr(a.overflow_flag, 1u);
       }
     }
   }
   __syncthreads();
   const uint32_t used = min(pool_top, (uint32_t)kVotePool);
-  if (used == 0) return;  // block-uniform: no protein needs a set
+  if (used == 0) return;  // block-uniform: no protein needs a set (nor a deferred one)
   uint4* pool4 = reinterpret_cast<uint4*>(pool);
   for (uint32_t i = tid; i < used / 2; i += 64 * P) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
@@ -555,35 +599,30 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
 #pragma unroll
     for (int i = 1; i < P; ++i) p += c >= chunk0[i] ? 1u : 0u;
     const uint32_t cap = pcap[p];
-    if (cap == 0) continue;  // wave-uniform
-    const int64_t n_win = pwin[p];
-    const int64_t w0 = (int64_t)(c - chunk0[p]) * kChunk;
-    const uint32_t* __restrict__ words = a.hits + (pbeg[p] - o0);
-    const uint8_t* __restrict__ res = a.residues + pbeg[p];
-    uint32_t h[V];
-    WinWords ww[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int64_t w = w0 + v * 64 + lane;
-      const int64_t wc = w < n_win ? w : n_win - 1;
-      const uint32_t x = words[wc];
-      ww[v] = window_words(res, (uint64_t)wc);
-      h[v] = w < n_win ? x : 0u;
-    }
-    unsigned long long* set = pool + pbase[p];
-    uint32_t fresh = 0;
-#pragma unroll
-    for (int v = 0; v < V; ++v)
-      if (h[v]) {
-        uint64_t key;
-        pack_window<K>(lut, funnel(ww[v].lo, ww[v].hi, ww[v].sh), key);
-        fresh += set_insert(set, cap - 1, key) ? 1u : 0u;
-      }
-    fresh = wave_sum(fresh);
+    if (cap == 0 || (cap & kDeferred)) continue;  // wave-uniform
+    const uint32_t fresh = dedupe_chunk<K>(a, lut, pool + pbase[p], cap - 1, pbeg[p], pwin[p],
+                                           (int64_t)(c - chunk0[p]) * kChunk, lane);
     if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
   }
   __syncthreads();
-  if (tid < np && pcap[tid]) write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
+  if (tid < np && pcap[tid] && !(pcap[tid] & kDeferred))
+    write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
+  // ---- phase 3: proteins that did not fit beside the others take the whole pool in turn ------
+  for (int p = 0; p < np; ++p) {
+    const uint32_t cap = pcap[p];
+    if (!(cap & kDeferred)) continue;  // block-uniform
+    const uint32_t c2 = cap & ~kDeferred;
+    __syncthreads();  // the pool's previous contents are no longer read
+    for (uint32_t i = tid; i < c2 / 2; i += 64 * P) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    for (uint32_t c = chunk0[p] + wave; c < chunk0[p + 1]; c += P) {
+      const uint32_t fresh = dedupe_chunk<K>(a, lut, pool, c2 - 1, pbeg[p], pwin[p],
+                                             (int64_t)(c - chunk0[p]) * kChunk, lane);
+      if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
+    }
+    __syncthreads();
+    if (tid == 0) write_vote(a, p0 + p, pmin[p], pmax[p], pcnt[p]);
+  }
 }
 
 __device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* red, int op) {
@@ -841,41 +880,62 @@ static bool probe_lane_shape() {
 }
 
 template <int K>
-static hipError_t launch_proteins_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  const uint64_t n_pos = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  // Grid from the batch average (the host does not see the segment's residue count).
+  const uint64_t seg = a.seq_hi - a.seq_lo;
+  const uint64_t n_pos = a.n_seq ? a.n_residues / a.n_seq * seg + 1 : 0;
   const uint64_t per_block = 256ull * kProbeWin;
   const uint64_t want = (n_pos + per_block - 1) / per_block;
   const uint64_t cap = (uint64_t)n_cu * kProbeBlocksPerCU;
-  if (want) {
-    const dim3 grid((unsigned)(want < cap ? want : cap));
-    if (probe_lane_shape())
-      hipLaunchKernelGGL((probe_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((probe_quad_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  const unsigned blocks = (a.n_seq + kVoteWaves - 1) / kVoteWaves;
-  hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(vote_long_kernel<K>, dim3(n_cu * kLongBlocksPerCU), dim3(256), 0, stream, a);
+  if (!want || a.n_residues < (uint64_t)K) return hipSuccess;
+  const dim3 grid((unsigned)(want < cap ? want : cap));
+  if (probe_lane_shape())
+    hipLaunchKernelGGL((probe_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((probe_quad_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
-hipError_t launch_proteins(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  if (a.n_seq == 0) return hipSuccess;
-  switch (a.k) {
-    case 1: return launch_proteins_k<1>(a, n_cu, stream);
-    case 2: return launch_proteins_k<2>(a, n_cu, stream);
-    case 3: return launch_proteins_k<3>(a, n_cu, stream);
-    case 4: return launch_proteins_k<4>(a, n_cu, stream);
-    case 5: return launch_proteins_k<5>(a, n_cu, stream);
-    case 6: return launch_proteins_k<6>(a, n_cu, stream);
-    case 7: return launch_proteins_k<7>(a, n_cu, stream);
-    case 8: return launch_proteins_k<8>(a, n_cu, stream);
-    default: return hipErrorInvalidValue;
+template <int K>
+static hipError_t launch_vote_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  const unsigned blocks = (a.seq_hi - a.seq_lo + kVoteWaves - 1) / kVoteWaves;
+  if (!blocks) return hipSuccess;
+  hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t launch_long_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  hipLaunchKernelGGL(vote_long_kernel<K>, dim3(kFallbackBlocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+#define KMA_DISPATCH_K(FN)                              \
+  switch (a.k) {                                         \
+    case 1: return FN<1>(a, n_cu, stream);               \
+    case 2: return FN<2>(a, n_cu, stream);               \
+    case 3: return FN<3>(a, n_cu, stream);               \
+    case 4: return FN<4>(a, n_cu, stream);               \
+    case 5: return FN<5>(a, n_cu, stream);               \
+    case 6: return FN<6>(a, n_cu, stream);               \
+    case 7: return FN<7>(a, n_cu, stream);               \
+    case 8: return FN<8>(a, n_cu, stream);               \
+    default: return hipErrorInvalidValue;                \
   }
+
+hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  if (a.n_seq == 0) return hipSuccess;
+  KMA_DISPATCH_K(launch_probe_k)
+}
+
+hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  if (a.n_seq == 0) return hipSuccess;
+  KMA_DISPATCH_K(launch_vote_k)
+}
+
+hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  if (a.n_seq == 0) return hipSuccess;
+  KMA_DISPATCH_K(launch_long_k)
 }
 
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {

@@ -28,7 +28,7 @@ EXPORTS = (
     "kma_table_create", "kma_table_create_packed", "kma_table_info_get", "kma_table_destroy",
     "kma_table_buckets_for", "kma_table_build_device", "kma_table_wrap_device",
     "kma_table_device_ptr", "kma_workspace_create", "kma_workspace_reserve",
-    "kma_workspace_destroy",
+    "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_contig_window_count",
 )
@@ -83,6 +83,9 @@ def load(path: str | None = None):
         L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
         L.kma_workspace_destroy.argtypes = [_vp]
         L.kma_workspace_reserve.argtypes = [_vp, _u64]
+        L.kma_workspace_timing.argtypes = [_vp, _int]
+        L.kma_workspace_timing_read.argtypes = [_vp, C.POINTER(_u32), C.POINTER(C.c_double),
+                                                C.POINTER(C.c_double)]
         L.kma_annotate_proteins.argtypes = [_vp, _u8p, _u64p, _u32, _int, _u32, _i32p, _i32p,
                                             _u8p, _vp, _u32]
         L.kma_annotate_proteins_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _u32,
@@ -207,6 +210,16 @@ class Workspace:
 
     def reserve(self, n_residues: int):
         _check(load().kma_workspace_reserve(self._h, n_residues))
+
+    def timing(self, enable: bool = True):
+        """Per-phase hipEvent timing of the device calls made with this workspace."""
+        _check(load().kma_workspace_timing(self._h, int(enable)))
+
+    def timing_read(self):
+        """(n_calls, probe_ms_total, vote_ms_total) since the last read; clears them."""
+        n, p, v = _u32(), C.c_double(), C.c_double()
+        _check(load().kma_workspace_timing_read(self._h, C.byref(n), C.byref(p), C.byref(v)))
+        return n.value, p.value, v.value
 
     def close(self):
         if self._h:

@@ -1,0 +1,101 @@
+"""The C++ host `kma apply` (mirror of ApplyKmerProcessor + its reporters) end to end on the
+reference's own genome fixture small.gto. Expected reports are built here from the oracle's
+per-protein calls with the reporters' rules (rep/DefaultApplyKmerReporter.java:43-55,
+rep/VerifyApplyKmerReporter.java:32-45). Error-path tests need no GPU."""
+import gzip
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PKG
+
+KMA = os.path.join(PKG, "build", "kma")
+
+
+@pytest.fixture(scope="module")
+def kma_bin(native_lib):
+    if not os.path.exists(KMA):
+        subprocess.run(["make", "-s", "-C", PKG, "build/kma"], check=True)
+    return KMA
+
+
+@pytest.fixture(scope="module")
+def apply_inputs(tmp_path_factory, small_gto):
+    d = tmp_path_factory.mktemp("apply")
+    gdir = d / "gtos"
+    gdir.mkdir()
+    with gzip.open(os.path.join(GOLDEN, "small.gto.gz"), "rb") as f, \
+            open(gdir / "97478.30.gto", "wb") as o:
+        shutil.copyfileobj(f, o)
+    pegs = [f for f in small_gto["features"] if f["type"] == "CDS"]
+    rng = np.random.default_rng(17)
+    rows = []
+    for i, f in enumerate(pegs[:300]):
+        p = f["protein_translation"]
+        for j in rng.choice(len(p) - 7, 12, replace=False):
+            rows.append((p[j:j + 8], f"ROLE{i % 60:03d}"))
+    rows.append((pegs[5]["protein_translation"][:8], "ROLE999"))  # makes peg 5 ambiguous
+    rows.append(("ACDEFGH", "ROLE001"))  # wrong length: loaded, never matches
+    with open(d / "kmerdb.tbl", "w") as f:
+        f.writelines(f"{k}\t{r}\n" for k, r in rows)
+    roles = [f"ROLE{i:03d}" for i in range(0, 60, 2)] + ["ROLE999"]
+    with open(d / "roles.in.use", "w") as f:
+        f.writelines(f"{r}\tsome role name {r}\n" for r in roles)
+    return d, rows, roles, pegs
+
+
+def _expected(oracle_c, small_gto, rows, roles, pegs, min_hits):
+    ids = {}
+    for _, r in rows:
+        ids.setdefault(r, len(ids))
+    inv = {v: k for k, v in ids.items()}
+    t = oracle_c.Table([r[0] for r in rows], [ids[r[1]] for r in rows])
+    res, off = oracle_c.pack_strings([f.get("protein_translation", "") for f in pegs])
+    fid, cnt, st = oracle_c.apply(t, res, off, 8, min_hits, 0)
+    col = {r: i for i, r in enumerate(roles)}
+    counts = [0] * len(roles)
+    verify = ["genome_id\tpeg_id\trole\thits\tfunction"]
+    gid = small_gto["id"]
+    for f, fi, c, s in zip(pegs, fid, cnt, st):
+        if s == 1:
+            role = inv[int(fi)]
+            if role in col:
+                counts[col[role]] += 1
+            verify.append(f"{gid}\t{f['id']}\t{role}\t{int(c)}\t{f.get('function', '')}")
+    apply = [gid + "\t" + "\t".join(map(str, counts))]
+    return apply, verify
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("min_hits", [5, 2])
+def test_kma_apply_reports(kma_bin, oracle_c, small_gto, apply_inputs, min_hits):
+    d, rows, roles, pegs = apply_inputs
+    exp_apply, exp_verify = _expected(oracle_c, small_gto, rows, roles, pegs, min_hits)
+    assert sum(int(x) for x in exp_apply[0].split("\t")[1:]) > 20
+    args = [kma_bin, "apply", "-m", str(min_hits), str(d / "kmerdb.tbl"),
+            str(d / "roles.in.use"), str(d / "gtos")]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == exp_apply
+    out = subprocess.run(args[:2] + ["--format", "VERIFY"] + args[2:], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == exp_verify
+
+
+def test_kma_apply_errors(kma_bin, apply_inputs, tmp_path):
+    d, _, _, _ = apply_inputs
+    r = subprocess.run([kma_bin, "apply", str(d / "kmerdb.tbl"), str(d / "roles.in.use"),
+                        str(tmp_path / "missing")], capture_output=True, text=True)
+    assert r.returncode == 1 and "Input directory" in r.stderr and "not found" in r.stderr
+    r = subprocess.run([kma_bin, "apply", "-m", "0", str(d / "kmerdb.tbl"),
+                        str(d / "roles.in.use"), str(d / "gtos")], capture_output=True, text=True)
+    assert r.returncode == 2 and "Min-hits must be positive." in r.stderr
+    r = subprocess.run([kma_bin, "apply", "--format", "TRAIN", "a", "b", "c"],
+                       capture_output=True, text=True)
+    assert r.returncode == 2
+    r = subprocess.run([kma_bin, "frobnicate"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Invalid command frobnicate." in r.stderr

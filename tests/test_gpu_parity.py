@@ -224,3 +224,31 @@ def test_device_api_with_torch_buffers(kma):
     assert (tally.cpu().numpy().astype(np.uint32) == ht).all()
     ws.close()
     t.close()
+
+
+def test_workspace_phase_timing(kma):
+    """kma_workspace_timing: per-phase hipEvent durations of device calls (probe, vote)."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_workload(500, 20_000, 200, seed=31)
+    dev = torch.device("cuda", 0)
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        n_res = int(wl.offsets[-1])
+        ws = kma.Workspace(0, n_res)
+        res = torch.from_numpy(wl.residues).to(dev)
+        off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
+        n = wl.n_seq
+        outs = [torch.empty(n, dtype=d, device=dev) for d in (torch.int32, torch.int32, torch.uint8)]
+        stream = torch.cuda.current_stream().cuda_stream
+        ws.timing(True)
+        for _ in range(3):
+            kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
+                                         *[o.data_ptr() for o in outs], 0, 0, stream)
+        calls, probe_ms, vote_ms = ws.timing_read()
+        assert calls == 3 and probe_ms > 0 and vote_ms > 0
+        assert ws.timing_read()[0] == 0
+        with pytest.raises(kma.KmerAnnoError) as e:  # reservation too small
+            kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res + 1, 5,
+                                         0, *[o.data_ptr() for o in outs], 0, 0, stream)
+        assert e.value.code == kma.E_CAPACITY
+        ws.close()
