@@ -81,7 +81,7 @@ extern "C" {
  *   so key equality is exactly the String.equals of the reference's HashMap lookup.
  * A table slot is the 64-bit word (key << 24) | fid, so fid < 2^24.                         */
 #define KMA_MAX_K 8
-#define KMA_MAX_FID ((1u << 24) - 1u)
+#define KMA_MAX_FID ((1u << 23) - 1u)
 
 typedef struct kma_table kma_table;         /* opaque: a signature table resident on one GPU */
 typedef struct kma_workspace kma_workspace; /* opaque: per-stream scratch for _device calls  */
@@ -97,6 +97,7 @@ typedef struct kma_table_info {
   uint32_t max_probe;    /* longest bucket chain a stored key needs (1 = home bucket)      */
   uint32_t n_extra_syms; /* bytes mapped to codes 28..31                                   */
   uint8_t extra_syms[4];
+  int32_t minimizer_len; /* m: a key's home bucket is a hash of its minimizer m-mer        */
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -140,10 +141,11 @@ int kma_table_destroy(kma_table* table);
  * that is later broadcast over RCCL to the other GPUs of the node).
  *   kma_table_buckets_for : bucket count for n keys at the load factor
  *   kma_table_build_device: d_slots (n_buckets*64 bytes) and d_winner (n_buckets*8 u32) are
- *                           caller scratch; keys/fids are device arrays; builds on `stream`.
+ *                           caller scratch; keys/fids are device arrays; builds on `stream`;
+ *                           d_status (4 u32) receives {table full, entries, max probe}.
  *   kma_table_wrap_device : adopt an already-built slot array (not owned, not freed).        */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
-int kma_table_build_device(void* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
                            const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
                            uint32_t* d_status, void* stream);
 int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device,
@@ -176,7 +178,7 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                           uint32_t* out_tally, uint32_t n_fid);
 /* Device form: every pointer is device memory on the table's device; `d_residues` is 8-byte
- * aligned and readable for 16 bytes past offsets[n_seq]; n_residues = offsets[n_seq] -
+ * aligned and readable for 32 bytes past offsets[n_seq]; n_residues = offsets[n_seq] -
  * offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is accumulated into, not
  * cleared. Asynchronous on `stream`.                                                          */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,

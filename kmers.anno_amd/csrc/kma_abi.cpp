@@ -17,9 +17,21 @@
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
 
+int kma::minimizer_len(int k, uint64_t n_buckets) {
+  static const int forced = [] {
+    const char* e = getenv("KMA_MINIMIZER");
+    return e ? atoi(e) : 0;
+  }();
+  const int m6 = k < 6 ? k : 6, m7 = k < 7 ? k : 7;
+  if (forced == 6) return m6;
+  if (forced == 7) return m7;
+  return n_buckets <= (1ull << 22) ? m6 : m7;
+}
+
 struct kma_table {
   int device = 0;
   int k = 8;
+  int mlen = 6;  // minimizer length of the layout (kma::minimizer_len)
   uint64_t n_buckets = 0;
   uint64_t* d_slots = nullptr;
   bool owned = false;
@@ -183,6 +195,7 @@ int make_table_object(int device, int k, uint64_t n_buckets, uint64_t* d_slots, 
   kma_table* t = new kma_table();
   t->device = device;
   t->k = k;
+  t->mlen = kma::minimizer_len(k, n_buckets);
   t->n_buckets = n_buckets;
   t->d_slots = d_slots;
   t->owned = owned;
@@ -198,22 +211,24 @@ int make_table_object(int device, int k, uint64_t n_buckets, uint64_t* d_slots, 
   t->info.bytes = n_buckets * 64;
   t->info.k = k;
   t->info.device = device;
+  t->info.minimizer_len = t->mlen;
   *out = t;
   return KMA_OK;
 }
 
 constexpr uint64_t kMaxBuckets = 1ull << 29;  // slot index and bucket index stay 32-bit
 
-int build_on_device(uint64_t* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
                     const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, uint32_t* d_status,
                     hipStream_t s) {
   if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than 2^29 buckets");
   KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * 64, s));
   KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::kSlotsPerBucket * sizeof(uint32_t), s));
   KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
-  KMA_HIP(kma::launch_build_insert(d_slots, d_winner, (uint32_t)n_buckets, d_keys, n, d_status,
-                                   s));
-  KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, (uint32_t)n_buckets,
+  const int m = kma::minimizer_len(k, n_buckets);
+  KMA_HIP(kma::launch_build_insert(d_slots, d_winner, (uint32_t)n_buckets, k, m, d_keys, n,
+                                   d_status, s));
+  KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, (uint32_t)n_buckets, k, m,
                                      d_status + 1, s));
   return KMA_OK;
 }
@@ -225,7 +240,7 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
   if (lf <= 0) lf = 0.5;
   if (lf > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", lf);
   for (uint64_t r = 0; r < n; ++r)
-    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^24-1",
+    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^23-1",
                                             fids[r], (unsigned long long)r);
   const uint64_t nb = kma_table_buckets_for(n, lf);
   if (nb > kMaxBuckets)
@@ -244,7 +259,7 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
   KMA_HIP(hipMalloc(&d_slots, nb * 64));
   KMA_HIP(hipMemcpy(d_keys, keys.data(), n * 8, hipMemcpyHostToDevice));
   KMA_HIP(hipMemcpy(d_fids, fids, n * 4, hipMemcpyHostToDevice));
-  int rc = build_on_device(d_slots, nb, d_winner, d_keys, d_fids, n, d_status, nullptr);
+  int rc = build_on_device(d_slots, nb, k, d_winner, d_keys, d_fids, n, d_status, nullptr);
   uint32_t st[4] = {};
   if (rc == KMA_OK) {
     hipError_t e = hipMemcpy(st, d_status, 16, hipMemcpyDeviceToHost);
@@ -357,13 +372,14 @@ int kma_table_destroy(kma_table* table) {
   return KMA_OK;
 }
 
-int kma_table_build_device(void* d_slots, uint64_t n_buckets, uint32_t* d_winner,
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
                            const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
                            uint32_t* d_status, void* stream) {
   if (!d_slots || !d_winner || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
     return fail(KMA_E_INVALID, "null argument");
-  return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, d_winner, d_keys, d_fids, n,
-                         d_status, static_cast<hipStream_t>(stream));
+  if (int rc = check_k(k)) return rc;
+  return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, d_winner, d_keys, d_fids,
+                         n, d_status, static_cast<hipStream_t>(stream));
 }
 
 int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device, kma_table** out) {
@@ -500,6 +516,7 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   a.n_seq = n_seq;
   a.n_residues = n_residues;
   a.k = t->k;
+  a.mlen = t->mlen;
   a.min_hits = min_hits;
   a.flags = flags;
   a.out_fid = d_fid;
@@ -576,13 +593,13 @@ int kma_annotate_proteins(const kma_table* t, const uint8_t* residues, const uin
   uint64_t* d_off;
   int32_t *d_fid, *d_cnt;
   uint32_t* d_tally = nullptr;
-  KMA_HIP(b.alloc(&d_res, nres + 16));
+  KMA_HIP(b.alloc(&d_res, nres + 32));
   KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
   KMA_HIP(b.alloc(&d_fid, n_seq * 4ull));
   KMA_HIP(b.alloc(&d_cnt, n_seq * 4ull));
   KMA_HIP(b.alloc(&d_st, n_seq));
   KMA_HIP(hipMemcpy(d_res, residues + base, nres, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemset(d_res + nres, 0, 16));
+  KMA_HIP(hipMemset(d_res + nres, 0, 32));
   KMA_HIP(hipMemcpy(d_off, rel.data(), (n_seq + 1) * 8ull, hipMemcpyHostToDevice));
   if (out_tally && n_fid) {
     KMA_HIP(b.alloc(&d_tally, n_fid * 4ull));
@@ -663,6 +680,7 @@ int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t*
   a.n_contig = n_contig;
   a.total_bases = total;
   a.k = t->k;
+  a.mlen = t->mlen;
   a.codon_codes = d_codes;
   a.staging = d_staging;
   a.block_counts = d_counts;

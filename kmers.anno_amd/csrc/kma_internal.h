@@ -10,31 +10,73 @@ namespace kma {
 // ---- signature-table layout in HBM ------------------------------------------------------------
 // n_buckets x 64-byte buckets (n_buckets < 2^29); each bucket = 8 slots of one u64:
 //   low dword  = key bits 0..31            (never 0 for a valid key: codes are 1..31)
-//   high dword = key bits 32..39 << 24 | fid (24 bits)
-// An all-zero slot is empty. A key lives in its home bucket or, if that is full, in the next
-// buckets (linear bucket probing, wrapping). Lookups stop at the first bucket holding the key or
-// an empty slot. Every compare is a 32-bit operation.
+//   high dword = key bits 32..39 << 24 | overflow bit << 23 | fid (23 bits)
+// A slot whose low dword is 0 is empty. A key lives in its home bucket or, if that was full,
+// in the next buckets (linear bucket probing, wrapping). The 8 overflow bits of a bucket (one
+// per slot, independent of the slot's key) form a filter of the keys homed there that live
+// further down the chain: overflow bit ovf_index(key) of the home bucket is set for each. A
+// lookup that misses its home bucket walks the chain only if its bit is set (then it stops at
+// the key or at a bucket with an empty slot), so a miss costs one 64-byte request except for
+// ~1% of keys. Every compare is a 32-bit operation.
 constexpr int kSlotsPerBucket = 8;
-constexpr uint32_t kFidMask = (1u << 24) - 1;
+constexpr uint32_t kFidMask = (1u << 23) - 1;
+constexpr uint32_t kOvfBit = 1u << 23;         // in the high dword
+constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
 
 __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
   return ((uint64_t)((uint32_t)(key >> 32) << 24 | (fid & kFidMask)) << 32) | (uint32_t)key;
 }
+// Which slot of the home bucket carries the key's overflow bit (from the key's low dword).
+__host__ __device__ inline uint32_t ovf_index(uint32_t klo) { return (klo * 0x9E3779B1u) >> 29; }
 __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
   return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
 }
 
-// Home bucket: a 32-bit mix of the <= 40-bit key (murmur3 fmix32 over both halves), mapped to
-// [0, n_buckets) by a multiply-high (Lemire fast range).
-__host__ __device__ inline uint32_t home_bucket(uint64_t key, uint32_t n_buckets) {
-  uint32_t h = (uint32_t)key * 0x9E3779B1u ^ ((uint32_t)(key >> 32) + 0x7F4A7C15u) * 0x85EBCA77u;
+__host__ __device__ inline uint32_t mix32(uint32_t h) {  // murmur3 fmix32
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
   h ^= h >> 13;
   h *= 0xC2B2AE35u;
   h ^= h >> 16;
+  return h;
+}
+
+// Minimizer of a packed K-mer: the smallest hash over its K - m + 1 m-mers (5-bit residue
+// codes, first residue most significant). m is a table property (minimizer_len below).
+__host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
+  const uint32_t mask = (uint32_t)((1ull << (5 * m)) - 1);
+  uint32_t best = 0xFFFFFFFFu;
+  for (int p = 0; p <= k - m; ++p) {
+    const uint32_t sub = (uint32_t)(key >> (5 * (k - m - p))) & mask;
+    const uint32_t h = mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
+    best = best < h ? best : h;
+  }
+  return best;
+}
+
+// Home bucket = the key's MINIMIZER hashed onto [0, n_buckets) (Lemire fast range). Two
+// consecutive windows of a protein share their minimizer with probability 2/(K - m + 2)
+// (1/2 for K = 8, m = 6; 1/3 for m = 7), so they share their home bucket and one 64-byte
+// request serves both: the probe kernel walks runs of consecutive windows and requests a bucket
+// only when it changes. Exactness is kept by the full-key compare.
+__host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
+#ifdef KMA_HOME_FLAT  // A/B build only: hash of the whole key
+  const uint32_t h = mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u));
+  (void)k, (void)m;
+#else
+  const uint32_t h = mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
+#endif
   return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
 }
+
+// Minimizer length of a table of n_buckets buckets for K-mers. Keys sharing a minimizer share
+// a bucket, so the m-mer space must stay large against the table: with 20 amino acids, m = 6
+// gives 6.4e7 m-mers and overflows ~12% of keys past their home bucket at 1e8 keys, m = 7
+// keeps that at ~2.6% (and still shares a bucket between consecutive windows 1/3 of the time).
+// So m = 6 up to 2^22 buckets (16.8M keys at load factor 0.5), else 7 (m <= K). The table
+// layout depends on it; build and lookup both derive it from (K, n_buckets). Defined in
+// kma_abi.cpp (KMA_MINIMIZER=6|7 overrides it, for layout experiments only).
+int minimizer_len(int k, uint64_t n_buckets);
 
 // ---- kernel parameter blocks ------------------------------------------------------------------
 struct ProteinArgs {
@@ -46,6 +88,7 @@ struct ProteinArgs {
   uint32_t n_seq;
   uint64_t n_residues;  // offsets[n_seq] - offsets[0]
   int32_t k;
+  int32_t mlen;  // minimizer length of the table
   int32_t min_hits;
   uint32_t flags;
   int32_t* out_fid;
@@ -60,9 +103,13 @@ struct ProteinArgs {
   uint32_t reset_flag;      // K1 of the first segment clears overflow_flag
 };
 
-// K1 probe kernel: kProbeWin windows per thread per step, all first-bucket loads in flight.
+// K1 probe kernel: kProbeWin consecutive windows per lane per step (a run), all distinct
+// first-bucket loads in flight.
 constexpr int kProbeWin = 4;
 constexpr int kProbeBlocksPerCU = 8;
+// K1 defers overflow-chain walks to a per-wave LDS queue of kChainQ positions, resolved a
+// wave's 64 lanes at a time.
+constexpr int kChainQ = 384;
 // K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteWaves
 // proteins (kVoteWin words per lane per chunk) and an LDS pool of kVotePool u64 set entries.
 // Proteins whose set does not fit are finished by vote_long_kernel: one block each, an LDS set
@@ -87,6 +134,7 @@ struct ContigArgs {
   uint32_t n_contig;
   uint64_t total_bases;
   int32_t k;
+  int32_t mlen;
   const uint8_t* codon_codes;  // 64 entries (TCAG order): 5-bit aa code, 0 = stop
   uint64_t* staging;           // n_blocks x kContigTile*2 packed hits
   uint32_t* block_counts;      // n_blocks
@@ -96,11 +144,12 @@ struct ContigArgs {
 constexpr int kContigTile = 256;  // forward positions per block
 
 // ---- launchers (kma_kernels.hip) --------------------------------------------------------------
-hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets,
-                               const uint64_t* keys, uint64_t n, uint32_t* status,
+hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets, int k,
+                               int m, const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream);
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
-                                 uint32_t n_buckets, uint32_t* stats, hipStream_t stream);
+                                 uint32_t n_buckets, int k, int m, uint32_t* stats,
+                                 hipStream_t stream);
 hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K1
 hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream);   // K2 (segment)
 hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream);   // long proteins

@@ -92,7 +92,7 @@ __device__ __forceinline__ void scan_bucket(const uint4 (&q)[4], uint64_t key, b
   empty = false;
 #pragma unroll
   for (int j = 0; j < kSlotsPerBucket; ++j) {
-    const bool m = lo[j] == klo && (hi[j] & ~kFidMask) == khi;
+    const bool m = lo[j] == klo && (hi[j] & kKeyHiMask) == khi;
     fid = m ? (hi[j] & kFidMask) : fid;
     slot = m ? (uint32_t)j : slot;
     hit = hit || m;
@@ -109,30 +109,52 @@ __device__ __forceinline__ void load_bucket(const uint64_t* __restrict__ slots, 
   q[3] = bp[3];
 }
 
-// Full probe from the home bucket (chains included). Returns true on a hit.
-__device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint32_t n_buckets,
-                                      uint64_t key, uint32_t& fid) {
-  uint32_t b = home_bucket(key, n_buckets), slot = 0;
-  for (uint32_t step = 0; step < n_buckets; ++step) {  // bounded even for a full foreign table
+// The key's overflow bit in its home bucket (held in registers).
+__device__ __forceinline__ bool ovf_bit(const uint4 (&q)[4], uint64_t key) {
+  const uint32_t s = ovf_index((uint32_t)key);
+  const uint4 v = q[s >> 1];
+  return (((s & 1) ? v.w : v.y) & kOvfBit) != 0u;
+}
+
+// Walk the overflow chain after home bucket `b` (the key missed there and its overflow bit is
+// set): stop at the key or at the first bucket with an empty slot. Returns true on a hit.
+__device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, uint32_t n_buckets,
+                                           uint32_t b, uint64_t key, uint32_t& fid) {
+  bool hit = false, empty = false;
+  uint32_t slot = 0;
+  for (uint32_t step = 1; step < n_buckets && !hit && !empty; ++step) {  // bounded
+    b = (b + 1 == n_buckets) ? 0 : b + 1;
     uint4 q[4];
     load_bucket(slots, b, q);
-    bool hit, empty;
     scan_bucket(q, key, hit, empty, fid, slot);
-    if (hit) return true;
-    if (empty) return false;
-    b = (b + 1 == n_buckets) ? 0 : b + 1;
   }
-  return false;
+  return hit;
+}
+
+// Full probe from the home bucket (chains included). Returns true on a hit.
+__device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint32_t n_buckets,
+                                      int k, int m, uint64_t key, uint32_t& fid) {
+  const uint32_t b = home_bucket(key, k, m, n_buckets);
+  uint32_t slot = 0;
+  uint4 q[4];
+  load_bucket(slots, b, q);
+  bool hit, empty;
+  scan_bucket(q, key, hit, empty, fid, slot);
+  if (hit) return true;
+  if (!ovf_bit(q, key)) return false;
+  return walk_chain(slots, n_buckets, b, key, fid);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Table construction. Insert: claim the first empty slot of the probe chain with a 64-bit CAS
-// (slot key bits, fid still 0) or find the key already there; either way record the row index
-// with atomicMax so the LAST row of a duplicate key wins (HashMap.put semantics).
-// Finalize: write the winning row's fid into the slot; collect entry count and max probe.
+// (slot key bits, fid still 0; the slot's overflow bit may already be set) or find the key
+// already there; either way record the row index with atomicMax so the LAST row of a duplicate
+// key wins (HashMap.put semantics). A key placed past its home bucket sets its overflow bit
+// there. Finalize: write the winning row's fid into the slot; collect entry count and max
+// probe.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint32_t* winner,
-                                                           uint32_t n_buckets,
+                                                           uint32_t n_buckets, int k, int m,
                                                            const uint64_t* __restrict__ keys,
                                                            uint64_t n, uint32_t* status) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
@@ -140,15 +162,16 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
     const uint64_t key = keys[i];
     if (key == 0) continue;
     const uint64_t want = slot_make(key, 0);
-    uint32_t b = home_bucket(key, n_buckets);
+    const uint32_t home = home_bucket(key, k, m, n_buckets);
+    uint32_t b = home;
     bool done = false;
     for (uint32_t p = 0; p < n_buckets && !done; ++p) {
       for (int j = 0; j < kSlotsPerBucket; ++j) {
         uint64_t* sp = slots + (uint64_t)b * kSlotsPerBucket + j;
         uint64_t v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v == 0) {
-          const uint64_t old = atomicCAS((unsigned long long*)sp, 0ull, want);
-          v = old == 0 ? want : old;
+        while ((uint32_t)v == 0u) {  // empty (possibly with its overflow bit set): claim it
+          const uint64_t old = atomicCAS((unsigned long long*)sp, (unsigned long long)v, v | want);
+          v = old == v ? (v | want) : old;
         }
         if (slot_key(v) == key) {
           atomicMax(winner + (uint64_t)b * kSlotsPerBucket + j, (uint32_t)(i + 1));
@@ -156,16 +179,23 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
           break;
         }
       }
-      b = (b + 1 == n_buckets) ? 0 : b + 1;
+      if (!done) b = (b + 1 == n_buckets) ? 0 : b + 1;
     }
-    if (!done) atomicOr(status, 1u);  // table full: cannot happen at load factor < 1
+    if (!done) {
+      atomicOr(status, 1u);  // table full: cannot happen at load factor < 1
+    } else if (b != home) {
+      uint32_t* hi = reinterpret_cast<uint32_t*>(
+                         slots + (uint64_t)home * kSlotsPerBucket + ovf_index((uint32_t)key)) + 1;
+      atomicOr(hi, kOvfBit);
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
                                                              const uint32_t* __restrict__ winner,
                                                              const uint32_t* __restrict__ fids,
-                                                             uint32_t n_buckets, uint32_t* stats) {
+                                                             uint32_t n_buckets, int k, int m,
+                                                             uint32_t* stats) {
   const uint64_t n_slots = (uint64_t)n_buckets * kSlotsPerBucket;
   uint32_t entries = 0, max_probe = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_slots;
@@ -174,7 +204,7 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
     if (w == 0) continue;
     const uint64_t v = slots[i];
     slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
-    const uint32_t b = (uint32_t)(i / kSlotsPerBucket), h = home_bucket(slot_key(v), n_buckets);
+    const uint32_t b = (uint32_t)(i / kSlotsPerBucket), h = home_bucket(slot_key(v), k, m, n_buckets);
     const uint32_t d = (b >= h ? b - h : b + n_buckets - h) + 1u;
     entries++;
     max_probe = max(max_probe, d);
@@ -196,7 +226,7 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 // Residue loads are unconditional (a lane past the end re-reads position 0) so that no loaded
 // register is merged on a branch join, which would force a vmcnt(0) per load.
 // ---------------------------------------------------------------------------------------------
-template <int K, int U>
+template <int K, int M, int U>
 __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
   const int t = threadIdx.x;
@@ -224,7 +254,7 @@ __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       ok[j] = pack_window<K>(lut, bytes[j], key[j]) && g0 + j * 256 + t < n_pos;
-      bk[j] = home_bucket(key[j], nb);
+      bk[j] = home_bucket(key[j], K, M, nb);
     }
     uint4 q[U][4];  // undefined on lanes that do not probe: consumed unconditionally below
 #pragma unroll
@@ -236,15 +266,8 @@ __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
       uint32_t fid = 0, slot = 0;
       scan_bucket(q[j], key[j], hit, empty, fid, slot);
       hit = ok[j] && hit;
-      if (ok[j] && !hit && !empty) {  // rare: walk the chain past a full home bucket
-        uint32_t b = bk[j];
-        for (uint32_t step = 1; step < nb && !hit && !empty; ++step) {
-          b = (b + 1 == nb) ? 0 : b + 1;
-          uint4 qq[4];
-          load_bucket(slots, b, qq);
-          scan_bucket(qq, key[j], hit, empty, fid, slot);
-        }
-      }
+      if (ok[j] && !hit && ovf_bit(q[j], key[j]))  // rare: walk the overflow chain
+        hit = walk_chain(slots, nb, bk[j], key[j], fid);
       const uint64_t g = g0 + j * 256 + t;
       if (g < n_pos) a.hits[g] = hit ? fid + 1u : 0u;
     }
@@ -252,27 +275,77 @@ __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K1, quad-cooperative form. Each lane packs the key of its own windows, then the four lanes
-// of a quad probe their four windows' buckets together: for the window of quad lane r, lane p
-// loads bytes [16p, 16p + 16) of the bucket (one dwordx4), so one wave instruction reads 16
-// whole 64-byte lines (the access shape with the higher measured random-gather rate, and 4x
-// fewer VGPRs per probe than a lane reading a whole bucket). Matches are combined with DPP
-// quad reductions and kept by the window's owner lane. Overflow chains (rare) are walked by
-// the owner lane alone.
+// K1, quad-cooperative form (default). Each lane packs the key of its own windows, then the
+// four lanes of a quad probe their four windows' buckets together: for the window of quad lane
+// r, lane p loads bytes [16p, 16p + 16) of the bucket (one dwordx4), so one wave instruction
+// reads 16 whole 64-byte lines (the access shape with the higher measured random-gather rate,
+// and 4x fewer VGPRs per probe than a lane reading a whole bucket). Matches are combined with
+// DPP quad reductions and kept by the window's owner lane. Adjacent lanes hold consecutive
+// windows, which share their minimizer home bucket half of the time: the repeated line is
+// served by the CU's L1/L2 instead of HBM. Overflow chains (~1% of probes) are deferred to the
+// wave's chain queue.
 // ---------------------------------------------------------------------------------------------
 template <int R>
 __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, R * 0x55, 0xF, 0xF, false);
 }
-__device__ __forceinline__ uint32_t quad_max(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
-  return max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+__device__ __forceinline__ uint32_t quad_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
 }
 
-template <int K, int U>
+// One quad's verdict on a bucket it loaded cooperatively (lane `part` holds slots 2part and
+// 2part + 1 in v) for key (kl, kh): fid + 1 of the matching slot (0 = not in this bucket), with
+// bit 31 = the key's overflow bit (chain walk needed if there is no match). Keys are unique in
+// a table, so at most one lane matches and OR is the reduction. Every lane of the quad must
+// call it (DPP). Branch-free on purpose: a short-circuit here lets the compiler split the
+// 16-byte load into a lazily loaded tail behind a branch and a vmcnt(0).
+__device__ __forceinline__ uint32_t match_part(const uint4 v, uint32_t kl, uint32_t kh,
+                                               uint32_t part) {
+  const uint32_t m0 = (uint32_t)(v.x == kl) & (uint32_t)((v.y & kKeyHiMask) == kh);
+  const uint32_t m1 = (uint32_t)(v.z == kl) & (uint32_t)((v.w & kKeyHiMask) == kh);
+  uint32_t w = (m0 * ((v.y & kFidMask) + 1u)) | (m1 * ((v.w & kFidMask) + 1u));
+  const uint32_t ob = ovf_index(kl);
+  const uint32_t hi = (ob & 1u) ? v.w : v.y;
+  w |= (uint32_t)((ob >> 1) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
+  return quad_or(w);
+}
+
+// Deferred overflow-chain walks (K1). A window whose home bucket misses with the key's overflow
+// bit set is written as a miss and its position queued in the wave's LDS slice; the wave
+// resolves its queue 64 walks at a time (one lane each: re-pack the key, walk the chain with
+// whole-bucket loads, overwrite the word), so the walk's dependent latency is paid once per
+// ~64 walks rather than once per probe step.
+__device__ __forceinline__ void chain_push(uint64_t* q, uint32_t& n, bool pend, uint64_t g) {
+  const uint64_t m = __ballot(pend);
+  if (pend) q[n + popc_below(m)] = g;
+  n += (uint32_t)__popcll(m);
+}
+template <int K, int M>
+__device__ __forceinline__ void chain_flush(const ProteinArgs& a, const uint8_t* lut,
+                                         const uint8_t* __restrict__ res, const uint64_t* q,
+                                         uint32_t n) {
+  __builtin_amdgcn_wave_barrier();  // queue writes of other lanes are visible (LDS in order)
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t e = lane; e < n; e += 64) {
+    const uint64_t g = q[e];
+    uint64_t key;
+    pack_window<K>(lut, window_bytes(res, g), key);
+    uint32_t fid = 0;
+    const bool hit = walk_chain(a.slots, a.n_buckets, home_bucket(key, K, M, a.n_buckets), key,
+                                fid);
+    a.hits[g] = hit ? fid + 1u : 0u;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int K, int M, int U>
 __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
+  __shared__ uint64_t chain_q[4][kChainQ];
   const int t = threadIdx.x, part = t & 3;
+  uint64_t* cq = chain_q[t >> 6];
+  uint32_t cn = 0;  // wave-uniform queue length
   if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
@@ -305,7 +378,7 @@ __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
                       g0 + j * 256 + t < n_pos;
       klo[j] = (uint32_t)key;
       khi[j] = (uint32_t)(key >> 32) << 24;
-      bk[j] = ok ? home_bucket(key, nb) : kNone;
+      bk[j] = ok ? home_bucket(key, K, M, nb) : kNone;
     }
     // Cooperative loads: all 4U dwordx4 of the lane in flight before any compare. A window
     // that does not probe reads bucket 0 (its result is discarded): no branch-merged loads.
@@ -327,11 +400,10 @@ __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
       const uint64_t g = g0 + stride + j * 256 + t;
       ww[j] = window_words(res, g < n_pos ? g : 0);
     }
-    uint32_t word[U], full[U];
+    uint32_t word[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       word[j] = 0;
-      full[j] = 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t kl = r == 0 ? quad_bcast<0>(klo[j]) : r == 1 ? quad_bcast<1>(klo[j])
@@ -340,35 +412,150 @@ __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
                           : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
         // Branch-free on purpose: a short-circuit here lets the compiler split the 16-byte
         // load into a lazily loaded tail behind a branch and a vmcnt(0).
-        const uint4 v = q[j][r];
-        const uint32_t m0 = (uint32_t)(v.x == kl) & (uint32_t)((v.y & ~kFidMask) == kh);
-        const uint32_t m1 = (uint32_t)(v.z == kl) & (uint32_t)((v.w & ~kFidMask) == kh);
-        uint32_t w = (m0 * ((v.y & kFidMask) + 1u)) | (m1 * ((v.w & kFidMask) + 1u));
-        uint32_t f = (uint32_t)(v.x != 0u) & (uint32_t)(v.z != 0u);  // no empty slot here
-        w = quad_max(w);
-        f = 1u - quad_max(1u - f);  // quad min: 1 iff the whole bucket is full
-        word[j] = part == r ? w : word[j];
-        full[j] = part == r ? f : full[j];
+        const uint32_t x = match_part(q[j][r], kl, kh, part);
+        word[j] = part == r ? x : word[j];
       }
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint64_t g = g0 + j * 256 + t;
-      if (bk[j] != kNone && word[j] == 0u && full[j]) {  // rare: chain past a full home bucket
-        const uint64_t key = ((uint64_t)(khi[j] >> 24) << 32) | klo[j];
-        uint32_t b = bk[j], fid = 0, slot = 0;
-        bool hit = false, empty = false;
-        for (uint32_t step = 1; step < nb && !hit && !empty; ++step) {
-          b = (b + 1 == nb) ? 0 : b + 1;
-          uint4 qq[4];
-          load_bucket(slots, b, qq);
-          scan_bucket(qq, key, hit, empty, fid, slot);
-        }
-        word[j] = hit ? fid + 1u : 0u;
-      }
-      if (g < n_pos) a.hits[g] = bk[j] != kNone ? word[j] : 0u;
+      if (g < n_pos) a.hits[g] = bk[j] != kNone ? word[j] & 0x7FFFFFFFu : 0u;
+      chain_push(cq, cn, bk[j] != kNone && word[j] == 0x80000000u, g);  // rare: chain walk
+    }
+    if (cn > kChainQ - 64 * U) {
+      chain_flush<K, M>(a, lut, res, cq, cn);
+      cn = 0;
     }
   }
+  if (cn) chain_flush<K, M>(a, lut, res, cq, cn);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1, run form (KMA_PROBE=run). Each lane takes R consecutive windows (a run); with minimizer home
+// buckets consecutive windows often share their bucket, so a bucket is requested only where
+// the run's bucket changes — a repeated one reads the (cache-hot) bucket 0 line instead and
+// reuses the registers of the previous window. Loads are quad-cooperative as in
+// probe_quad_kernel (the four lanes of a quad read one bucket, a dwordx4 each), all distinct
+// loads of the step in flight before any compare, and the next step's residues are loaded
+// under them. One 24-byte residue read per lane covers its R + K - 1 residues; the run's R
+// result words leave in one 16-byte store.
+// ---------------------------------------------------------------------------------------------
+template <int K, int M, int R>
+__global__ __launch_bounds__(256) void probe_run_kernel(ProteinArgs a) {
+  static_assert(R + K - 1 + 7 <= 24, "a run's residues must fit three aligned words");
+  __shared__ uint8_t lut[256];
+  __shared__ uint64_t chain_q[4][kChainQ];
+  const int t = threadIdx.x, part = t & 3;
+  uint64_t* cq = chain_q[t >> 6];
+  uint32_t cn = 0;  // wave-uniform queue length
+  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
+  lut[t] = a.lut[t];
+  __syncthreads();
+  const uint64_t o0 = a.offsets[0];
+  const uint64_t n_all = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint64_t seg_hi = a.offsets[a.seq_hi] - o0;
+  const uint64_t n_pos = seg_hi < n_all ? seg_hi : n_all;
+  const uint8_t* __restrict__ res = a.residues + o0;
+  const uint64_t* __restrict__ slots = a.slots;
+  const uint4* __restrict__ part_base = reinterpret_cast<const uint4*>(slots) + part;
+  const uint32_t nb = a.n_buckets;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const uint64_t stride = (uint64_t)gridDim.x * (256 * R);
+  uint64_t g0 = (a.offsets[a.seq_lo] - o0) + (uint64_t)blockIdx.x * (256 * R);
+  // Residue words of this lane's run, loaded one step ahead.
+  uint64_t rw[3];
+  uint32_t rsh;
+  {
+    const uint64_t gl = g0 + (uint64_t)t * R, gc = gl < n_pos ? gl : 0;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (gc & ~7ull));
+    rw[0] = src[0];
+    rw[1] = src[1];
+    rw[2] = src[2];
+    rsh = (uint32_t)(gc & 7);
+  }
+  for (; g0 < n_pos; g0 += stride) {
+    const uint64_t gl = g0 + (uint64_t)t * R;
+    uint32_t klo[R], khi[R], bk[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t o = rsh + j;  // byte offset of window j in the 24-byte stream
+      const uint64_t bytes = o < 8 ? funnel(rw[0], rw[1], o * 8) : funnel(rw[1], rw[2], (o - 8) * 8);
+      uint64_t key;
+      const bool ok = pack_window<K>(lut, bytes, key) && gl + j < n_pos;
+      klo[j] = (uint32_t)key;
+      khi[j] = (uint32_t)(key >> 32) << 24;
+      bk[j] = ok ? home_bucket(key, K, M, nb) : kNone;
+    }
+    // Distinct buckets along the run: window j requests only if its bucket differs from j-1's.
+    uint32_t fresh[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      fresh[j] = bk[j] != kNone && (j == 0 || bk[j] != bk[j - 1]) ? 1u : 0u;
+    uint4 q[R][4];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t b = r == 0 ? quad_bcast<0>(bk[j]) : r == 1 ? quad_bcast<1>(bk[j])
+                         : r == 2 ? quad_bcast<2>(bk[j]) : quad_bcast<3>(bk[j]);
+        const uint32_t f = r == 0 ? quad_bcast<0>(fresh[j]) : r == 1 ? quad_bcast<1>(fresh[j])
+                         : r == 2 ? quad_bcast<2>(fresh[j]) : quad_bcast<3>(fresh[j]);
+        q[j][r] = part_base[(uint64_t)(f ? b : 0u) * 4];  // repeated bucket: hot line 0
+      }
+    }
+    // Next step's residues under the bucket loads (raw words: consumed next step).
+    {
+      const uint64_t gn = gl + stride, gc = gn < n_pos ? gn : 0;
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (gc & ~7ull));
+      rw[0] = src[0];
+      rw[1] = src[1];
+      rw[2] = src[2];
+      rsh = (uint32_t)(gc & 7);
+    }
+    uint32_t word[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      word[j] = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t f = r == 0 ? quad_bcast<0>(fresh[j]) : r == 1 ? quad_bcast<1>(fresh[j])
+                         : r == 2 ? quad_bcast<2>(fresh[j]) : quad_bcast<3>(fresh[j]);
+        if (j > 0) {  // a repeated bucket takes the previous window's data (selects, no branch)
+          q[j][r].x = f ? q[j][r].x : q[j - 1][r].x;
+          q[j][r].y = f ? q[j][r].y : q[j - 1][r].y;
+          q[j][r].z = f ? q[j][r].z : q[j - 1][r].z;
+          q[j][r].w = f ? q[j][r].w : q[j - 1][r].w;
+        }
+        const uint32_t kl = r == 0 ? quad_bcast<0>(klo[j]) : r == 1 ? quad_bcast<1>(klo[j])
+                          : r == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
+        const uint32_t kh = r == 0 ? quad_bcast<0>(khi[j]) : r == 1 ? quad_bcast<1>(khi[j])
+                          : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
+        // Branch-free on purpose (a short-circuit lets the compiler split the 16-byte load).
+        const uint32_t x = match_part(q[j][r], kl, kh, part);
+        word[j] = part == r ? x : word[j];
+      }
+    }
+    bool pend[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      pend[j] = bk[j] != kNone && word[j] == 0x80000000u;  // rare: chain walk, deferred
+      word[j] = bk[j] != kNone ? word[j] & 0x7FFFFFFFu : 0u;
+    }
+    if (R == 4 && gl + R <= n_pos && (gl & 3) == 0) {
+      *reinterpret_cast<uint4*>(a.hits + gl) = make_uint4(word[0], word[1], word[2], word[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (gl + j < n_pos) a.hits[gl + j] = word[j];
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) chain_push(cq, cn, pend[j], gl + j);
+    if (cn > kChainQ - 64 * R) {
+      chain_flush<K, M>(a, lut, res, cq, cn);
+      cn = 0;
+    }
+  }
+  if (cn) chain_flush<K, M>(a, lut, res, cq, cn);
 }
 
 // Open-addressing set of distinct hit keys (u64, 0 = empty) in LDS or global memory, capacity a
@@ -800,8 +987,8 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
       kp = (kp << 5) | cp;
       km |= (uint64_t)cm << (5 * j);
     }
-    hp = pv && probe(a.slots, a.n_buckets, kp, fp);
-    hm = mv && probe(a.slots, a.n_buckets, km, fm);
+    hp = pv && probe(a.slots, a.n_buckets, k, a.mlen, kp, fp);
+    hm = mv && probe(a.slots, a.n_buckets, k, a.mlen, km, fm);
     if (a.tally) {
       if (hp && fp < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fp, 1u);
       if (hm && fm < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fm, 1u);
@@ -838,7 +1025,7 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a,
     kma_hit h;
     h.contig = c;
     h.left = (int32_t)(x + 1);
-    h.fid = (uint32_t)v & kFidMask;
+    h.fid = (uint32_t)v & 0xFFFFFFu;
     h.strand = minus ? '-' : '+';
     h.frame = (uint8_t)((minus ? (len - 3 * a.k - x) : x) % 3 + 1);
     h.pad = 0;
@@ -854,33 +1041,36 @@ static unsigned grid_for(uint64_t n, unsigned cap = 8192) {
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
-hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets,
-                               const uint64_t* keys, uint64_t n, uint32_t* status,
+hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets, int k,
+                               int m, const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream) {
   hipLaunchKernelGGL(build_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream, slots, winner,
-                     n_buckets, keys, n, status);
+                     n_buckets, k, m, keys, n, status);
   return hipGetLastError();
 }
 
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
-                                 uint32_t n_buckets, uint32_t* stats, hipStream_t stream) {
+                                 uint32_t n_buckets, int k, int m, uint32_t* stats,
+                                 hipStream_t stream) {
   hipLaunchKernelGGL(build_finalize_kernel,
                      dim3(grid_for((uint64_t)n_buckets * kSlotsPerBucket)), dim3(256), 0, stream,
-                     slots, winner, fids, n_buckets, stats);
+                     slots, winner, fids, n_buckets, k, m, stats);
   return hipGetLastError();
 }
 
-// K1 access shape: quad-cooperative (default) or one lane per bucket (KMA_PROBE=lane).
-static bool probe_lane_shape() {
-  static const bool lane = [] {
+// K1 form: quad-cooperative loads, one window per lane per step (default; measured fastest),
+// or KMA_PROBE=run (runs of consecutive windows, repeated buckets not re-requested) /
+// KMA_PROBE=lane (a lane reads a whole bucket).
+static int probe_form() {
+  static const int form = [] {
     const char* e = getenv("KMA_PROBE");
-    return e && e[0] == 'l';
+    return !e ? 1 : e[0] == 'l' ? 2 : e[0] == 'r' ? 0 : 1;
   }();
-  return lane;
+  return form;
 }
 
-template <int K>
-static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+template <int K, int M>
+static hipError_t launch_probe_km(const ProteinArgs& a, int n_cu, hipStream_t stream) {
   // Grid from the batch average (the host does not see the segment's residue count).
   const uint64_t seg = a.seq_hi - a.seq_lo;
   const uint64_t n_pos = a.n_seq ? a.n_residues / a.n_seq * seg + 1 : 0;
@@ -889,11 +1079,25 @@ static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t str
   const uint64_t cap = (uint64_t)n_cu * kProbeBlocksPerCU;
   if (!want || a.n_residues < (uint64_t)K) return hipSuccess;
   const dim3 grid((unsigned)(want < cap ? want : cap));
-  if (probe_lane_shape())
-    hipLaunchKernelGGL((probe_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL((probe_quad_kernel<K, kProbeWin>), grid, dim3(256), 0, stream, a);
+  switch (probe_form()) {
+    case 2: hipLaunchKernelGGL((probe_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a); break;
+    case 1:
+      hipLaunchKernelGGL((probe_quad_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a);
+      break;
+    default:
+      hipLaunchKernelGGL((probe_run_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a);
+  }
   return hipGetLastError();
+}
+
+// Minimizer length is a template parameter of K1: m = min(K, 6), or 7 for large tables.
+template <int K>
+static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  constexpr int M6 = K < 6 ? K : 6;
+  constexpr int M7 = K < 7 ? M6 : 7;
+  if (a.mlen == M7 && M7 != M6) return launch_probe_km<K, M7>(a, n_cu, stream);
+  if (a.mlen != M6) return hipErrorInvalidValue;
+  return launch_probe_km<K, M6>(a, n_cu, stream);
 }
 
 template <int K>

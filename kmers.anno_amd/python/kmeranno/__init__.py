@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(PKG_ROOT, "build", "libkmeranno.so")
+LIB_PATH = os.environ.get("KMERANNO_LIB") or os.path.join(PKG_ROOT, "build", "libkmeranno.so")
 
 OK = 0
 E_INVALID, E_DEVICE, E_NOMEM, E_CAPACITY, E_ALPHABET, E_TABLE_FULL = -1, -2, -3, -4, -5, -6
@@ -44,7 +44,7 @@ class TableInfo(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_skipped", C.c_uint64), ("n_entries", C.c_uint64),
                 ("n_buckets", C.c_uint64), ("bytes", C.c_uint64), ("k", C.c_int32),
                 ("device", C.c_int32), ("max_probe", C.c_uint32), ("n_extra_syms", C.c_uint32),
-                ("extra_syms", C.c_uint8 * 4)]
+                ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
@@ -77,7 +77,7 @@ def load(path: str | None = None):
         L.kma_table_destroy.argtypes = [_vp]
         L.kma_table_buckets_for.restype = _u64
         L.kma_table_buckets_for.argtypes = [_u64, C.c_double]
-        L.kma_table_build_device.argtypes = [_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp]
+        L.kma_table_build_device.argtypes = [_vp, _u64, _int, _vp, _vp, _vp, _u64, _vp, _vp]
         L.kma_table_wrap_device.argtypes = [_vp, _u64, _int, _int, C.POINTER(_vp)]
         L.kma_table_device_ptr.argtypes = [_vp, C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
@@ -110,12 +110,12 @@ def device_count() -> int:
 
 
 def pack_strings(strs):
-    """Concatenate strings -> (uint8 buffer padded by 16 bytes, uint64 offsets)."""
+    """Concatenate strings -> (uint8 buffer padded by 32 bytes, uint64 offsets)."""
     bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
     offsets = np.zeros(len(bs) + 1, dtype=np.uint64)
     if bs:
         offsets[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
-    buf = np.frombuffer(b"".join(bs) + b"\0" * 16, dtype=np.uint8).copy()
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 32, dtype=np.uint8).copy()
     return buf, offsets
 
 
@@ -238,8 +238,8 @@ def buckets_for(n_keys: int, load_factor: float = 0.5) -> int:
 
 
 def build_device(d_slots: int, n_buckets: int, d_winner: int, d_keys: int, d_fids: int, n: int,
-                 d_status: int, stream: int = 0):
-    _check(load().kma_table_build_device(d_slots, n_buckets, d_winner, d_keys, d_fids, n,
+                 d_status: int, stream: int = 0, k: int = 8):
+    _check(load().kma_table_build_device(d_slots, n_buckets, k, d_winner, d_keys, d_fids, n,
                                          d_status, stream or None))
 
 

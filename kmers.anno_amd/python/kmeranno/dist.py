@@ -27,11 +27,11 @@ def shard_bounds(offsets: np.ndarray, world: int) -> np.ndarray:
 
 
 def shard(residues: np.ndarray, offsets: np.ndarray, world: int, rank: int):
-    """(residues slice padded by 16 bytes, rebased offsets, first protein index) of a shard."""
+    """(residues slice padded by 32 bytes, rebased offsets, first protein index) of a shard."""
     b = shard_bounds(offsets, world)
     lo, hi = int(b[rank]), int(b[rank + 1])
     r0, r1 = int(offsets[lo]), int(offsets[hi])
-    res = np.concatenate([residues[r0:r1], np.zeros(16, np.uint8)])
+    res = np.concatenate([residues[r0:r1], np.zeros(32, np.uint8)])
     off = (offsets[lo:hi + 1] - np.uint64(r0)).astype(np.uint64)
     return res, off, lo
 

@@ -50,7 +50,7 @@ class Workload:
     keys: np.ndarray       # uint64 [T] packed table kmers (file order)
     fids: np.ndarray       # uint32 [T]
     n_fid: int
-    residues: np.ndarray   # uint8 ASCII, padded by 16 zero bytes
+    residues: np.ndarray   # uint8 ASCII, padded by 32 zero bytes
     offsets: np.ndarray    # uint64 [n_seq + 1]
     kinds: np.ndarray      # uint8 [n_seq]: 0 copy, 1 random, 2 chimera
     true_fid: np.ndarray   # int32 [n_seq]: source function (-1 random)
@@ -113,7 +113,7 @@ def make_table(table_size: int, n_fid: int, seed: int, k: int = 8) -> SignatureS
 
 
 def make_queries(sig: SignatureSet, n_seq: int, seed: int, mutation: float = 0.10):
-    """(residues padded by 16 bytes, offsets, kinds, true_fid) for one batch."""
+    """(residues padded by 32 bytes, offsets, kinds, true_fid) for one batch."""
     rng = np.random.default_rng(seed)
     lens = cds_lengths()
     protos, n_fid = sig.protos, sig.n_fid
@@ -135,7 +135,7 @@ def make_queries(sig: SignatureSet, n_seq: int, seed: int, mutation: float = 0.1
                                 mutation))
     offsets = np.zeros(n_seq + 1, np.uint64)
     offsets[1:] = np.cumsum([len(s) for s in seqs])
-    residues = np.concatenate(seqs + [np.zeros(16, np.uint8)])
+    residues = np.concatenate(seqs + [np.zeros(32, np.uint8)])
     return residues, offsets, kinds, true_fid
 
 

@@ -62,7 +62,7 @@ def pack_strings(strs):
     bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strs]
     offsets = np.zeros(len(bs) + 1, dtype=np.uint64)
     offsets[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
-    buf = np.frombuffer(b"".join(bs) + b"\0" * 16, dtype=np.uint8).copy()
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 32, dtype=np.uint8).copy()
     return buf, offsets
 
 

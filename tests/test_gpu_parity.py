@@ -86,7 +86,7 @@ def test_config1_golden(kma, flags):
     assert (tally == np.bincount(called, minlength=100)).all()
 
 
-@pytest.mark.parametrize("lf", [0.5, 0.9])
+@pytest.mark.parametrize("lf", [0.5, 0.9, 0.95])
 def test_synthetic_vs_oracle(kma, oracle_c, lf):
     """2,000 proteins vs a 200k-entry table (seeded), packed-key table path, two load factors
     (0.9 forces multi-bucket probe chains)."""
