@@ -28,6 +28,12 @@ int kma::minimizer_len(int k, uint64_t n_buckets) {
   return n_buckets <= (1ull << 22) ? m6 : m7;
 }
 
+constexpr uint64_t kHitsPad = 64;
+// A protein goes to vote_long_kernel only if its set needs more than K2's LDS gives one
+// protein (> kWaveSet / 2, resp. > kVotePool / 2 hits), so it has more than 128 windows.
+static_assert(kma::kWaveSet >= 256 && kma::kVotePool >= 256, "pending list bound");
+uint64_t pending_cap(uint64_t n_residues) { return n_residues / 128 + 64; }
+
 struct kma_table {
   int device = 0;
   int k = 8;
@@ -46,6 +52,7 @@ struct kma_workspace {
   uint32_t* d_flag = nullptr;
   uint64_t* d_scratch = nullptr;
   uint32_t* d_hits = nullptr;  // K1 words: one u32 per residue position
+  uint32_t* d_pending = nullptr;  // K2 -> vote_long list (a pending protein has > 128 windows)
   uint64_t hits_cap = 0;
   // Segmented overlap: K2 of segment i on `side` while K1 of segment i + 1 runs on the call's
   // stream (fork/join through events, graph-capturable).
@@ -418,6 +425,8 @@ int kma_workspace_create(int device, kma_workspace** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 8);
+  if (e == hipSuccess) e = hipMalloc(&w->d_hits, kHitsPad * 4);  // reserve() grows it
+  if (e == hipSuccess) e = hipMalloc(&w->d_pending, pending_cap(0) * 4);
   if (e != hipSuccess) {
     if (w->d_flag) (void)hipFree(w->d_flag);
     delete w;
@@ -429,13 +438,17 @@ int kma_workspace_create(int device, kma_workspace** out) {
 
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
-  if (n_residues <= ws->hits_cap) return KMA_OK;
+  if (ws->d_hits && n_residues <= ws->hits_cap) return KMA_OK;
   DeviceScope ds(ws->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   if (ws->d_hits) (void)hipFree(ws->d_hits);
   ws->d_hits = nullptr;
   ws->hits_cap = 0;
-  KMA_HIP(hipMalloc(&ws->d_hits, n_residues * 4));
+  if (ws->d_pending) (void)hipFree(ws->d_pending);
+  ws->d_pending = nullptr;
+  // Padded by kHitsPad words (never empty): K2 may read word 0 for a chunk past the end.
+  KMA_HIP(hipMalloc(&ws->d_hits, (n_residues + kHitsPad) * 4));
+  KMA_HIP(hipMalloc(&ws->d_pending, pending_cap(n_residues) * 4));
   ws->hits_cap = n_residues;
   return KMA_OK;
 }
@@ -484,6 +497,7 @@ int kma_workspace_destroy(kma_workspace* ws) {
   (void)hipFree(ws->d_flag);
   (void)hipFree(ws->d_scratch);
   if (ws->d_hits) (void)hipFree(ws->d_hits);
+  if (ws->d_pending) (void)hipFree(ws->d_pending);
   delete ws;
   return KMA_OK;
 }
@@ -526,6 +540,7 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   a.n_fid = d_tally ? n_fid : 0;
   a.hits = ws->d_hits;
   a.overflow_flag = ws->d_flag;
+  a.pending = ws->d_pending;
   a.scratch = ws->d_scratch;
   hipEvent_t* ev = nullptr;
   if (ws->timing) {
@@ -560,6 +575,18 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
       KMA_HIP(kma::launch_vote(a, ws->n_cu, ws->side));
     } else {
       KMA_HIP(kma::launch_vote(a, ws->n_cu, s));
+#ifdef KMA_VOTE_TRACE  // experiment builds only: per-block phase clocks of K2 -> file
+      if (const char* f = getenv("KMA_TRACE_FILE")) {
+        const uint64_t nb = (n_seq + kma::kVoteProteins - 1) / kma::kVoteProteins;
+        std::vector<uint64_t> tr(nb * 8);
+        KMA_HIP(hipStreamSynchronize(s));
+        KMA_HIP(hipMemcpy(tr.data(), ws->d_scratch, tr.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* o = fopen(f, "wb")) {
+          fwrite(tr.data(), 8, tr.size(), o);
+          fclose(o);
+        }
+      }
+#endif
     }
   }
   if (S > 1) {

@@ -97,7 +97,8 @@ struct ProteinArgs {
   uint32_t* tally;  // may be null
   uint32_t n_fid;
   uint32_t* hits;           // workspace: fid + 1 (0 = miss) per residue position
-  uint32_t* overflow_flag;  // workspace: set when a protein needs the global dedupe pass
+  uint32_t* overflow_flag;  // workspace: length of `pending` (K1 zeroes it)
+  uint32_t* pending;        // workspace: proteins left to vote_long_kernel
   uint64_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u64
   uint32_t seq_lo, seq_hi;  // the segment [seq_lo, seq_hi) of proteins this launch covers
   uint32_t reset_flag;      // K1 of the first segment clears overflow_flag
@@ -110,18 +111,48 @@ constexpr int kProbeBlocksPerCU = 8;
 // K1 defers overflow-chain walks to a per-wave LDS queue of kChainQ positions, resolved a
 // wave's 64 lanes at a time.
 constexpr int kChainQ = 384;
-// K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteWaves
-// proteins (kVoteWin words per lane per chunk) and an LDS pool of kVotePool u64 set entries.
+// K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteProteins
+// proteins (kVoteWin consecutive windows per lane per chunk; a wave's first kVoteHold chunks
+// stay in registers between the passes) and an LDS pool of kVotePool u64 set entries.
 // Proteins whose set does not fit are finished by vote_long_kernel: one block each, an LDS set
 // of kLongSet keys, else kFallbackCap keys of workspace scratch per block.
+// (The KMA_VOTE_* macros exist for tuning builds: `make variant`.)
+#ifndef KMA_VOTE_WAVES
+#define KMA_VOTE_WAVES 4
+#endif
+#ifndef KMA_VOTE_PROTEINS
+#define KMA_VOTE_PROTEINS 8
+#endif
+#ifndef KMA_VOTE_POOL
+#define KMA_VOTE_POOL 2048
+#endif
+#ifndef KMA_VOTE_HOLD
+#define KMA_VOTE_HOLD 2
+#endif
 constexpr int kWavesPerBlock = 4;
 constexpr int kVoteWin = 4;
 constexpr int kChunk = 64 * kVoteWin;
-constexpr int kVoteWaves = 8;
-constexpr int kVotePool = 4096;
+constexpr int kVoteWaves = KMA_VOTE_WAVES;
+constexpr int kVoteProteins = KMA_VOTE_PROTEINS;
+constexpr int kVotePool = KMA_VOTE_POOL;
+constexpr int kVoteHold = KMA_VOTE_HOLD;
 constexpr int kLongSet = 8192;
-constexpr uint8_t kStatusPending = 0xFF;
+// K2 wave form: kWaveProteins proteins per wave, kWaveHold chunks held in registers, an LDS set
+// slice of kWaveSet u64 per wave (4 waves per block).
+#ifndef KMA_WAVE_PROTEINS
+#define KMA_WAVE_PROTEINS 1
+#endif
+#ifndef KMA_WAVE_HOLD
+#define KMA_WAVE_HOLD 2
+#endif
+#ifndef KMA_WAVE_SET
+#define KMA_WAVE_SET 512
+#endif
+constexpr int kWaveProteins = KMA_WAVE_PROTEINS;
+constexpr int kWaveHold = KMA_WAVE_HOLD;
+constexpr int kWaveSet = KMA_WAVE_SET;
 constexpr uint32_t kDeferred = 1u << 31;  // K2: set taken from the whole pool in phase 3
+constexpr uint32_t kLongCap = 0xFFFFFFFFu;  // K2: set too large for the pool (vote_long_kernel)
 constexpr int kLongBlocksPerCU = 4;
 constexpr int kFallbackBlocks = 64;
 constexpr uint32_t kFallbackCap = 1u << 17;  // u64 entries per block (1 MiB)

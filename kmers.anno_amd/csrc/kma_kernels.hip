@@ -24,20 +24,29 @@
 namespace kma {
 namespace {
 
+// Wave-wide reductions (all 64 lanes active; result wave-uniform): DPP inside each row of 16
+// lanes (quad swaps, half-row and row mirrors: ALU-speed, no LDS round trip as ds_bpermute
+// takes), then the four row results by readlane.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));   // [2,3,0,1]
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false));  // half mirror
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false));  // row mirror
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return op(op(r0, r1), op(r2, r3));
+}
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-  return v;
+  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-  return v;
+  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x + y; });
 }
 // Number of set bits of m in lanes below this lane (v_mbcnt).
 __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
@@ -572,6 +581,19 @@ __device__ __forceinline__ bool set_insert(unsigned long long* set, uint32_t mas
     h = (h + 1u) & mask;
   }
 }
+// Set capacity for h keys: a power of two >= 2h (linear probing stays short at load <= 1/2;
+// tighter sets measured slower: LDS CAS retries are dependent round trips).
+__device__ __forceinline__ uint32_t set_cap(uint32_t h) {
+  uint32_t cap = 8;
+  while (cap < 2 * h) cap <<= 1;
+  return cap;
+}
+
+// A protein whose distinct-key set does not fit K2's LDS: appended to the workspace's pending
+// list (its length is the word K1 zeroes), voted by vote_long_kernel.
+__device__ __forceinline__ void push_pending(const ProteinArgs& a, uint32_t s) {
+  a.pending[atomicAdd(a.overflow_flag, 1u)] = s;
+}
 
 __device__ __forceinline__ void write_vote(const ProteinArgs& a, uint32_t s, uint32_t mn,
                                            uint32_t mx, uint32_t cnt) {
@@ -635,56 +657,109 @@ __device__ __forceinline__ void vote_range(const ProteinArgs& a, const uint8_t* 
   }
 }
 
-// One chunk of kChunk windows of a protein (a wave, kVoteWin per lane, all loads in flight):
-// every hit window's key is re-packed from the residues and inserted in `set`; returns the
-// wave's number of new keys.
-template <int K>
-__device__ __forceinline__ uint32_t dedupe_chunk(const ProteinArgs& a, const uint8_t* lut,
-                                                 unsigned long long* set, uint32_t mask,
-                                                 uint64_t beg, int64_t n_win, int64_t w0,
-                                                 int lane) {
-  constexpr int V = kVoteWin;
-  const uint32_t* __restrict__ words = a.hits + (beg - a.offsets[0]);
-  const uint8_t* __restrict__ res = a.residues + beg;
-  uint32_t h[V];
-  WinWords ww[V];
+// ---- K2 chunks ---------------------------------------------------------------------------------
+// A protein's windows are word indices [base, base + n_win) of the K1 words (base = its first
+// residue relative to offsets[0]; word x belongs to residue offsets[0] + x). K2 cuts them into
+// chunks of kChunk windows on a 4-aligned grid starting at base & ~3: lane l of a wave holds
+// the four consecutive windows X..X+3, X = (base & ~3) + kChunk * q + 4l, so its words are one
+// aligned 16-byte load and its residues (4 + K - 1 bytes) three aligned 8-byte words.
+struct Chunk {
+  uint32_t h[4];        // K1 word of each window (0: miss, outside the protein, or dead chunk)
+  uint64_t r0, r1, r2;  // residue words from 8-aligned offsets[0] + X (clamped)
+  uint32_t sh;          // byte offset of window X in r0
+};
+static_assert(kVoteWin == 4, "a lane holds four consecutive windows of a chunk");
+
+__device__ __forceinline__ uint32_t chunks_of(uint64_t base, uint32_t n_win) {
+  return n_win ? (uint32_t)(((base & 3u) + n_win + kChunk - 1) / kChunk) : 0u;
+}
+
+// Load chunk q of the protein at word index `base` with n_win >= 1 windows (live) — or, for a
+// dead chunk (!live), harmless reads of word 0 whose results are dropped. Unconditional,
+// clamped loads: no branch-merged registers.
+__device__ __forceinline__ void load_chunk(const ProteinArgs& a, uint64_t base, uint32_t n_win,
+                                           uint32_t q, bool live, int lane, Chunk& c) {
+  const uint64_t last = live ? base + n_win - 1 : 0;
+  const uint64_t X = live ? (base & ~3ull) + (uint64_t)q * kChunk + 4u * lane : 0;
+  const uint64_t Xc = X <= last ? X : (last & ~3ull);
+  const uint4 w = *reinterpret_cast<const uint4*>(a.hits + Xc);
+  const uint64_t ri = a.offsets[0] + (X <= last ? X : last);
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(a.residues + (ri & ~7ull));
+  c.r0 = src[0];
+  c.r1 = src[1];
+  c.r2 = src[2];
+  c.sh = (uint32_t)(ri & 7);
+  const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    const int64_t w = w0 + v * 64 + lane;
-    const int64_t wc = w < n_win ? w : n_win - 1;
-    const uint32_t x = words[wc];
-    ww[v] = window_words(res, (uint64_t)wc);
-    h[v] = w < n_win ? x : 0u;
+  for (int j = 0; j < 4; ++j) c.h[j] = (live && X + j >= base && X + j <= last) ? x[j] : 0u;
+}
+
+// Insert the chunk's hit keys in `set` (capacity cap); returns the wave's number of new keys.
+// The first attempts of the lane's four inserts are independent CASes issued together (one LDS
+// round trip); only a taken slot holding another key continues probing.
+template <int K>
+__device__ __forceinline__ uint32_t dedupe_insert(const uint8_t* lut, unsigned long long* set,
+                                                  uint32_t cap, const Chunk& c) {
+  uint64_t key[4];
+  uint32_t slot[4];
+  unsigned long long old[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t o = c.sh + j;
+    const uint64_t bytes = o < 8 ? funnel(c.r0, c.r1, o * 8) : funnel(c.r1, c.r2, (o - 8) * 8);
+#ifdef KMA_ABL_NOLUT  // timing ablation only (wrong keys if K < 8)
+    key[j] = bytes | 1;
+#else
+    pack_window<K>(lut, bytes, key[j]);
+#endif
+    slot[j] = set_hash(key[j]) & (cap - 1u);
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    old[j] = c.h[j] ? atomicCAS(set + slot[j], 0ull, (unsigned long long)key[j]) : key[j];
   uint32_t fresh = 0;
 #pragma unroll
-  for (int v = 0; v < V; ++v)
-    if (h[v]) {
-      uint64_t key;
-      pack_window<K>(lut, funnel(ww[v].lo, ww[v].hi, ww[v].sh), key);
-      fresh += set_insert(set, mask, key) ? 1u : 0u;
+  for (int j = 0; j < 4; ++j) {
+    if (old[j] == 0ull) {
+      fresh++;
+    } else if (old[j] != key[j]) {
+      uint32_t i = slot[j];
+      for (;;) {
+        i = (i + 1u) & (cap - 1u);
+        const unsigned long long o = atomicCAS(set + i, 0ull, (unsigned long long)key[j]);
+        if (o == 0ull) { fresh++; break; }
+        if (o == key[j]) break;
+      }
     }
+  }
   return wave_sum(fresh);
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2 — vote. A block of kVoteWaves waves owns kVoteWaves consecutive proteins; their windows are
-// cut into chunks of kChunk windows and the waves share the chunks of all the block's proteins,
-// so a long protein is spread over the block instead of one wave (no serial tail).
-//   pass 1: per chunk, the K1 words (kVoteWin per lane, all in flight) -> per-protein min fid,
-//           max fid, hits H in LDS. No hit -> NONE; two roles -> AMBIGUOUS (badPeg); multiset
-//           -> count H; H < 2 -> count H. These need no set.
-//   pass 2: a protein with one role and H >= 2 gets a set of >= 2H u64 keys from the block's
-//           LDS pool; each hit window's key is re-packed from the residues and inserted, so a
-//           kmer occurring twice in one protein counts once (ProteinKmers is a set).
-// A protein whose set does not fit the pool is marked pending for vote_long_kernel.
+// K2 — vote. A block of kVoteWaves waves owns kVoteProteins consecutive proteins; their chunks
+// are dealt to the waves round-robin (chunk c to wave c % kVoteWaves), so a long protein is
+// spread over the block instead of one wave (no serial tail).
+//   pass 1: a wave loads its first kVoteHold chunks (words + residues) at once and keeps them
+//           in registers; per chunk, min fid, max fid and hits H go to LDS. No hit -> NONE; two
+//           roles -> AMBIGUOUS (badPeg); multiset -> count H; H < 2 -> count H: no set.
+//   pass 2: a protein with one role and H >= 2 gets a set of set_cap(H) u64 keys from the
+//           block's LDS pool; each hit window's key is re-packed from the held residues and
+//           inserted, so a kmer occurring twice in one protein counts once (ProteinKmers is a
+//           set). Chunks past the held ones (blocks with long proteins) are reloaded.
+//   phase 3: proteins whose set did not fit beside the others take the whole pool in turn.
+// A protein whose set exceeds the pool is marked pending for vote_long_kernel.
+// The kernel is bound by dependent latency (offsets -> words -> LDS atomics; measured per phase
+// with KMA_VOTE_TRACE builds), so every wave has all its loads in flight at once and blocks are
+// small enough (LDS, registers) for many to be resident.
 // ---------------------------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
-  constexpr int V = kVoteWin;
-  constexpr int P = kVoteWaves;
+  constexpr int W = kVoteWaves;
+  constexpr int P = kVoteProteins;
+  constexpr int U = kVoteHold;
+  static_assert(P <= 64 && (P & (P - 1)) == 0, "header is one wave; binary search needs 2^n");
   __shared__ __attribute__((aligned(16))) unsigned long long pool[kVotePool];
-  __shared__ uint64_t pbeg[P];
+  __shared__ uint64_t pbase_w[P];  // word index of window 0
   __shared__ uint32_t pwin[P], chunk0[P + 1], pmin[P], pmax[P], phits[P], pcnt[P], pbase[P],
       pcap[P];
   __shared__ uint32_t pool_top;
@@ -693,55 +768,63 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   const uint32_t p0 = a.seq_lo + blockIdx.x * P;
   const int np = (int)min<uint32_t>(P, a.seq_hi - p0);
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
-  if (tid < 256) lut[tid] = a.lut[tid];
-  if (tid < P) {
-    uint32_t w = 0;
-    pbeg[tid] = 0;
-    if (tid < np) {
-      const int64_t n = n_windows(a, p0 + tid, K);
+#ifdef KMA_VOTE_TRACE
+  if (tid > 0 && tid < 7) a.scratch[blockIdx.x * 8 + tid] = 0;
+  if (tid == 0) a.scratch[blockIdx.x * 8 + 0] = wall_clock64();
+#define KMA_TRACE_AT(n) \
+  if (tid == 0) a.scratch[blockIdx.x * 8 + (n)] = wall_clock64();
+#else
+#define KMA_TRACE_AT(n)
+#endif
+  for (int i = tid; i < 256; i += 64 * W) lut[i] = a.lut[i];
+  if (wave == 0) {  // header: windows, chunk prefix (wave scan)
+    uint32_t w = 0, nc = 0;
+    uint64_t base = 0;
+    if (lane < np) {
+      const int64_t n = n_windows(a, p0 + lane, K);
       w = n > 0 ? (uint32_t)n : 0u;
-      pbeg[tid] = a.offsets[p0 + tid];
+      base = a.offsets[p0 + lane] - a.offsets[0];
+      nc = chunks_of(base, w);
     }
-    pwin[tid] = w;
-    pmin[tid] = 0xFFFFFFFFu;
-    pmax[tid] = 0u;
-    phits[tid] = 0u;
-    pcnt[tid] = 0u;
-    pcap[tid] = 0u;
-  }
-  if (tid == 0) {
-    uint32_t c = 0;
-    for (int i = 0; i < P; ++i) {
-      chunk0[i] = c;
-      c += (pwin[i] + kChunk - 1) / kChunk;
+    uint32_t incl = nc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)incl, o, 64);
+      incl += lane >= o ? x : 0u;
     }
-    chunk0[P] = c;
-    pool_top = 0;
+    if (lane < P) {
+      pbase_w[lane] = base;
+      pwin[lane] = w;
+      chunk0[lane] = incl - nc;
+      pmin[lane] = 0xFFFFFFFFu;
+      pmax[lane] = 0u;
+      phits[lane] = 0u;
+      pcnt[lane] = 0u;
+      pcap[lane] = 0u;
+      if (lane == P - 1) chunk0[P] = incl;
+    }
+    if (lane == 0) pool_top = 0;
   }
   __syncthreads();
-  const uint64_t o0 = a.offsets[0];
+  KMA_TRACE_AT(1)
   const uint32_t n_chunks = chunk0[P];
-  // ---- pass 1 ----------------------------------------------------------------------------------
-  for (uint32_t c = wave; c < n_chunks; c += P) {
+#ifdef KMA_VOTE_TRACE
+  if (tid == 0) a.scratch[blockIdx.x * 8 + 7] = n_chunks;
+#endif
+  // The protein of chunk c: the last p with chunk0[p] <= c (proteins without chunks skipped).
+  auto owner = [&](uint32_t c) {
     uint32_t p = 0;
 #pragma unroll
-    for (int i = 1; i < P; ++i) p += c >= chunk0[i] ? 1u : 0u;
-    const int64_t n_win = pwin[p];
-    const int64_t w0 = (int64_t)(c - chunk0[p]) * kChunk;
-    const uint32_t* __restrict__ words = a.hits + (pbeg[p] - o0);
-    uint32_t h[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int64_t w = w0 + v * 64 + lane;
-      const uint32_t x = words[w < n_win ? w : n_win - 1];
-      h[v] = w < n_win ? x : 0u;
-    }
+    for (uint32_t step = P / 2; step > 0; step >>= 1) p += chunk0[p + step] <= c ? step : 0u;
+    return p;
+  };
+  auto reduce_chunk = [&](const Chunk& ch, uint32_t p) {
     uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, hits = 0u;
 #pragma unroll
-    for (int v = 0; v < V; ++v)
-      if (h[v]) {
-        fmin = min(fmin, h[v] - 1u);
-        fmax = max(fmax, h[v] - 1u);
+    for (int j = 0; j < 4; ++j)
+      if (ch.h[j]) {
+        fmin = min(fmin, ch.h[j] - 1u);
+        fmax = max(fmax, ch.h[j] - 1u);
         hits++;
       }
     fmin = wave_min(fmin);
@@ -752,16 +835,37 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
       atomicMax(pmax + p, fmax);
       atomicAdd(phits + p, hits);
     }
+  };
+  // ---- pass 1 ----------------------------------------------------------------------------------
+  Chunk held[U];
+  uint32_t hp[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = wave + u * W;
+    const bool live = c < n_chunks;  // wave-uniform
+    const uint32_t p = owner(live ? c : 0u);
+    hp[u] = p;
+    load_chunk(a, pbase_w[p], pwin[p], live ? c - chunk0[p] : 0u, live, lane, held[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) reduce_chunk(held[u], hp[u]);
+  for (uint32_t c = wave + U * W; c < n_chunks; c += W) {  // long proteins
+    const uint32_t p = owner(c);
+    Chunk ch;
+    load_chunk(a, pbase_w[p], pwin[p], c - chunk0[p], true, lane, ch);
+    reduce_chunk(ch, p);
   }
   __syncthreads();
+  KMA_TRACE_AT(2)
   // ---- decide; take sets from the pool -------------------------------------------------------
+  // Outputs are written after the block's last barrier: a barrier waits for the block's
+  // outstanding global stores (one vmcnt for loads and stores on this architecture).
   if (tid < np) {
     const uint32_t mn = pmin[tid], mx = pmax[tid], h = phits[tid];
     if (mn == 0xFFFFFFFFu || mn != mx || multiset || h < 2) {
-      write_vote(a, p0 + tid, mn, mx, h);
+      pcnt[tid] = h;  // final now: count = H
     } else {
-      uint32_t cap = 64;
-      while (cap < 2 * h) cap <<= 1;
+      const uint32_t cap = set_cap(h);
       const uint32_t base = atomicAdd(&pool_top, cap);
       if (base + cap <= (uint32_t)kVotePool) {
         pbase[tid] = base;
@@ -769,46 +873,209 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
       } else if (cap <= (uint32_t)kVotePool) {
         pcap[tid] = cap | kDeferred;  // phase 3: the whole pool, after pass 2
       } else {
-        a.out_status[p0 + tid] = kStatusPending;  // vote_long_kernel, global-memory set
-        atomicOr(a.overflow_flag, 1u);
+        pcap[tid] = kLongCap;  // vote_long_kernel, global-memory set
       }
     }
   }
   __syncthreads();
+  KMA_TRACE_AT(3)
+  // Every protein's output, after the last barrier.
+  auto finish = [&]() {
+    if (tid < np) {
+      if (pcap[tid] == kLongCap) {
+        push_pending(a, p0 + tid);
+      } else {
+        write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
+      }
+    }
+  };
   const uint32_t used = min(pool_top, (uint32_t)kVotePool);
-  if (used == 0) return;  // block-uniform: no protein needs a set (nor a deferred one)
+  bool deferred = false;
+  for (int p = 0; p < np; ++p) deferred |= (pcap[p] & kDeferred) && pcap[p] != kLongCap;
+  if (used == 0 && !deferred) {  // block-uniform: no protein needs the pool
+    finish();
+    return;
+  }
   uint4* pool4 = reinterpret_cast<uint4*>(pool);
-  for (uint32_t i = tid; i < used / 2; i += 64 * P) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t i = tid; i < used / 2; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
+  KMA_TRACE_AT(4)
   // ---- pass 2: distinct hit keys ----------------------------------------------------------------
-  for (uint32_t c = wave; c < n_chunks; c += P) {
-    uint32_t p = 0;
+#ifndef KMA_ABL_NOPASS2  // timing ablation only
 #pragma unroll
-    for (int i = 1; i < P; ++i) p += c >= chunk0[i] ? 1u : 0u;
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = wave + u * W, p = hp[u];
     const uint32_t cap = pcap[p];
-    if (cap == 0 || (cap & kDeferred)) continue;  // wave-uniform
-    const uint32_t fresh = dedupe_chunk<K>(a, lut, pool + pbase[p], cap - 1, pbeg[p], pwin[p],
-                                           (int64_t)(c - chunk0[p]) * kChunk, lane);
+    if (c >= n_chunks || cap == 0 || (cap & kDeferred)) continue;  // wave-uniform (kLongCap too)
+    const uint32_t fresh = dedupe_insert<K>(lut, pool + pbase[p], cap, held[u]);
     if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
   }
+  for (uint32_t c = wave + U * W; c < n_chunks; c += W) {
+    const uint32_t p = owner(c);
+    const uint32_t cap = pcap[p];
+    if (cap == 0 || (cap & kDeferred)) continue;  // wave-uniform
+    Chunk ch;
+    load_chunk(a, pbase_w[p], pwin[p], c - chunk0[p], true, lane, ch);
+    const uint32_t fresh = dedupe_insert<K>(lut, pool + pbase[p], cap, ch);
+    if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
+  }
+#endif
   __syncthreads();
-  if (tid < np && pcap[tid] && !(pcap[tid] & kDeferred))
-    write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
+  KMA_TRACE_AT(5)
   // ---- phase 3: proteins that did not fit beside the others take the whole pool in turn ------
   for (int p = 0; p < np; ++p) {
     const uint32_t cap = pcap[p];
-    if (!(cap & kDeferred)) continue;  // block-uniform
+    if (!(cap & kDeferred) || cap == kLongCap) continue;  // block-uniform
     const uint32_t c2 = cap & ~kDeferred;
     __syncthreads();  // the pool's previous contents are no longer read
-    for (uint32_t i = tid; i < c2 / 2; i += 64 * P) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = tid; i < c2 / 2; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    for (uint32_t c = chunk0[p] + wave; c < chunk0[p + 1]; c += P) {
-      const uint32_t fresh = dedupe_chunk<K>(a, lut, pool, c2 - 1, pbeg[p], pwin[p],
-                                             (int64_t)(c - chunk0[p]) * kChunk, lane);
+    for (uint32_t c = chunk0[p] + wave; c < chunk0[p + 1]; c += W) {
+      Chunk ch;
+      load_chunk(a, pbase_w[p], pwin[p], c - chunk0[p], true, lane, ch);
+      const uint32_t fresh = dedupe_insert<K>(lut, pool, c2, ch);
       if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
     }
-    __syncthreads();
-    if (tid == 0) write_vote(a, p0 + p, pmin[p], pmax[p], pcnt[p]);
+  }
+  __syncthreads();
+  finish();
+  KMA_TRACE_AT(6)
+#undef KMA_TRACE_AT
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2, wave form (default). Each wave owns kWaveProteins consecutive proteins and votes them on
+// its own: no block barrier after the LUT load, so a wave's latency chain (offsets -> words and
+// residues of up to kWaveHold chunks, all in flight -> DPP reductions -> LDS set inserts ->
+// outputs) is never coupled to a slower wave's.
+//   - chunks as in vote_kernel (4 consecutive windows per lane), dealt to the wave's proteins in
+//     order; the first kWaveHold stay in registers, later ones (long proteins) are re-read;
+//   - per protein: min fid, max fid, hits H (wave reductions, scalar accumulators);
+//     NONE / AMBIGUOUS / multiset / H < 2 are final;
+//   - otherwise a set of set_cap(H) u64 keys in the wave's LDS slice (kWaveSet entries; the
+//     wave's set proteins take it in turn); a larger set -> pending for vote_long_kernel.
+// ---------------------------------------------------------------------------------------------
+template <int N, typename T>
+__device__ __forceinline__ T pick(const T (&v)[N], uint32_t i) {  // v[i], i wave-uniform
+  T r = v[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j) r = i == (uint32_t)j ? v[j] : r;
+  return r;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void vote_wave_kernel(ProteinArgs a) {
+  constexpr int PW = kWaveProteins;
+  constexpr int U = kWaveHold;
+  constexpr int S = kWaveSet;
+  static_assert(PW < 64, "one offset per lane");
+  __shared__ __attribute__((aligned(16))) unsigned long long sets[4][S];
+  __shared__ uint8_t lut[256];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t s0 = a.seq_lo + (blockIdx.x * 4u + wave) * PW;
+  const uint32_t n_here = s0 < a.seq_hi ? min((uint32_t)PW, a.seq_hi - s0) : 0u;
+  const uint64_t o0 = a.offsets[0];
+  const uint64_t off = lane <= (int)n_here ? a.offsets[s0 + (lane <= (int)n_here ? lane : 0)] : 0;
+  lut[tid] = a.lut[tid];
+  __syncthreads();  // the only barrier
+  if (n_here == 0) return;
+  const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  const int64_t adj = (a.flags & KMA_F_END_EXCLUSIVE) ? -K : -K + 1;
+  uint64_t base[PW];
+  uint32_t nwin[PW], c0[PW + 1];
+  c0[0] = 0;
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const uint64_t b = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), i) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)off, i);
+    const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), i + 1)
+                        << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)off, i + 1);
+    const int64_t n = (uint32_t)i < n_here ? (int64_t)(e - b) + adj : 0;
+    nwin[i] = n > 0 ? (uint32_t)n : 0u;
+    base[i] = b - o0;
+    c0[i + 1] = c0[i] + chunks_of(base[i], nwin[i]);
+  }
+  const uint32_t total = c0[PW];
+  auto owner = [&](uint32_t c) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 1; i < PW; ++i) p += c >= c0[i] ? 1u : 0u;
+    return p;
+  };
+  auto load = [&](uint32_t c, bool live, Chunk& ch) {
+    const uint32_t p = owner(live ? c : 0u);
+    load_chunk(a, pick(base, p), pick(nwin, p), live ? c - pick(c0, p) : 0u, live, lane, ch);
+    return p;
+  };
+  uint32_t mn[PW], mx[PW], hits[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) mn[i] = 0xFFFFFFFFu, mx[i] = 0u, hits[i] = 0u;
+  auto reduce = [&](const Chunk& ch, uint32_t p) {
+    uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, h = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (ch.h[j]) {
+        fmin = min(fmin, ch.h[j] - 1u);
+        fmax = max(fmax, ch.h[j] - 1u);
+        h++;
+      }
+    fmin = wave_min(fmin);
+    fmax = wave_max(fmax);
+    h = wave_sum(h);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if ((uint32_t)i == p) mn[i] = min(mn[i], fmin), mx[i] = max(mx[i], fmax), hits[i] += h;
+  };
+  // ---- pass 1: all held chunks in flight at once ----------------------------------------------
+  Chunk held[U];
+  uint32_t hp[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) hp[u] = load((uint32_t)u, (uint32_t)u < total, held[u]);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if ((uint32_t)u < total) reduce(held[u], hp[u]);
+  for (uint32_t c = U; c < total; ++c) {  // long proteins
+    Chunk ch;
+    const uint32_t p = load(c, true, ch);
+    reduce(ch, p);
+  }
+  // ---- decide, then the set proteins one at a time in the wave's slice -------------------------
+  unsigned long long* set = sets[wave];
+  uint32_t cnt[PW];
+  bool pending[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    cnt[i] = hits[i];
+    pending[i] = false;
+    if (mn[i] == 0xFFFFFFFFu || mn[i] != mx[i] || multiset || hits[i] < 2) continue;
+    const uint32_t cap = set_cap(hits[i]);
+    if (cap > (uint32_t)S) {
+      pending[i] = true;
+      continue;
+    }
+    uint4* set4 = reinterpret_cast<uint4*>(set);
+    for (uint32_t e = lane; e < cap / 2; e += 64) set4[e] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t fresh = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if ((uint32_t)u < total && hp[u] == (uint32_t)i)
+        fresh += dedupe_insert<K>(lut, set, cap, held[u]);
+    for (uint32_t c = max((uint32_t)U, c0[i]); c < c0[i + 1]; ++c) {  // re-read past the held
+      Chunk ch;
+      load(c, true, ch);
+      fresh += dedupe_insert<K>(lut, set, cap, ch);
+    }
+    cnt[i] = fresh;
+  }
+  // ---- outputs: lane i writes protein i ---------------------------------------------------------
+  if (lane < (int)n_here) {
+    const uint32_t i = (uint32_t)lane;
+    if (pick(pending, i)) {
+      push_pending(a, s0 + i);  // vote_long_kernel
+    } else {
+      write_vote(a, s0 + i, pick(mn, i), pick(mx, i), pick(cnt, i));
+    }
   }
 }
 
@@ -825,7 +1092,8 @@ __device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* red, int 
   return r;
 }
 
-// K2 for the pending (long) proteins: one block per protein, grid-striding over the statuses.
+// K2 for the pending proteins (sets too large for K2's LDS): one block per protein,
+// grid-striding over the workspace's pending list.
 // Proteins of up to kLongSet / 2 windows keep their distinct-key set in LDS; longer ones are
 // taken by the first kFallbackBlocks blocks with a set in their slice of workspace scratch
 // (kFallbackCap u64); longer still are TOO_LONG.
@@ -848,72 +1116,44 @@ __device__ void vote_long_one(const ProteinArgs& a, const uint8_t* lut, uint32_t
   __syncthreads();  // the set is reused by the next protein
 }
 
-// Block-cooperative scan of statuses [s0, s0 + 256): the pending proteins whose window count
-// satisfies `want`, compacted into `list` (returns their number). One status load per thread.
-template <class Want>
-__device__ __forceinline__ uint32_t scan_pending(const ProteinArgs& a, uint32_t s0, Want want,
-                                                 uint32_t* list, uint32_t* wave_cnt) {
-  const int tid = threadIdx.x, wave = tid >> 6;
-  const uint32_t s = s0 + tid;
-  const bool p = s < a.n_seq && a.out_status[s] == kStatusPending && want(s);
-  const uint64_t m = __ballot(p);
-  __syncthreads();  // list / wave_cnt are reused across chunks
-  if ((tid & 63) == 0) wave_cnt[wave] = (uint32_t)__popcll(m);
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-  for (int w = 0; w < kWavesPerBlock; ++w) {
-    base += w < wave ? wave_cnt[w] : 0u;
-    total += wave_cnt[w];
-  }
-  if (p) list[base + popc_below(m)] = s;
-  __syncthreads();
-  return total;
-}
-
 template <int K>
 __global__ __launch_bounds__(256) void vote_long_kernel(ProteinArgs a) {
-  if (__hip_atomic_load(a.overflow_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    return;
+  const uint32_t n = __hip_atomic_load(a.overflow_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n == 0u || blockIdx.x >= n) return;
   __shared__ __attribute__((aligned(16))) unsigned long long lds_set[kLongSet];
   __shared__ uint8_t lut[256];
-  __shared__ uint32_t red[kWavesPerBlock], wave_cnt[kWavesPerBlock], list[256];
+  __shared__ uint32_t red[kWavesPerBlock];
   const int tid = threadIdx.x;
   lut[tid] = a.lut[tid];
   __syncthreads();
-  // Proteins of up to kLongSet / 2 windows: LDS set; chunks of 256 statuses per block.
-  for (uint32_t s0 = blockIdx.x * 256u; s0 < a.n_seq; s0 += gridDim.x * 256u) {
-    const uint32_t n = scan_pending(a, s0, [&](uint32_t s) {
-      return n_windows(a, s, K) <= kLongSet / 2; }, list, wave_cnt);
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t s = list[i];
-      const int64_t n_win = n_windows(a, s, K);
-      uint32_t cap = 64;
-      while (cap < 2 * (uint32_t)n_win) cap <<= 1;
-      vote_long_one<K>(a, lut, s, n_win, lds_set, cap, red);
-    }
+  // Proteins of up to kLongSet / 2 windows: an LDS set, every block.
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t s = a.pending[i];
+    const int64_t n_win = n_windows(a, s, K);
+    if (n_win > kLongSet / 2) continue;  // block-uniform
+    uint32_t cap = 64;
+    while (cap < 2 * (uint32_t)n_win) cap <<= 1;
+    vote_long_one<K>(a, lut, s, n_win, lds_set, cap, red);
   }
   if (blockIdx.x >= kFallbackBlocks) return;
   // Longer proteins: the first kFallbackBlocks blocks, a set in workspace scratch.
   unsigned long long* gset =
       reinterpret_cast<unsigned long long*>(a.scratch) + (uint64_t)blockIdx.x * kFallbackCap;
-  for (uint32_t s0 = blockIdx.x * 256u; s0 < a.n_seq; s0 += kFallbackBlocks * 256u) {
-    const uint32_t n = scan_pending(a, s0, [&](uint32_t s) {
-      return n_windows(a, s, K) > kLongSet / 2; }, list, wave_cnt);
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t s = list[i];
-      const int64_t n_win = n_windows(a, s, K);
-      if (n_win > (int64_t)(kFallbackCap / 2)) {
-        if (tid == 0) {
-          a.out_fid[s] = -1;
-          a.out_count[s] = 0;
-          a.out_status[s] = KMA_STATUS_TOO_LONG;
-        }
-        continue;
+  for (uint32_t i = blockIdx.x; i < n; i += kFallbackBlocks) {
+    const uint32_t s = a.pending[i];
+    const int64_t n_win = n_windows(a, s, K);
+    if (n_win <= kLongSet / 2) continue;
+    if (n_win > (int64_t)(kFallbackCap / 2)) {
+      if (tid == 0) {
+        a.out_fid[s] = -1;
+        a.out_count[s] = 0;
+        a.out_status[s] = KMA_STATUS_TOO_LONG;
       }
-      uint32_t cap = 64;
-      while (cap < 2 * (uint32_t)n_win) cap <<= 1;
-      vote_long_one<K>(a, lut, s, n_win, gset, cap, red);
+      continue;
     }
+    uint32_t cap = 64;
+    while (cap < 2 * (uint32_t)n_win) cap <<= 1;
+    vote_long_one<K>(a, lut, s, n_win, gset, cap, red);
   }
 }
 
@@ -1102,15 +1342,27 @@ static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t str
 
 template <int K>
 static hipError_t launch_vote_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  const unsigned blocks = (a.seq_hi - a.seq_lo + kVoteWaves - 1) / kVoteWaves;
-  if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
+  static const bool block_form = [] {
+    const char* e = getenv("KMA_VOTE");
+    return e && e[0] == 'b';
+  }();
+  if (block_form) {  // KMA_VOTE=block: the block-shared form (A/B)
+    const unsigned blocks = (a.seq_hi - a.seq_lo + kVoteProteins - 1) / kVoteProteins;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
+  } else {
+    const uint64_t waves = (a.seq_hi - a.seq_lo + kWaveProteins - 1) / kWaveProteins;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(vote_wave_kernel<K>, dim3(blocks), dim3(256), 0, stream, a);
+  }
   return hipGetLastError();
 }
 
 template <int K>
 static hipError_t launch_long_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  hipLaunchKernelGGL(vote_long_kernel<K>, dim3(kFallbackBlocks), dim3(256), 0, stream, a);
+  const unsigned blocks = (unsigned)max(kFallbackBlocks, n_cu * kLongBlocksPerCU);
+  hipLaunchKernelGGL(vote_long_kernel<K>, dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

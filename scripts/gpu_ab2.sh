@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of table layouts and K1 forms on one box. Each case in $CASES is
-# name=ENV1=v1,ENV2=v2 (env for the bench; KMERANNO_LIB=flat picks the flat-hash A/B build):
+# name=ENV1=v1,ENV2=v2 (env for the bench; KMERANNO_LIB=<v> picks the A/B build
+# kmers.anno_amd/build/<v>/libkmeranno.so of `make variant VNAME=<v>`):
 # a c2 bench line plus c2/c5 kernel stats per case. Parity runs first (default + other K1 forms).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
@@ -10,14 +11,14 @@ step() { local name=$1 t=$2; shift 2; echo "=== $name" >> $OUT/steps.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
 if [ -z "$NO_PYTEST" ]; then
   step pytest_gpu 900 python -m pytest tests -x -q -m gpu
-  for shape in quad lane; do
+  for shape in ${PARITY_SHAPES:-run lane}; do
     KMA_PROBE=$shape step pytest_$shape 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu
   done
 fi
 for c in ${CASES:-"min=KMA_PROBE=run"}; do
   name=${c%%=*}; envs=${c#*=}
   ( for kv in ${envs//,/ }; do
-      [ "$kv" = KMERANNO_LIB=flat ] && kv=KMERANNO_LIB=$PWD/kmers.anno_amd/build/flat/libkmeranno.so
+      case $kv in KMERANNO_LIB=*) kv=KMERANNO_LIB=$PWD/kmers.anno_amd/build/${kv#*=}/libkmeranno.so ;; esac
       export "$kv"; done
     step bench_c2_$name 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline
     step prof_c2_$name 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2_$name -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
