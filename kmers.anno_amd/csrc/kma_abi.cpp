@@ -30,9 +30,10 @@ int kma::minimizer_len(int k, uint64_t n_buckets) {
 
 constexpr uint64_t kHitsPad = 64;
 // A protein goes to vote_long_kernel only if its set needs more than K2's LDS gives one
-// protein (> kWaveSet / 2, resp. > kVotePool / 2 hits), so it has more than 128 windows.
-static_assert(kma::kWaveSet >= 256 && kma::kVotePool >= 256, "pending list bound");
-uint64_t pending_cap(uint64_t n_residues) { return n_residues / 128 + 64; }
+// protein (>= 3/4 kWaveSet - 256, resp. > kVotePool / 2 hits), so it has more than 128 windows.
+static_assert(kma::kWaveSet >= 512 && kma::kVotePool >= 256, "pending list bound");
+// Two lists of up to n_residues / 128 + 32 records each (a list entry has > 128 windows).
+uint64_t pending_cap(uint64_t n_residues) { return 2 * (n_residues / 128 + 32); }
 
 struct kma_table {
   int device = 0;
@@ -51,8 +52,8 @@ struct kma_workspace {
   int n_cu = 256;
   uint32_t* d_flag = nullptr;
   uint64_t* d_scratch = nullptr;
-  uint32_t* d_hits = nullptr;  // K1 words: one u32 per residue position
-  uint32_t* d_pending = nullptr;  // K2 -> vote_long list (a pending protein has > 128 windows)
+  uint32_t* d_hits = nullptr;  // K1 words (fid + 1), then K1 slot ids: u32 per residue each
+  kma::PendingRec* d_pending = nullptr;  // K2 -> vote_long list (> 128 windows each)
   uint64_t hits_cap = 0;
   // Segmented overlap: K2 of segment i on `side` while K1 of segment i + 1 runs on the call's
   // stream (fork/join through events, graph-capturable).
@@ -425,8 +426,8 @@ int kma_workspace_create(int device, kma_workspace** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 8);
-  if (e == hipSuccess) e = hipMalloc(&w->d_hits, kHitsPad * 4);  // reserve() grows it
-  if (e == hipSuccess) e = hipMalloc(&w->d_pending, pending_cap(0) * 4);
+  if (e == hipSuccess) e = hipMalloc(&w->d_hits, 2 * kHitsPad * 4);  // reserve() grows it
+  if (e == hipSuccess) e = hipMalloc(&w->d_pending, pending_cap(0) * sizeof(kma::PendingRec));
   if (e != hipSuccess) {
     if (w->d_flag) (void)hipFree(w->d_flag);
     delete w;
@@ -447,8 +448,9 @@ int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
   if (ws->d_pending) (void)hipFree(ws->d_pending);
   ws->d_pending = nullptr;
   // Padded by kHitsPad words (never empty): K2 may read word 0 for a chunk past the end.
-  KMA_HIP(hipMalloc(&ws->d_hits, (n_residues + kHitsPad) * 4));
-  KMA_HIP(hipMalloc(&ws->d_pending, pending_cap(n_residues) * 4));
+  // hits then slot ids, each n_residues + kHitsPad words
+  KMA_HIP(hipMalloc(&ws->d_hits, 2 * (n_residues + kHitsPad) * 4));
+  KMA_HIP(hipMalloc(&ws->d_pending, pending_cap(n_residues) * sizeof(kma::PendingRec)));
   ws->hits_cap = n_residues;
   return KMA_OK;
 }
@@ -539,8 +541,10 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.hits = ws->d_hits;
+  a.sids = ws->d_hits + ws->hits_cap + kHitsPad;
   a.overflow_flag = ws->d_flag;
   a.pending = ws->d_pending;
+  a.pending_half = (uint32_t)(pending_cap(ws->hits_cap) / 2);
   a.scratch = ws->d_scratch;
   hipEvent_t* ev = nullptr;
   if (ws->timing) {

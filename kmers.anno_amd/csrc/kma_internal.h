@@ -22,6 +22,9 @@ constexpr int kSlotsPerBucket = 8;
 constexpr uint32_t kFidMask = (1u << 23) - 1;
 constexpr uint32_t kOvfBit = 1u << 23;         // in the high dword
 constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
+// K1's per-window verdict while probing: fid + 1 in bits 0..23, slot in bucket at kSlotShift.
+constexpr uint32_t kWordFid = (1u << 24) - 1;
+constexpr uint32_t kSlotShift = 24;
 
 __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
   return ((uint64_t)((uint32_t)(key >> 32) << 24 | (fid & kFidMask)) << 32) | (uint32_t)key;
@@ -79,6 +82,12 @@ __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint
 int minimizer_len(int k, uint64_t n_buckets);
 
 // ---- kernel parameter blocks ------------------------------------------------------------------
+// A protein K2 leaves to vote_long_kernel: one role (fid), hits H >= 2, its window range.
+struct PendingRec {
+  uint32_t s, fid, hits, n_win;
+  uint64_t base;  // word index of window 0 (residue offsets[0] + base)
+};
+
 struct ProteinArgs {
   const uint64_t* slots;
   uint32_t n_buckets;
@@ -97,23 +106,32 @@ struct ProteinArgs {
   uint32_t* tally;  // may be null
   uint32_t n_fid;
   uint32_t* hits;           // workspace: fid + 1 (0 = miss) per residue position
-  uint32_t* overflow_flag;  // workspace: length of `pending` (K1 zeroes it)
-  uint32_t* pending;        // workspace: proteins left to vote_long_kernel
+  uint32_t* sids;           // workspace: slot id of the hit (the key's identity in the table)
+  uint32_t* overflow_flag;  // workspace: lengths of the two `pending` lists (K1 zeroes them)
+  struct PendingRec* pending;  // workspace: proteins left to vote_long_kernel (two lists)
+  uint32_t pending_half;       // start of the second list
   uint64_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u64
   uint32_t seq_lo, seq_hi;  // the segment [seq_lo, seq_hi) of proteins this launch covers
   uint32_t reset_flag;      // K1 of the first segment clears overflow_flag
 };
 
-// K1 probe kernel: kProbeWin consecutive windows per lane per step (a run), all distinct
-// first-bucket loads in flight.
-constexpr int kProbeWin = 4;
-constexpr int kProbeBlocksPerCU = 8;
+// K1 probe kernel: kProbeWin windows per lane per step, all first-bucket loads in flight
+// (3: 70 VGPRs, 7 waves/SIMD; 4 needs 125 VGPRs and measured 9% slower at c5). The grid is
+// the resident population (hipOccupancy...); kProbeBlocksPerCU is only the fallback.
+#ifndef KMA_PROBE_WIN
+#define KMA_PROBE_WIN 3
+#endif
+#ifndef KMA_PROBE_BPC
+#define KMA_PROBE_BPC 8
+#endif
+constexpr int kProbeWin = KMA_PROBE_WIN;
+constexpr int kProbeBlocksPerCU = KMA_PROBE_BPC;
 // K1 defers overflow-chain walks to a per-wave LDS queue of kChainQ positions, resolved a
 // wave's 64 lanes at a time.
 constexpr int kChainQ = 384;
 // K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteProteins
 // proteins (kVoteWin consecutive windows per lane per chunk; a wave's first kVoteHold chunks
-// stay in registers between the passes) and an LDS pool of kVotePool u64 set entries.
+// stay in registers between the passes) and an LDS pool of kVotePool u32 set entries.
 // Proteins whose set does not fit are finished by vote_long_kernel: one block each, an LDS set
 // of kLongSet keys, else kFallbackCap keys of workspace scratch per block.
 // (The KMA_VOTE_* macros exist for tuning builds: `make variant`.)
@@ -124,7 +142,7 @@ constexpr int kChainQ = 384;
 #define KMA_VOTE_PROTEINS 8
 #endif
 #ifndef KMA_VOTE_POOL
-#define KMA_VOTE_POOL 2048
+#define KMA_VOTE_POOL 4096
 #endif
 #ifndef KMA_VOTE_HOLD
 #define KMA_VOTE_HOLD 2
@@ -137,18 +155,16 @@ constexpr int kVoteProteins = KMA_VOTE_PROTEINS;
 constexpr int kVotePool = KMA_VOTE_POOL;
 constexpr int kVoteHold = KMA_VOTE_HOLD;
 constexpr int kLongSet = 8192;
-// K2 wave form: kWaveProteins proteins per wave, kWaveHold chunks held in registers, an LDS set
-// slice of kWaveSet u64 per wave (4 waves per block).
-#ifndef KMA_WAVE_PROTEINS
-#define KMA_WAVE_PROTEINS 1
-#endif
+constexpr int kLongHold = 4;  // vote_long_kernel: chunks of a protein in flight per wave
+constexpr int kLongWaveSet = kLongSet * 2 / 4;  // u32 slot ids per wave in vote_long_kernel
+// K2 wave form: one protein per wave, kWaveHold chunks in flight, an LDS set slice of kWaveSet
+// u32 slot ids per wave (4 waves per block), filled to at most 3/4.
 #ifndef KMA_WAVE_HOLD
-#define KMA_WAVE_HOLD 2
+#define KMA_WAVE_HOLD 4
 #endif
 #ifndef KMA_WAVE_SET
-#define KMA_WAVE_SET 512
+#define KMA_WAVE_SET 1024
 #endif
-constexpr int kWaveProteins = KMA_WAVE_PROTEINS;
 constexpr int kWaveHold = KMA_WAVE_HOLD;
 constexpr int kWaveSet = KMA_WAVE_SET;
 constexpr uint32_t kDeferred = 1u << 31;  // K2: set taken from the whole pool in phase 3

@@ -21,6 +21,9 @@
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace kma {
 namespace {
 
@@ -126,9 +129,11 @@ __device__ __forceinline__ bool ovf_bit(const uint4 (&q)[4], uint64_t key) {
 }
 
 // Walk the overflow chain after home bucket `b` (the key missed there and its overflow bit is
-// set): stop at the key or at the first bucket with an empty slot. Returns true on a hit.
+// set): stop at the key or at the first bucket with an empty slot. Returns true on a hit, with
+// the key's fid and slot id (bucket * 8 + slot: the key's identity in this table).
 __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, uint32_t n_buckets,
-                                           uint32_t b, uint64_t key, uint32_t& fid) {
+                                           uint32_t b, uint64_t key, uint32_t& fid,
+                                           uint32_t& sid) {
   bool hit = false, empty = false;
   uint32_t slot = 0;
   for (uint32_t step = 1; step < n_buckets && !hit && !empty; ++step) {  // bounded
@@ -137,6 +142,7 @@ __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, u
     load_bucket(slots, b, q);
     scan_bucket(q, key, hit, empty, fid, slot);
   }
+  sid = b * kSlotsPerBucket + slot;
   return hit;
 }
 
@@ -151,7 +157,8 @@ __device__ __forceinline__ bool probe(const uint64_t* __restrict__ slots, uint32
   scan_bucket(q, key, hit, empty, fid, slot);
   if (hit) return true;
   if (!ovf_bit(q, key)) return false;
-  return walk_chain(slots, n_buckets, b, key, fid);
+  uint32_t sid;
+  return walk_chain(slots, n_buckets, b, key, fid, sid);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -239,7 +246,7 @@ template <int K, int M, int U>
 __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
   const int t = threadIdx.x;
-  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
+  if (a.reset_flag && blockIdx.x == 0 && t < 2) a.overflow_flag[t] = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
   const uint64_t o0 = a.offsets[0];
@@ -275,10 +282,14 @@ __global__ __launch_bounds__(256) void probe_kernel(ProteinArgs a) {
       uint32_t fid = 0, slot = 0;
       scan_bucket(q[j], key[j], hit, empty, fid, slot);
       hit = ok[j] && hit;
+      uint32_t sid = bk[j] * kSlotsPerBucket + slot;
       if (ok[j] && !hit && ovf_bit(q[j], key[j]))  // rare: walk the overflow chain
-        hit = walk_chain(slots, nb, bk[j], key[j], fid);
+        hit = walk_chain(slots, nb, bk[j], key[j], fid, sid);
       const uint64_t g = g0 + j * 256 + t;
-      if (g < n_pos) a.hits[g] = hit ? fid + 1u : 0u;
+      if (g < n_pos) {
+        a.hits[g] = hit ? fid + 1u : 0u;
+        a.sids[g] = sid;
+      }
     }
   }
 }
@@ -304,8 +315,9 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 }
 
 // One quad's verdict on a bucket it loaded cooperatively (lane `part` holds slots 2part and
-// 2part + 1 in v) for key (kl, kh): fid + 1 of the matching slot (0 = not in this bucket), with
-// bit 31 = the key's overflow bit (chain walk needed if there is no match). Keys are unique in
+// 2part + 1 in v) for key (kl, kh): fid + 1 of the matching slot in bits 0..23 (0 = not in this
+// bucket), the slot's index in the bucket in bits 24..26, and bit 31 = the key's overflow bit
+// (chain walk needed if there is no match). Keys are unique in
 // a table, so at most one lane matches and OR is the reduction. Every lane of the quad must
 // call it (DPP). Branch-free on purpose: a short-circuit here lets the compiler split the
 // 16-byte load into a lazily loaded tail behind a branch and a vmcnt(0).
@@ -314,6 +326,7 @@ __device__ __forceinline__ uint32_t match_part(const uint4 v, uint32_t kl, uint3
   const uint32_t m0 = (uint32_t)(v.x == kl) & (uint32_t)((v.y & kKeyHiMask) == kh);
   const uint32_t m1 = (uint32_t)(v.z == kl) & (uint32_t)((v.w & kKeyHiMask) == kh);
   uint32_t w = (m0 * ((v.y & kFidMask) + 1u)) | (m1 * ((v.w & kFidMask) + 1u));
+  w |= (m0 | m1) * ((2u * part + m1) << kSlotShift);  // slot within the bucket
   const uint32_t ob = ovf_index(kl);
   const uint32_t hi = (ob & 1u) ? v.w : v.y;
   w |= (uint32_t)((ob >> 1) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
@@ -340,10 +353,11 @@ __device__ __forceinline__ void chain_flush(const ProteinArgs& a, const uint8_t*
     const uint64_t g = q[e];
     uint64_t key;
     pack_window<K>(lut, window_bytes(res, g), key);
-    uint32_t fid = 0;
+    uint32_t fid = 0, sid = 0;
     const bool hit = walk_chain(a.slots, a.n_buckets, home_bucket(key, K, M, a.n_buckets), key,
-                                fid);
+                                fid, sid);
     a.hits[g] = hit ? fid + 1u : 0u;
+    a.sids[g] = sid;
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -355,7 +369,7 @@ __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
   const int t = threadIdx.x, part = t & 3;
   uint64_t* cq = chain_q[t >> 6];
   uint32_t cn = 0;  // wave-uniform queue length
-  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
+  if (a.reset_flag && blockIdx.x == 0 && t < 2) a.overflow_flag[t] = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
   // This segment's positions: [offsets[seq_lo], offsets[seq_hi]) relative to offsets[0],
@@ -428,7 +442,12 @@ __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint64_t g = g0 + j * 256 + t;
-      if (g < n_pos) a.hits[g] = bk[j] != kNone ? word[j] & 0x7FFFFFFFu : 0u;
+      if (g < n_pos) {
+        const uint32_t w = bk[j] != kNone ? word[j] & kWordFid : 0u;
+        a.hits[g] = w;
+        // Slot ids only under hits (K2 reads them nowhere else): misses store nothing.
+        if (w) a.sids[g] = bk[j] * kSlotsPerBucket + ((word[j] >> kSlotShift) & 7u);
+      }
       chain_push(cq, cn, bk[j] != kNone && word[j] == 0x80000000u, g);  // rare: chain walk
     }
     if (cn > kChainQ - 64 * U) {
@@ -457,7 +476,7 @@ __global__ __launch_bounds__(256) void probe_run_kernel(ProteinArgs a) {
   const int t = threadIdx.x, part = t & 3;
   uint64_t* cq = chain_q[t >> 6];
   uint32_t cn = 0;  // wave-uniform queue length
-  if (a.reset_flag && blockIdx.x == 0 && t == 0) *a.overflow_flag = 0u;  // K2 runs after K1
+  if (a.reset_flag && blockIdx.x == 0 && t < 2) a.overflow_flag[t] = 0u;  // K2 runs after K1
   lut[t] = a.lut[t];
   __syncthreads();
   const uint64_t o0 = a.offsets[0];
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(256) void probe_run_kernel(ProteinArgs a) {
       rw[2] = src[2];
       rsh = (uint32_t)(gc & 7);
     }
-    uint32_t word[R];
+    uint32_t word[R], sid[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       word[j] = 0;
@@ -548,14 +567,16 @@ __global__ __launch_bounds__(256) void probe_run_kernel(ProteinArgs a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       pend[j] = bk[j] != kNone && word[j] == 0x80000000u;  // rare: chain walk, deferred
-      word[j] = bk[j] != kNone ? word[j] & 0x7FFFFFFFu : 0u;
+      sid[j] = bk[j] * kSlotsPerBucket + ((word[j] >> kSlotShift) & 7u);
+      word[j] = bk[j] != kNone ? word[j] & kWordFid : 0u;
     }
     if (R == 4 && gl + R <= n_pos && (gl & 3) == 0) {
       *reinterpret_cast<uint4*>(a.hits + gl) = make_uint4(word[0], word[1], word[2], word[3]);
+      *reinterpret_cast<uint4*>(a.sids + gl) = make_uint4(sid[0], sid[1], sid[2], sid[3]);
     } else {
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        if (gl + j < n_pos) a.hits[gl + j] = word[j];
+        if (gl + j < n_pos) a.hits[gl + j] = word[j], a.sids[gl + j] = sid[j];
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) chain_push(cq, cn, pend[j], gl + j);
@@ -589,10 +610,18 @@ __device__ __forceinline__ uint32_t set_cap(uint32_t h) {
   return cap;
 }
 
-// A protein whose distinct-key set does not fit K2's LDS: appended to the workspace's pending
-// list (its length is the word K1 zeroes), voted by vote_long_kernel.
-__device__ __forceinline__ void push_pending(const ProteinArgs& a, uint32_t s) {
-  a.pending[atomicAdd(a.overflow_flag, 1u)] = s;
+// A protein with one role whose distinct-key set does not fit K2's LDS: appended to the
+// workspace's pending list (its length is the word K1 zeroes) with what K2 learned of it, and
+// counted by vote_long_kernel.
+// Two lists: sets of up to kLongWaveSet ids (a wave each in vote_long_kernel; length in
+// overflow_flag[0], records from pending[0]) and larger ones (a block each; length in
+// overflow_flag[1], records from pending[pending_half]).
+__device__ __forceinline__ void push_pending(const ProteinArgs& a, uint32_t s, uint32_t fid,
+                                             uint32_t hits, uint64_t base, uint32_t n_win) {
+  const bool big = set_cap(hits) > (uint32_t)kLongWaveSet;
+  PendingRec* r = big ? a.pending + a.pending_half + atomicAdd(a.overflow_flag + 1, 1u)
+                      : a.pending + atomicAdd(a.overflow_flag, 1u);
+  *r = PendingRec{s, fid, hits, n_win, base};
 }
 
 __device__ __forceinline__ void write_vote(const ProteinArgs& a, uint32_t s, uint32_t mn,
@@ -664,9 +693,8 @@ __device__ __forceinline__ void vote_range(const ProteinArgs& a, const uint8_t* 
 // the four consecutive windows X..X+3, X = (base & ~3) + kChunk * q + 4l, so its words are one
 // aligned 16-byte load and its residues (4 + K - 1 bytes) three aligned 8-byte words.
 struct Chunk {
-  uint32_t h[4];        // K1 word of each window (0: miss, outside the protein, or dead chunk)
-  uint64_t r0, r1, r2;  // residue words from 8-aligned offsets[0] + X (clamped)
-  uint32_t sh;          // byte offset of window X in r0
+  uint32_t h[4];    // K1 word of each window (0: miss, outside the protein, or dead chunk)
+  uint32_t sid[4];  // K1 slot id of each hit window: the key's identity in the table
 };
 static_assert(kVoteWin == 4, "a lane holds four consecutive windows of a chunk");
 
@@ -683,51 +711,40 @@ __device__ __forceinline__ void load_chunk(const ProteinArgs& a, uint64_t base, 
   const uint64_t X = live ? (base & ~3ull) + (uint64_t)q * kChunk + 4u * lane : 0;
   const uint64_t Xc = X <= last ? X : (last & ~3ull);
   const uint4 w = *reinterpret_cast<const uint4*>(a.hits + Xc);
-  const uint64_t ri = a.offsets[0] + (X <= last ? X : last);
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(a.residues + (ri & ~7ull));
-  c.r0 = src[0];
-  c.r1 = src[1];
-  c.r2 = src[2];
-  c.sh = (uint32_t)(ri & 7);
+  const uint4 d = *reinterpret_cast<const uint4*>(a.sids + Xc);
+  c.sid[0] = d.x;
+  c.sid[1] = d.y;
+  c.sid[2] = d.z;
+  c.sid[3] = d.w;
   const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) c.h[j] = (live && X + j >= base && X + j <= last) ? x[j] : 0u;
 }
 
-// Insert the chunk's hit keys in `set` (capacity cap); returns the wave's number of new keys.
-// The first attempts of the lane's four inserts are independent CASes issued together (one LDS
-// round trip); only a taken slot holding another key continues probing.
-template <int K>
-__device__ __forceinline__ uint32_t dedupe_insert(const uint8_t* lut, unsigned long long* set,
-                                                  uint32_t cap, const Chunk& c) {
-  uint64_t key[4];
-  uint32_t slot[4];
-  unsigned long long old[4];
+// Insert the chunk's hit keys in `set` (u32 entries: slot id + 1, 0 = empty; capacity cap, a
+// power of two); returns the wave's number of new keys. A key's slot id is unique in the table,
+// so equal ids are equal kmers. The first attempts of the lane's four inserts are independent
+// CASes issued together (one LDS round trip); only a taken slot holding another id continues.
+__device__ __forceinline__ uint32_t dedupe_insert(uint32_t* set, uint32_t cap, const Chunk& c) {
+  uint32_t key[4], slot[4], old[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t o = c.sh + j;
-    const uint64_t bytes = o < 8 ? funnel(c.r0, c.r1, o * 8) : funnel(c.r1, c.r2, (o - 8) * 8);
-#ifdef KMA_ABL_NOLUT  // timing ablation only (wrong keys if K < 8)
-    key[j] = bytes | 1;
-#else
-    pack_window<K>(lut, bytes, key[j]);
-#endif
-    slot[j] = set_hash(key[j]) & (cap - 1u);
+    key[j] = c.sid[j] + 1u;
+    slot[j] = mix32(key[j]) & (cap - 1u);
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    old[j] = c.h[j] ? atomicCAS(set + slot[j], 0ull, (unsigned long long)key[j]) : key[j];
+  for (int j = 0; j < 4; ++j) old[j] = c.h[j] ? atomicCAS(set + slot[j], 0u, key[j]) : key[j];
   uint32_t fresh = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    if (old[j] == 0ull) {
+    if (old[j] == 0u) {
       fresh++;
     } else if (old[j] != key[j]) {
       uint32_t i = slot[j];
       for (;;) {
         i = (i + 1u) & (cap - 1u);
-        const unsigned long long o = atomicCAS(set + i, 0ull, (unsigned long long)key[j]);
-        if (o == 0ull) { fresh++; break; }
+        const uint32_t o = atomicCAS(set + i, 0u, key[j]);
+        if (o == 0u) { fresh++; break; }
         if (o == key[j]) break;
       }
     }
@@ -739,13 +756,13 @@ __device__ __forceinline__ uint32_t dedupe_insert(const uint8_t* lut, unsigned l
 // K2 — vote. A block of kVoteWaves waves owns kVoteProteins consecutive proteins; their chunks
 // are dealt to the waves round-robin (chunk c to wave c % kVoteWaves), so a long protein is
 // spread over the block instead of one wave (no serial tail).
-//   pass 1: a wave loads its first kVoteHold chunks (words + residues) at once and keeps them
+//   pass 1: a wave loads its first kVoteHold chunks (words + slot ids) at once and keeps them
 //           in registers; per chunk, min fid, max fid and hits H go to LDS. No hit -> NONE; two
 //           roles -> AMBIGUOUS (badPeg); multiset -> count H; H < 2 -> count H: no set.
-//   pass 2: a protein with one role and H >= 2 gets a set of set_cap(H) u64 keys from the
-//           block's LDS pool; each hit window's key is re-packed from the held residues and
-//           inserted, so a kmer occurring twice in one protein counts once (ProteinKmers is a
-//           set). Chunks past the held ones (blocks with long proteins) are reloaded.
+//   pass 2: a protein with one role and H >= 2 gets a set of set_cap(H) u32 entries from the
+//           block's LDS pool; each hit window's slot id (K1: the key's unique slot in the
+//           table) is inserted, so a kmer occurring twice in one protein counts once
+//           (ProteinKmers is a set). Chunks past the held ones (long proteins) are reloaded.
 //   phase 3: proteins whose set did not fit beside the others take the whole pool in turn.
 // A protein whose set exceeds the pool is marked pending for vote_long_kernel.
 // The kernel is bound by dependent latency (offsets -> words -> LDS atomics; measured per phase
@@ -758,12 +775,11 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   constexpr int P = kVoteProteins;
   constexpr int U = kVoteHold;
   static_assert(P <= 64 && (P & (P - 1)) == 0, "header is one wave; binary search needs 2^n");
-  __shared__ __attribute__((aligned(16))) unsigned long long pool[kVotePool];
+  __shared__ __attribute__((aligned(16))) uint32_t pool[kVotePool];
   __shared__ uint64_t pbase_w[P];  // word index of window 0
   __shared__ uint32_t pwin[P], chunk0[P + 1], pmin[P], pmax[P], phits[P], pcnt[P], pbase[P],
       pcap[P];
   __shared__ uint32_t pool_top;
-  __shared__ uint8_t lut[256];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t p0 = a.seq_lo + blockIdx.x * P;
   const int np = (int)min<uint32_t>(P, a.seq_hi - p0);
@@ -776,7 +792,6 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
 #else
 #define KMA_TRACE_AT(n)
 #endif
-  for (int i = tid; i < 256; i += 64 * W) lut[i] = a.lut[i];
   if (wave == 0) {  // header: windows, chunk prefix (wave scan)
     uint32_t w = 0, nc = 0;
     uint64_t base = 0;
@@ -883,7 +898,7 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   auto finish = [&]() {
     if (tid < np) {
       if (pcap[tid] == kLongCap) {
-        push_pending(a, p0 + tid);
+        push_pending(a, p0 + tid, pmin[tid], phits[tid], pbase_w[tid], pwin[tid]);
       } else {
         write_vote(a, p0 + tid, pmin[tid], pmax[tid], pcnt[tid]);
       }
@@ -897,7 +912,7 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
     return;
   }
   uint4* pool4 = reinterpret_cast<uint4*>(pool);
-  for (uint32_t i = tid; i < used / 2; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t i = tid; i < used / 4; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   KMA_TRACE_AT(4)
   // ---- pass 2: distinct hit keys ----------------------------------------------------------------
@@ -907,7 +922,7 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
     const uint32_t c = wave + u * W, p = hp[u];
     const uint32_t cap = pcap[p];
     if (c >= n_chunks || cap == 0 || (cap & kDeferred)) continue;  // wave-uniform (kLongCap too)
-    const uint32_t fresh = dedupe_insert<K>(lut, pool + pbase[p], cap, held[u]);
+    const uint32_t fresh = dedupe_insert(pool + pbase[p], cap, held[u]);
     if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
   }
   for (uint32_t c = wave + U * W; c < n_chunks; c += W) {
@@ -916,7 +931,7 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
     if (cap == 0 || (cap & kDeferred)) continue;  // wave-uniform
     Chunk ch;
     load_chunk(a, pbase_w[p], pwin[p], c - chunk0[p], true, lane, ch);
-    const uint32_t fresh = dedupe_insert<K>(lut, pool + pbase[p], cap, ch);
+    const uint32_t fresh = dedupe_insert(pool + pbase[p], cap, ch);
     if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
   }
 #endif
@@ -928,12 +943,12 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
     if (!(cap & kDeferred) || cap == kLongCap) continue;  // block-uniform
     const uint32_t c2 = cap & ~kDeferred;
     __syncthreads();  // the pool's previous contents are no longer read
-    for (uint32_t i = tid; i < c2 / 2; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = tid; i < c2 / 4; i += 64 * W) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     for (uint32_t c = chunk0[p] + wave; c < chunk0[p + 1]; c += W) {
       Chunk ch;
       load_chunk(a, pbase_w[p], pwin[p], c - chunk0[p], true, lane, ch);
-      const uint32_t fresh = dedupe_insert<K>(lut, pool, c2, ch);
+      const uint32_t fresh = dedupe_insert(pool, c2, ch);
       if (lane == 0 && fresh) atomicAdd(pcnt + p, fresh);
     }
   }
@@ -944,138 +959,67 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2, wave form (default). Each wave owns kWaveProteins consecutive proteins and votes them on
-// its own: no block barrier after the LUT load, so a wave's latency chain (offsets -> words and
-// residues of up to kWaveHold chunks, all in flight -> DPP reductions -> LDS set inserts ->
-// outputs) is never coupled to a slower wave's.
-//   - chunks as in vote_kernel (4 consecutive windows per lane), dealt to the wave's proteins in
-//     order; the first kWaveHold stay in registers, later ones (long proteins) are re-read;
-//   - per protein: min fid, max fid, hits H (wave reductions, scalar accumulators);
-//     NONE / AMBIGUOUS / multiset / H < 2 are final;
-//   - otherwise a set of set_cap(H) u64 keys in the wave's LDS slice (kWaveSet entries; the
-//     wave's set proteins take it in turn); a larger set -> pending for vote_long_kernel.
+// K2, wave form (KMA_VOTE=wave). One wave per protein, one pass, no barrier: the wave streams its
+// protein's chunks (kWaveHold at a time, all in flight; 4 consecutive windows per lane as in
+// vote_kernel), reducing min fid / max fid / hits H (DPP wave reductions) and inserting every
+// hit's slot id into the wave's LDS set slice as it goes — speculatively, before the role is
+// known, so no chunk is read twice and no wave waits for another:
+//   NONE / AMBIGUOUS / multiset / H < 2 -> from the reductions;
+//   one role, H >= 2 -> count = distinct slot ids (ProteinKmers is a set);
+//   the set is capped at 3/4 of its kWaveSet slots: a protein that would pass the cap stops
+//   inserting and, if it has one role and H >= 2, goes to vote_long_kernel (pending list).
 // ---------------------------------------------------------------------------------------------
-template <int N, typename T>
-__device__ __forceinline__ T pick(const T (&v)[N], uint32_t i) {  // v[i], i wave-uniform
-  T r = v[0];
-#pragma unroll
-  for (int j = 1; j < N; ++j) r = i == (uint32_t)j ? v[j] : r;
-  return r;
-}
-
 template <int K>
 __global__ __launch_bounds__(256) void vote_wave_kernel(ProteinArgs a) {
-  constexpr int PW = kWaveProteins;
   constexpr int U = kWaveHold;
-  constexpr int S = kWaveSet;
-  static_assert(PW < 64, "one offset per lane");
-  __shared__ __attribute__((aligned(16))) unsigned long long sets[4][S];
-  __shared__ uint8_t lut[256];
+  constexpr uint32_t S = kWaveSet;
+  static_assert((S & (S - 1)) == 0 && S >= 512, "set slice: a power of two");
+  __shared__ __attribute__((aligned(16))) uint32_t sets[4][S];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t s0 = a.seq_lo + (blockIdx.x * 4u + wave) * PW;
-  const uint32_t n_here = s0 < a.seq_hi ? min((uint32_t)PW, a.seq_hi - s0) : 0u;
-  const uint64_t o0 = a.offsets[0];
-  const uint64_t off = lane <= (int)n_here ? a.offsets[s0 + (lane <= (int)n_here ? lane : 0)] : 0;
-  lut[tid] = a.lut[tid];
-  __syncthreads();  // the only barrier
-  if (n_here == 0) return;
-  const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
-  const int64_t adj = (a.flags & KMA_F_END_EXCLUSIVE) ? -K : -K + 1;
-  uint64_t base[PW];
-  uint32_t nwin[PW], c0[PW + 1];
-  c0[0] = 0;
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const uint64_t b = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), i) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)off, i);
-    const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), i + 1)
-                        << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)off, i + 1);
-    const int64_t n = (uint32_t)i < n_here ? (int64_t)(e - b) + adj : 0;
-    nwin[i] = n > 0 ? (uint32_t)n : 0u;
-    base[i] = b - o0;
-    c0[i + 1] = c0[i] + chunks_of(base[i], nwin[i]);
-  }
-  const uint32_t total = c0[PW];
-  auto owner = [&](uint32_t c) {
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 1; i < PW; ++i) p += c >= c0[i] ? 1u : 0u;
-    return p;
-  };
-  auto load = [&](uint32_t c, bool live, Chunk& ch) {
-    const uint32_t p = owner(live ? c : 0u);
-    load_chunk(a, pick(base, p), pick(nwin, p), live ? c - pick(c0, p) : 0u, live, lane, ch);
-    return p;
-  };
-  uint32_t mn[PW], mx[PW], hits[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) mn[i] = 0xFFFFFFFFu, mx[i] = 0u, hits[i] = 0u;
-  auto reduce = [&](const Chunk& ch, uint32_t p) {
-    uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, h = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (ch.h[j]) {
-        fmin = min(fmin, ch.h[j] - 1u);
-        fmax = max(fmax, ch.h[j] - 1u);
-        h++;
-      }
-    fmin = wave_min(fmin);
-    fmax = wave_max(fmax);
-    h = wave_sum(h);
-#pragma unroll
-    for (int i = 0; i < PW; ++i)
-      if ((uint32_t)i == p) mn[i] = min(mn[i], fmin), mx[i] = max(mx[i], fmax), hits[i] += h;
-  };
-  // ---- pass 1: all held chunks in flight at once ----------------------------------------------
-  Chunk held[U];
-  uint32_t hp[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) hp[u] = load((uint32_t)u, (uint32_t)u < total, held[u]);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    if ((uint32_t)u < total) reduce(held[u], hp[u]);
-  for (uint32_t c = U; c < total; ++c) {  // long proteins
-    Chunk ch;
-    const uint32_t p = load(c, true, ch);
-    reduce(ch, p);
-  }
-  // ---- decide, then the set proteins one at a time in the wave's slice -------------------------
-  unsigned long long* set = sets[wave];
-  uint32_t cnt[PW];
-  bool pending[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    cnt[i] = hits[i];
-    pending[i] = false;
-    if (mn[i] == 0xFFFFFFFFu || mn[i] != mx[i] || multiset || hits[i] < 2) continue;
-    const uint32_t cap = set_cap(hits[i]);
-    if (cap > (uint32_t)S) {
-      pending[i] = true;
-      continue;
-    }
-    uint4* set4 = reinterpret_cast<uint4*>(set);
-    for (uint32_t e = lane; e < cap / 2; e += 64) set4[e] = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t fresh = 0;
+  const uint32_t s = a.seq_lo + blockIdx.x * 4u + wave;
+  if (s >= a.seq_hi) return;  // wave-uniform; no barrier anywhere in this kernel
+  uint32_t* set = sets[wave];
+  uint4* set4 = reinterpret_cast<uint4*>(set);
+  for (uint32_t e = lane; e < S / 4; e += 64) set4[e] = make_uint4(0u, 0u, 0u, 0u);
+  const uint64_t o0 = a.offsets[0], beg = a.offsets[s], end = a.offsets[s + 1];
+  const int64_t n = (int64_t)(end - beg) - K + ((a.flags & KMA_F_END_EXCLUSIVE) ? 0 : 1);
+  const uint32_t n_win = n > 0 ? (uint32_t)n : 0u;
+  const uint64_t base = beg - o0;
+  const uint32_t nc = chunks_of(base, n_win);
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u, hits = 0u, distinct = 0u;
+  bool full = false;  // wave-uniform
+  for (uint32_t c0 = 0; c0 < nc; c0 += U) {
+    Chunk ch[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if ((uint32_t)u < total && hp[u] == (uint32_t)i)
-        fresh += dedupe_insert<K>(lut, set, cap, held[u]);
-    for (uint32_t c = max((uint32_t)U, c0[i]); c < c0[i + 1]; ++c) {  // re-read past the held
-      Chunk ch;
-      load(c, true, ch);
-      fresh += dedupe_insert<K>(lut, set, cap, ch);
+      load_chunk(a, base, n_win, c0 + u < nc ? c0 + u : 0u, c0 + u < nc, lane, ch[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (c0 + u >= nc) break;  // wave-uniform
+      uint32_t fmin = 0xFFFFFFFFu, fmax = 0u, h = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ch[u].h[j]) {
+          fmin = min(fmin, ch[u].h[j] - 1u);
+          fmax = max(fmax, ch[u].h[j] - 1u);
+          h++;
+        }
+      h = wave_sum(h);
+      if (h == 0u) continue;  // wave-uniform
+      mn = min(mn, wave_min(fmin));
+      mx = max(mx, wave_max(fmax));
+      hits += h;
+      full = full || distinct + h > S * 3 / 4;
+      if (!full) distinct += dedupe_insert(set, S, ch[u]);
     }
-    cnt[i] = fresh;
   }
-  // ---- outputs: lane i writes protein i ---------------------------------------------------------
-  if (lane < (int)n_here) {
-    const uint32_t i = (uint32_t)lane;
-    if (pick(pending, i)) {
-      push_pending(a, s0 + i);  // vote_long_kernel
-    } else {
-      write_vote(a, s0 + i, pick(mn, i), pick(mx, i), pick(cnt, i));
-    }
+  if (lane == 0) {
+    if (mn == 0xFFFFFFFFu || mn != mx || (a.flags & KMA_F_MULTISET) || hits < 2)
+      write_vote(a, s, mn, mx, hits);
+    else if (full)
+      push_pending(a, s, mn, hits, base, n_win);  // vote_long_kernel
+    else
+      write_vote(a, s, mn, mx, distinct);
   }
 }
 
@@ -1118,42 +1062,67 @@ __device__ void vote_long_one(const ProteinArgs& a, const uint8_t* lut, uint32_t
 
 template <int K>
 __global__ __launch_bounds__(256) void vote_long_kernel(ProteinArgs a) {
-  const uint32_t n = __hip_atomic_load(a.overflow_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (n == 0u || blockIdx.x >= n) return;
+  const uint32_t nw = __hip_atomic_load(a.overflow_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nb = __hip_atomic_load(a.overflow_flag + 1, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x * 4u >= nw && blockIdx.x >= nb) return;
   __shared__ __attribute__((aligned(16))) unsigned long long lds_set[kLongSet];
   __shared__ uint8_t lut[256];
   __shared__ uint32_t red[kWavesPerBlock];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   lut[tid] = a.lut[tid];
   __syncthreads();
-  // Proteins of up to kLongSet / 2 windows: an LDS set, every block.
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    const uint32_t s = a.pending[i];
-    const int64_t n_win = n_windows(a, s, K);
-    if (n_win > kLongSet / 2) continue;  // block-uniform
-    uint32_t cap = 64;
-    while (cap < 2 * (uint32_t)n_win) cap <<= 1;
-    vote_long_one<K>(a, lut, s, n_win, lds_set, cap, red);
+  // Sets of up to kLongWaveSet slot ids: one wave per protein, a quarter of the LDS set each.
+  // The role is known (K2 found one), so only the distinct keys are counted; all of the
+  // protein's chunks (up to kLongHold at a time) are in flight together.
+  uint32_t* wset = reinterpret_cast<uint32_t*>(lds_set) + wave * kLongWaveSet;
+  for (uint32_t i = blockIdx.x * 4u + wave; i < nw; i += gridDim.x * 4u) {
+    const PendingRec r = a.pending[i];
+    const uint32_t cap = set_cap(r.hits);
+    uint4* set4 = reinterpret_cast<uint4*>(wset);
+    for (uint32_t e = lane; e < cap / 4; e += 64) set4[e] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t nc = chunks_of(r.base, r.n_win);
+    uint32_t cnt = 0;
+    for (uint32_t c = 0; c < nc; c += kLongHold) {
+      Chunk ch[kLongHold];
+#pragma unroll
+      for (int u = 0; u < kLongHold; ++u)
+        load_chunk(a, r.base, r.n_win, c + u < nc ? c + u : 0u, c + u < nc, lane, ch[u]);
+#pragma unroll
+      for (int u = 0; u < kLongHold; ++u)
+        if (c + u < nc) cnt += dedupe_insert(wset, cap, ch[u]);
+    }
+    if (lane == 0) write_vote(a, r.s, r.fid, r.fid, cnt);
   }
-  if (blockIdx.x >= kFallbackBlocks) return;
-  // Longer proteins: the first kFallbackBlocks blocks, a set in workspace scratch.
+  if (blockIdx.x >= nb) return;  // block-uniform
+  __syncthreads();  // the wave slices are done: the whole set is the block's
+  // Larger sets: one block per protein, the whole LDS set (up to kLongSet / 2 windows), else
+  // the first kFallbackBlocks blocks with a set in workspace scratch.
+  const PendingRec* big = a.pending + a.pending_half;
   unsigned long long* gset =
       reinterpret_cast<unsigned long long*>(a.scratch) + (uint64_t)blockIdx.x * kFallbackCap;
-  for (uint32_t i = blockIdx.x; i < n; i += kFallbackBlocks) {
-    const uint32_t s = a.pending[i];
-    const int64_t n_win = n_windows(a, s, K);
-    if (n_win <= kLongSet / 2) continue;
-    if (n_win > (int64_t)(kFallbackCap / 2)) {
+  for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
+    const PendingRec r = big[i];
+    if (r.n_win > kLongSet / 2) continue;
+    uint32_t cap = 64;
+    while (cap < 2 * r.n_win) cap <<= 1;
+    vote_long_one<K>(a, lut, r.s, r.n_win, lds_set, cap, red);
+  }
+  if (blockIdx.x >= kFallbackBlocks) return;
+  for (uint32_t i = blockIdx.x; i < nb; i += kFallbackBlocks) {
+    const PendingRec r = big[i];
+    if (r.n_win <= kLongSet / 2) continue;
+    if (r.n_win > kFallbackCap / 2) {
       if (tid == 0) {
-        a.out_fid[s] = -1;
-        a.out_count[s] = 0;
-        a.out_status[s] = KMA_STATUS_TOO_LONG;
+        a.out_fid[r.s] = -1;
+        a.out_count[r.s] = 0;
+        a.out_status[r.s] = KMA_STATUS_TOO_LONG;
       }
       continue;
     }
     uint32_t cap = 64;
-    while (cap < 2 * (uint32_t)n_win) cap <<= 1;
-    vote_long_one<K>(a, lut, s, n_win, gset, cap, red);
+    while (cap < 2 * r.n_win) cap <<= 1;
+    vote_long_one<K>(a, lut, r.s, r.n_win, gset, cap, red);
   }
 }
 
@@ -1309,25 +1278,48 @@ static int probe_form() {
   return form;
 }
 
-template <int K, int M>
-static hipError_t launch_probe_km(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+// Resident blocks per CU of a K1 kernel (queried once): the grid is exactly the resident
+// population, so no block waits for a second round (a grid-stride tail measured 9% at c5).
+template <typename Kern>
+static unsigned resident_blocks(Kern kern) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256, 0) != hipSuccess || n < 1)
+    n = kProbeBlocksPerCU;
+  if (getenv("KMA_DEBUG")) fprintf(stderr, "kma: K1 resident blocks per CU = %d\n", n);
+  return (unsigned)n;
+}
+
+template <int K, int M, typename Kern>
+static hipError_t launch_probe_grid(Kern kern, unsigned bpc, const ProteinArgs& a, int n_cu,
+                                    hipStream_t stream) {
   // Grid from the batch average (the host does not see the segment's residue count).
   const uint64_t seg = a.seq_hi - a.seq_lo;
   const uint64_t n_pos = a.n_seq ? a.n_residues / a.n_seq * seg + 1 : 0;
   const uint64_t per_block = 256ull * kProbeWin;
   const uint64_t want = (n_pos + per_block - 1) / per_block;
-  const uint64_t cap = (uint64_t)n_cu * kProbeBlocksPerCU;
+  const uint64_t cap = (uint64_t)n_cu * bpc;
   if (!want || a.n_residues < (uint64_t)K) return hipSuccess;
   const dim3 grid((unsigned)(want < cap ? want : cap));
-  switch (probe_form()) {
-    case 2: hipLaunchKernelGGL((probe_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a); break;
-    case 1:
-      hipLaunchKernelGGL((probe_quad_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a);
-      break;
-    default:
-      hipLaunchKernelGGL((probe_run_kernel<K, M, kProbeWin>), grid, dim3(256), 0, stream, a);
-  }
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, a);
   return hipGetLastError();
+}
+
+template <int K, int M>
+static hipError_t launch_probe_km(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  switch (probe_form()) {
+    case 2: {
+      static const unsigned bpc = resident_blocks(probe_kernel<K, M, kProbeWin>);
+      return launch_probe_grid<K, M>(probe_kernel<K, M, kProbeWin>, bpc, a, n_cu, stream);
+    }
+    case 1: {
+      static const unsigned bpc = resident_blocks(probe_quad_kernel<K, M, kProbeWin>);
+      return launch_probe_grid<K, M>(probe_quad_kernel<K, M, kProbeWin>, bpc, a, n_cu, stream);
+    }
+    default: {
+      static const unsigned bpc = resident_blocks(probe_run_kernel<K, M, kProbeWin>);
+      return launch_probe_grid<K, M>(probe_run_kernel<K, M, kProbeWin>, bpc, a, n_cu, stream);
+    }
+  }
 }
 
 // Minimizer length is a template parameter of K1: m = min(K, 6), or 7 for large tables.
@@ -1342,16 +1334,18 @@ static hipError_t launch_probe_k(const ProteinArgs& a, int n_cu, hipStream_t str
 
 template <int K>
 static hipError_t launch_vote_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  // Block-shared form by default: it spreads a long protein over the block's waves (measured
+  // 18.8 vs 25 us at c2); KMA_VOTE=wave selects the barrier-free wave form (A/B).
   static const bool block_form = [] {
     const char* e = getenv("KMA_VOTE");
-    return e && e[0] == 'b';
+    return !(e && e[0] == 'w');
   }();
-  if (block_form) {  // KMA_VOTE=block: the block-shared form (A/B)
+  if (block_form) {
     const unsigned blocks = (a.seq_hi - a.seq_lo + kVoteProteins - 1) / kVoteProteins;
     if (!blocks) return hipSuccess;
     hipLaunchKernelGGL(vote_kernel<K>, dim3(blocks), dim3(64 * kVoteWaves), 0, stream, a);
   } else {
-    const uint64_t waves = (a.seq_hi - a.seq_lo + kWaveProteins - 1) / kWaveProteins;
+    const uint64_t waves = a.seq_hi - a.seq_lo;  // one per protein
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (!blocks) return hipSuccess;
     hipLaunchKernelGGL(vote_wave_kernel<K>, dim3(blocks), dim3(256), 0, stream, a);
@@ -1361,7 +1355,7 @@ static hipError_t launch_vote_k(const ProteinArgs& a, int n_cu, hipStream_t stre
 
 template <int K>
 static hipError_t launch_long_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  const unsigned blocks = (unsigned)max(kFallbackBlocks, n_cu * kLongBlocksPerCU);
+  const unsigned blocks = (unsigned)max(kFallbackBlocks, n_cu * kLongBlocksPerCU);  // early exit
   hipLaunchKernelGGL(vote_long_kernel<K>, dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
