@@ -144,9 +144,10 @@ int main(int argc, char** argv) {
     return 1;
   }
   std::printf("{\"buffer_MiB\": %llu, \"shape\": \"%s\", \"inflight\": %d, \"nt\": %d, "
-              "\"blocks_per_cu\": %d, \"GBps\": %.1f, \"lines_per_s\": %.4g}\n",
+              "\"blocks_per_cu\": %d, \"GBps\": %.1f, \"lines_per_s\": %.4g, "
+              "\"lines_per_launch\": %.0f}\n",
               (unsigned long long)mib, quad ? "quad" : "lane", inflight, (int)nt, bpc, gbs,
-              gbs * 1e9 / 64);
+              gbs * 1e9 / 64, lines);
   CHECK(hipFree(buf));
   return 0;
 }

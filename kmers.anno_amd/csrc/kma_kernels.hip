@@ -1355,7 +1355,9 @@ static hipError_t launch_vote_k(const ProteinArgs& a, int n_cu, hipStream_t stre
 
 template <int K>
 static hipError_t launch_long_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
-  const unsigned blocks = (unsigned)max(kFallbackBlocks, n_cu * kLongBlocksPerCU);  // early exit
+  // Usually nothing is pending and every block exits at once; the launch then costs the
+  // same ~4.5 us at 1, 64 or 1024 blocks (measured): the dispatch and one flag read.
+  const unsigned blocks = (unsigned)max(kFallbackBlocks, n_cu * kLongBlocksPerCU);
   hipLaunchKernelGGL(vote_long_kernel<K>, dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
