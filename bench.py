@@ -38,6 +38,9 @@ BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probe
 # kma_gather_bench, 1.5 GiB buffer, quad shape (profiles/r01_gather_bench.jsonl): random 64-B
 # lines beyond L2 are served at ~5.5e10/s on MI355X.
 GATHER_CEILING_GBS = 3544.2
+# Per-launch HBM traffic of K1 from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (scripts/
+# gpu_traffic.sh), calibrated on the gather bench (scripts/traffic_summary.py).
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
           "8-mer signature table, 1 MI355X per rank",
@@ -133,7 +136,7 @@ def main():
         te = torch.cuda.Event(enable_timing=True)
         tb.record()
         kmeranno.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
-                              fids.data_ptr(), t_size, status.data_ptr(), sp)
+                              fids.data_ptr(), t_size, status.data_ptr(), sp, k=K)
         te.record()
         torch.cuda.synchronize()
         st = status.cpu().numpy()
@@ -205,6 +208,17 @@ def main():
         # position probed, + 1 B per residue streamed in.
         alg_bytes = n_pos * (BYTES_PER_LOOKUP + 4) + n_res
         achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
+        k1_name = os.environ.get("KMA_PROBE", "quad")
+        k1_name = {"lane": "probe_kernel", "run": "probe_run_kernel"}.get(k1_name,
+                                                                          "probe_quad_kernel")
+        m = table.info.minimizer_len
+        k1_name = f"{k1_name}<{K}, {m}, 3>"
+        traffic = None
+        try:
+            tr = json.load(open(TRAFFIC_FILE))["workloads"][args.workload][k1_name]
+            traffic = tr["traffic_bytes"]
+        except (OSError, KeyError, ValueError):
+            pass
         out = {
             "metric": "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs "
                       "roofline",
@@ -230,8 +244,10 @@ def main():
             "gpu_ms_per_step": gpu_ms / args.steps,
             "phases_ms": {"probe_K1": k1_ms, "vote_K2": k2_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "probe_quad_kernel<8,4> (K1: every window's bucket gather)",
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": "profiles/r02_traffic.json (rocprofv3 FETCH_SIZE + "
+                                           "WRITE_SIZE per launch, calibrated)",
+                         "kernel": f"{k1_name} (K1: every window's bucket gather)",
                          "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
                          "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
         }

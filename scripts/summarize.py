@@ -20,7 +20,7 @@ for f in sorted(glob.glob(os.path.join(out, "bench*.log"))):
             r = d["roofline"]
             print(f"{os.path.basename(f)}: {d['config']['workload'][:3]} n={d['n_gpus']} "
                   f"{d['value'] / 1e9:.2f} G lookups/s  {d['ms_per_step']:.4f} ms/step  "
-                  f"call {r['call_ms']:.4f} ms  achieved {r['achieved']:.0f} GB/s frac {r['frac']:.3f}"
+                  f"K1 {r['kernel_ms']:.4f} ms  achieved {r['achieved']:.0f} GB/s frac {r['frac']:.3f}"
                   + (f"  cpu {d['cpu_baseline']['value'] / 1e6:.2f} M/s" if "cpu_baseline" in d else ""))
 for f in sorted(glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True)):
     print(f)
