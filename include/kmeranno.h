@@ -79,7 +79,7 @@ extern "C" {
  *   codes 28..31 are assigned (in byte order) to at most four other bytes that occur in the
  *   table's kmers; 0 never occurs, so key 0 is the empty-slot sentinel. Packing is injective,
  *   so key equality is exactly the String.equals of the reference's HashMap lookup.
- * A table slot is the 64-bit word (key << 24) | fid, so fid < 2^24.                         */
+ * A table slot holds the key's 40 bits, an overflow-filter bit and the fid, so fid < 2^23.   */
 #define KMA_MAX_K 8
 #define KMA_MAX_FID ((1u << 23) - 1u)
 
@@ -141,8 +141,9 @@ int kma_table_destroy(kma_table* table);
  * that is later broadcast over RCCL to the other GPUs of the node).
  *   kma_table_buckets_for : bucket count for n keys at the load factor
  *   kma_table_build_device: d_slots (n_buckets*64 bytes) and d_winner (n_buckets*8 u32) are
- *                           caller scratch; keys/fids are device arrays; builds on `stream`;
- *                           d_status (4 u32) receives {table full, entries, max probe}.
+ *                           caller scratch; keys/fids are device arrays of K-mers (the layout
+ *                           depends on K); builds on `stream`; d_status (4 u32) receives
+ *                           {table full, entries, max probe}; fids are masked to 23 bits.
  *   kma_table_wrap_device : adopt an already-built slot array (not owned, not freed).        */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
@@ -155,7 +156,8 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 
 /* ---- workspaces -----------------------------------------------------------------------------
  * Per-stream scratch of the _device entry points. kma_workspace_reserve sizes it for calls of
- * up to n_residues residues (4 bytes per residue of HBM); it is the only call that allocates. */
+ * up to n_residues residues (8 bytes per residue of HBM: K1 words and slot ids); it is the
+ * only call that allocates.                                                                  */
 int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_destroy(kma_workspace* ws);
