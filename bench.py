@@ -40,7 +40,7 @@ BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probe
 GATHER_CEILING_GBS = 3544.2
 # Per-launch HBM traffic of K1 from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (scripts/
 # gpu_traffic.sh), calibrated on the gather bench (scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01b_traffic.json")
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
           "8-mer signature table, 1 MI355X per rank",
@@ -245,7 +245,7 @@ def main():
             "phases_ms": {"probe_K1": k1_ms, "vote_K2": k2_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": "profiles/r02_traffic.json (rocprofv3 FETCH_SIZE + "
+                         "traffic_source": "profiles/r01b_traffic.json (rocprofv3 FETCH_SIZE + "
                                            "WRITE_SIZE per launch, calibrated)",
                          "kernel": f"{k1_name} (K1: every window's bucket gather)",
                          "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
