@@ -163,7 +163,7 @@ int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_destroy(kma_workspace* ws);
 /* Per-phase device timing of the _device calls made with this workspace: with enable = 1 each
  * call records hipEvents on its stream around the probe phase (every window's table lookup)
- * and the vote phase (set semantics + vote). Not for graph capture. _read synchronises on
+ * and the vote phase (set semantics + vote; for kma_annotate_contigs_device: scan + emit). Not for graph capture. _read synchronises on
  * the recorded events (the last 256 calls), returns their count and summed milliseconds, and
  * clears the accumulators.                                                                  */
 int kma_workspace_timing(kma_workspace* ws, int enable);
@@ -200,6 +200,19 @@ int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
 int kma_annotate_contigs(const kma_table* table, const uint8_t* dna, const uint64_t* offsets,
                          uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
                          uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid);
+/* Device form (same semantics), asynchronous on `stream`: d_dna / d_offsets are device buffers
+ * on the table's device (contig s = d_dna[d_offsets[s] .. d_offsets[s+1]); d_offsets[0] may
+ * be nonzero); n_bases = offsets[n_contig] - offsets[0] (<= the contig reservation of `ws`);
+ * d_dna readable for 64 bytes past the last base. Hits [0, cap) go to d_hits in canonical
+ * order and *d_n_hits (device u64) receives the total, which may exceed cap (then the hits
+ * past cap are dropped: compare and call again with a larger buffer). d_tally (n_contig x
+ * n_fid u32, optional) is accumulated into. Never allocates or synchronises.                 */
+int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases);
+int kma_annotate_contigs_device(const kma_table* table, kma_workspace* ws, const uint8_t* d_dna,
+                                const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,
+                                int genetic_code, kma_hit* d_hits, uint64_t cap,
+                                uint64_t* d_n_hits, uint32_t* d_tally, uint32_t n_fid,
+                                void* stream);
 /* Window count of the 6-frame extractor before the '*'/'X' filter (for throughput metrics).  */
 uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k);
 

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -55,6 +56,13 @@ struct kma_workspace {
   uint32_t* d_hits = nullptr;  // K1 words (fid + 1), then K1 slot ids: u32 per residue each
   kma::PendingRec* d_pending = nullptr;  // K2 -> vote_long list (> 128 windows each)
   uint64_t hits_cap = 0;
+  // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
+  uint64_t* d_cstage = nullptr;
+  uint32_t* d_ccounts = nullptr;
+  uint64_t* d_cprefix = nullptr;
+  void* d_ctemp = nullptr;
+  size_t ctemp_bytes = 0;
+  uint64_t contig_cap = 0;  // bases
   // Segmented overlap: K2 of segment i on `side` while K1 of segment i + 1 runs on the call's
   // stream (fork/join through events, graph-capturable).
   hipStream_t side = nullptr;
@@ -408,6 +416,92 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
   return KMA_OK;
 }
 
+}  // extern "C"
+
+namespace {
+void free_contig_scratch(kma_workspace* ws) {
+  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix, ws->d_ctemp})
+    if (p) (void)hipFree(p);
+  ws->d_cstage = nullptr;
+  ws->d_ccounts = nullptr;
+  ws->d_cprefix = nullptr;
+  ws->d_ctemp = nullptr;
+  ws->ctemp_bytes = 0;
+  ws->contig_cap = 0;
+}
+
+uint64_t contig_blocks(uint64_t n_bases) {
+  return std::max<uint64_t>(1, (n_bases + kma::kContigTile - 1) / kma::kContigTile);
+}
+
+// Codon table of an NCBI code as 5-bit amino-acid codes (0 = stop or ambiguous).
+void codon_codes(const char* code, uint8_t out[64]) {
+  for (int i = 0; i < 64; ++i)
+    out[i] = (code[i] == '*' || code[i] == 'X') ? 0 : (uint8_t)(code[i] - 'A' + 1);
+}
+
+// The 6-frame pass: probe + block compaction and the block-count scan (enqueue_contigs), then
+// the canonical-order emit (enqueue_contig_emit; with out = null it only publishes the count).
+kma::ContigArgs contig_args(const kma_table* t, kma_workspace* ws, const uint8_t* d_dna,
+                            const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,
+                            const char* code, uint32_t* d_tally, uint32_t n_fid) {
+  kma::ContigArgs a{};
+  a.slots = t->d_slots;
+  a.n_buckets = (uint32_t)t->n_buckets;
+  a.dna = d_dna;
+  a.offsets = d_offsets;
+  a.n_contig = n_contig;
+  a.total_bases = n_bases;
+  a.k = t->k;
+  a.mlen = t->mlen;
+  a.staging = ws->d_cstage;
+  a.block_counts = ws->d_ccounts;
+  a.prefix = ws->d_cprefix;
+  a.tally = d_tally;
+  a.n_fid = d_tally ? n_fid : 0;
+  codon_codes(code, a.codon_codes);
+  return a;
+}
+
+int enqueue_contigs(kma_workspace* ws, const kma::ContigArgs& a, hipStream_t s) {
+  const uint64_t nb = contig_blocks(a.total_bases);
+  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
+  size_t tb = ws->ctemp_bytes;
+  KMA_HIP(kma::launch_contig_scan(ws->d_ccounts, ws->d_cprefix, nb, ws->d_ctemp, &tb, s));
+  return KMA_OK;
+}
+
+int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
+                        hipStream_t s) {
+  a.out = d_hits;
+  a.cap = d_hits ? cap : 0;
+  a.n_hits = d_n_hits;
+  KMA_HIP(kma::launch_contigs_emit(a, contig_blocks(a.total_bases), s));
+  return KMA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  if (n_bases >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
+  if (ws->d_cstage && n_bases <= ws->contig_cap) return KMA_OK;
+  DeviceScope ds(ws->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
+  free_contig_scratch(ws);
+  const uint64_t nb = contig_blocks(n_bases);
+  size_t tb = 0;
+  KMA_HIP(kma::launch_contig_scan(nullptr, nullptr, nb, nullptr, &tb, nullptr));
+  KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * 8));
+  KMA_HIP(hipMalloc(&ws->d_ccounts, nb * 4));
+  KMA_HIP(hipMalloc(&ws->d_cprefix, nb * 8));
+  KMA_HIP(hipMalloc(&ws->d_ctemp, tb ? tb : 1));
+  ws->ctemp_bytes = tb;
+  ws->contig_cap = nb * kma::kContigTile;
+  return KMA_OK;
+}
+
 int kma_workspace_create(int device, kma_workspace** out) {
   if (!out) return fail(KMA_E_INVALID, "null argument");
   DeviceScope ds(device);
@@ -500,6 +594,7 @@ int kma_workspace_destroy(kma_workspace* ws) {
   (void)hipFree(ws->d_scratch);
   if (ws->d_hits) (void)hipFree(ws->d_hits);
   if (ws->d_pending) (void)hipFree(ws->d_pending);
+  free_contig_scratch(ws);
   delete ws;
   return KMA_OK;
 }
@@ -663,6 +758,44 @@ uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int
   return n;
 }
 
+int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uint8_t* d_dna,
+                                const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,
+                                int genetic_code, kma_hit* d_hits, uint64_t cap,
+                                uint64_t* d_n_hits, uint32_t* d_tally, uint32_t n_fid,
+                                void* stream) {
+  if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
+  if (ws->device != t->device) return fail(KMA_E_INVALID, "workspace on another device");
+  const char* code = ncbi_code(genetic_code);
+  if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
+  if (!d_n_hits) return fail(KMA_E_INVALID, "null n_hits");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DeviceScope ds(t->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  if (n_contig == 0 || n_bases == 0) {
+    KMA_HIP(hipMemsetAsync(d_n_hits, 0, 8, s));
+    return KMA_OK;
+  }
+  if (!d_dna || !d_offsets) return fail(KMA_E_INVALID, "null device buffer");
+  if (n_bases > ws->contig_cap)
+    return fail(KMA_E_CAPACITY, "workspace reserved for %llu bases, call needs %llu",
+                (unsigned long long)ws->contig_cap, (unsigned long long)n_bases);
+  const kma::ContigArgs a =
+      contig_args(t, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid);
+  hipEvent_t* ev = nullptr;  // timing mode: (start, after the probe kernel, end)
+  if (ws->timing) {
+    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
+    KMA_HIP(hipEventRecord(ev[0], s));
+  }
+  const uint64_t nb = contig_blocks(n_bases);
+  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
+  if (ev) KMA_HIP(hipEventRecord(ev[1], s));
+  size_t tb = ws->ctemp_bytes;
+  KMA_HIP(kma::launch_contig_scan(ws->d_ccounts, ws->d_cprefix, nb, ws->d_ctemp, &tb, s));
+  const int rc = enqueue_contig_emit(a, d_hits, cap, d_n_hits, s);
+  if (rc == KMA_OK && ev) KMA_HIP(hipEventRecord(ev[2], s));
+  return rc;
+}
+
 int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
                          uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
                          uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid) {
@@ -676,69 +809,50 @@ int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t*
     if (offsets[c + 1] < offsets[c]) return fail(KMA_E_INVALID, "offsets decrease at %u", c);
   const uint64_t base = offsets[0], total = offsets[n_contig] - base;
   if (total >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
+  if (total == 0) return KMA_OK;
   std::vector<uint64_t> rel(offsets, offsets + n_contig + 1);
   for (auto& o : rel) o -= base;
-  uint8_t codes[64];
-  for (int i = 0; i < 64; ++i)
-    codes[i] = (code[i] == '*' || code[i] == 'X') ? 0 : (uint8_t)(code[i] - 'A' + 1);
   DeviceScope ds(t->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  const uint64_t n_blocks = std::max<uint64_t>(1, (total + kma::kContigTile - 1) / kma::kContigTile);
+  kma_workspace* ws = nullptr;
+  int rc = kma_workspace_create(t->device, &ws);
+  if (rc != KMA_OK) return rc;
+  std::unique_ptr<kma_workspace, int (*)(kma_workspace*)> ws_guard(ws, kma_workspace_destroy);
+  rc = kma_workspace_reserve_contigs(ws, total);
+  if (rc != KMA_OK) return rc;
   DevBufs b;
-  uint8_t *d_dna, *d_codes;
-  uint64_t *d_off, *d_staging, *d_prefix;
-  uint32_t *d_counts, *d_tally = nullptr;
+  uint8_t* d_dna;
+  uint64_t *d_off, *d_n;
+  uint32_t* d_tally = nullptr;
+  kma_hit* d_out = nullptr;
   KMA_HIP(b.alloc(&d_dna, total + 64));
   KMA_HIP(b.alloc(&d_off, (n_contig + 1) * 8ull));
-  KMA_HIP(b.alloc(&d_codes, 64));
-  KMA_HIP(b.alloc(&d_staging, n_blocks * 2 * kma::kContigTile * 8));
-  KMA_HIP(b.alloc(&d_counts, n_blocks * 4));
-  KMA_HIP(b.alloc(&d_prefix, n_blocks * 8));
+  KMA_HIP(b.alloc(&d_n, 8));
   KMA_HIP(hipMemcpy(d_dna, dna + base, total, hipMemcpyHostToDevice));
   KMA_HIP(hipMemset(d_dna + total, 0, 64));
   KMA_HIP(hipMemcpy(d_off, rel.data(), (n_contig + 1) * 8ull, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemcpy(d_codes, codes, 64, hipMemcpyHostToDevice));
-  if (out_tally && n_fid) {
-    const uint64_t tb = (uint64_t)n_contig * n_fid * 4;
+  const uint64_t tb = out_tally && n_fid ? (uint64_t)n_contig * n_fid * 4 : 0;
+  if (tb) {
     KMA_HIP(b.alloc(&d_tally, tb));
     KMA_HIP(hipMemcpy(d_tally, out_tally, tb, hipMemcpyHostToDevice));
   }
-  kma::ContigArgs a{};
-  a.slots = t->d_slots;
-  a.n_buckets = (uint32_t)t->n_buckets;
-  a.dna = d_dna;
-  a.offsets = d_off;
-  a.n_contig = n_contig;
-  a.total_bases = total;
-  a.k = t->k;
-  a.mlen = t->mlen;
-  a.codon_codes = d_codes;
-  a.staging = d_staging;
-  a.block_counts = d_counts;
-  a.tally = d_tally;
-  a.n_fid = d_tally ? n_fid : 0;
-  KMA_HIP(kma::launch_contigs_probe(a, n_blocks, nullptr));
-  size_t temp_bytes = 0;
-  KMA_HIP(kma::launch_contig_scan(d_counts, d_prefix, n_blocks, nullptr, &temp_bytes, nullptr));
-  void* d_temp;
-  KMA_HIP(b.alloc(&d_temp, temp_bytes));
-  KMA_HIP(kma::launch_contig_scan(d_counts, d_prefix, n_blocks, d_temp, &temp_bytes, nullptr));
-  uint64_t last_prefix = 0;
-  uint32_t last_count = 0;
-  KMA_HIP(hipMemcpy(&last_prefix, d_prefix + n_blocks - 1, 8, hipMemcpyDeviceToHost));
-  KMA_HIP(hipMemcpy(&last_count, d_counts + n_blocks - 1, 4, hipMemcpyDeviceToHost));
-  const uint64_t nh = last_prefix + last_count;
+  const kma::ContigArgs a =
+      contig_args(t, ws, d_dna, d_off, n_contig, total, code, d_tally, n_fid);
+  rc = enqueue_contigs(ws, a, nullptr);
+  if (rc == KMA_OK) rc = enqueue_contig_emit(a, nullptr, 0, d_n, nullptr);  // count only
+  if (rc != KMA_OK) return rc;
+  uint64_t nh = 0;
+  KMA_HIP(hipMemcpy(&nh, d_n, 8, hipMemcpyDeviceToHost));
   *n_hits = nh;
   // On KMA_E_CAPACITY nothing is written (the tally neither), so the caller can retry.
-  if (nh > cap) return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
-                            (unsigned long long)cap);
-  if (d_tally)
-    KMA_HIP(hipMemcpy(out_tally, d_tally, (uint64_t)n_contig * n_fid * 4, hipMemcpyDeviceToHost));
+  if (nh > cap || (nh && !out_hits))
+    return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
+                (unsigned long long)(out_hits ? cap : 0));
+  if (tb) KMA_HIP(hipMemcpy(out_tally, d_tally, tb, hipMemcpyDeviceToHost));
   if (nh == 0) return KMA_OK;
-  if (!out_hits) return fail(KMA_E_INVALID, "null out_hits");
-  uint8_t* d_out;
   KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
-  KMA_HIP(kma::launch_contigs(a, n_blocks, d_prefix, d_out, nullptr));
+  rc = enqueue_contig_emit(a, d_out, nh, d_n, nullptr);
+  if (rc != KMA_OK) return rc;
   KMA_HIP(hipMemcpy(out_hits, d_out, nh * sizeof(kma_hit), hipMemcpyDeviceToHost));
   return KMA_OK;
 }

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/kmeranno.h"
+
 namespace kma {
 
 // ---- signature-table layout in HBM ------------------------------------------------------------
@@ -176,17 +178,21 @@ constexpr uint32_t kFallbackCap = 1u << 17;  // u64 entries per block (1 MiB)
 struct ContigArgs {
   const uint64_t* slots;
   uint32_t n_buckets;
-  const uint8_t* dna;
-  const uint64_t* offsets;
+  const uint8_t* dna;          // contig s is dna[offsets[s] .. offsets[s+1])
+  const uint64_t* offsets;     // n_contig + 1 (device); offsets[0] need not be 0
   uint32_t n_contig;
-  uint64_t total_bases;
+  uint64_t total_bases;        // offsets[n_contig] - offsets[0] (< 2^39)
   int32_t k;
   int32_t mlen;
-  const uint8_t* codon_codes;  // 64 entries (TCAG order): 5-bit aa code, 0 = stop
-  uint64_t* staging;           // n_blocks x kContigTile*2 packed hits
+  uint64_t* staging;           // n_blocks x kContigTile*2 packed hits (relative position)
   uint32_t* block_counts;      // n_blocks
+  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (emit pass)
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
+  kma_hit* out;                // emit pass: hits [0, cap) in canonical order
+  uint64_t cap;
+  uint64_t* n_hits;            // emit pass: total hits (also when > cap)
+  uint8_t codon_codes[64];     // by value (TCAG order): 5-bit aa code, 0 = stop
 };
 constexpr int kContigTile = 256;  // forward positions per block
 
@@ -200,8 +206,7 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
 hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K1
 hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream);   // K2 (segment)
 hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream);   // long proteins
-hipError_t launch_contigs(const ContigArgs& a, uint64_t n_blocks, const uint64_t* d_prefix,
-                          uint8_t* out_hits, hipStream_t stream);
+hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
                               void* temp, size_t* temp_bytes, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);

@@ -1158,15 +1158,14 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
   constexpr int kSpan = kContigTile + 3 * KMA_MAX_K;
   __shared__ uint8_t bases[kSpan];
   __shared__ uint8_t aa_p[kSpan], aa_m[kSpan];
-  __shared__ uint8_t codes[64];
   __shared__ uint32_t wave_tot[kWavesPerBlock];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int k = a.k;
-  const uint64_t g0 = (uint64_t)blockIdx.x * kContigTile;
-  if (t < 64) codes[t] = a.codon_codes[t];
+  const uint64_t base = a.offsets[0], end = base + a.total_bases;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;  // relative to base
   for (int i = t; i < kSpan; i += blockDim.x) {
-    const uint64_t g = g0 + i;
-    bases[i] = (uint8_t)(g < a.total_bases ? base2(a.dna[g]) : 4u);
+    const uint64_t g = base + r0 + i;
+    bases[i] = (uint8_t)(g < end ? base2(a.dna[g]) : 4u);
   }
   __syncthreads();
   for (int i = t; i < kSpan - 2; i += blockDim.x) {
@@ -1174,16 +1173,16 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
     if ((b0 | b1 | b2) & 4u) {
       aa_p[i] = aa_m[i] = 0;  // 'X'
     } else {
-      aa_p[i] = codes[b0 * 16 + b1 * 4 + b2];
-      aa_m[i] = codes[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
+      aa_p[i] = a.codon_codes[b0 * 16 + b1 * 4 + b2];  // kernarg (scalar) loads
+      aa_m[i] = a.codon_codes[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
     }
   }
   __syncthreads();
 
-  const uint64_t g = g0 + t;
+  const uint64_t r = r0 + t, g = base + r;
   bool hp = false, hm = false;
   uint32_t fp = 0, fm = 0, contig = 0;
-  if (g < a.total_bases) {
+  if (g < end) {
     contig = contig_of(a.offsets, a.n_contig, g);
     const int64_t x = (int64_t)(g - a.offsets[contig]);
     const int64_t len = (int64_t)(a.offsets[contig + 1] - a.offsets[contig]);
@@ -1213,20 +1212,156 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
     total += wave_tot[w];
   }
   uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
-  if (hp) st[o++] = (g << 25) | fp;                // strand bit 24 = 0: '+'
-  if (hm) st[o] = (g << 25) | (1ull << 24) | fm;   // '-'
+  if (hp) st[o++] = (r << 25) | fp;                // strand bit 24 = 0: '+'
+  if (hm) st[o] = (r << 25) | (1ull << 24) | fm;   // '-'
   if (t == 0) a.block_counts[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a,
-                                                           const uint64_t* __restrict__ prefix,
-                                                           kma_hit* __restrict__ out) {
+// Quad form of the 6-frame probe (default; KMA_CPROBE=lane selects the kernel above). Same
+// tile, translation and compaction; the two windows a position anchors ('+' and '-') are
+// probed with the K1 quad-cooperative bucket loads (both probes' 8 dwordx4 of a lane in flight
+// before any compare, DPP quad match), the block's contigs are found once (two searches by
+// thread 0) and their offsets cached in LDS, so a position's contig costs no global loads.
+constexpr int kOffCache = 64;
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
+  constexpr int kSpan = kContigTile + 3 * K;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  __shared__ uint8_t bases[kSpan];
+  __shared__ uint8_t aa_p[kSpan], aa_m[kSpan];
+  __shared__ uint64_t offc[kOffCache + 1];
+  __shared__ uint32_t crange[2];
+  __shared__ uint32_t wave_tot[kWavesPerBlock];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
+  const uint64_t base = a.offsets[0], end = base + a.total_bases;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
+  const uint32_t nb = a.n_buckets;
+  if (t == 0) {
+    const uint64_t last = r0 + kContigTile < a.total_bases ? r0 + kContigTile : a.total_bases;
+    crange[0] = contig_of(a.offsets, a.n_contig, base + r0);
+    crange[1] = contig_of(a.offsets, a.n_contig, base + last - 1);
+  }
+  for (int i = t; i < kSpan; i += blockDim.x) {
+    const uint64_t g = base + r0 + i;
+    bases[i] = (uint8_t)(g < end ? base2(a.dna[g]) : 4u);
+  }
+  __syncthreads();
+  const uint32_t c_lo = crange[0], nc = crange[1] - c_lo + 1;  // contigs meeting the tile
+  if (nc <= (uint32_t)kOffCache)
+    for (uint32_t i = t; i <= nc; i += blockDim.x) offc[i] = a.offsets[c_lo + i];
+  for (int i = t; i < kSpan - 2; i += blockDim.x) {
+    const uint32_t b0 = bases[i], b1 = bases[i + 1], b2 = bases[i + 2];
+    if ((b0 | b1 | b2) & 4u) {
+      aa_p[i] = aa_m[i] = 0;  // 'X'
+    } else {
+      aa_p[i] = a.codon_codes[b0 * 16 + b1 * 4 + b2];
+      aa_m[i] = a.codon_codes[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
+    }
+  }
+  __syncthreads();
+
+  const uint64_t r = r0 + t, g = base + r;
+  uint32_t contig = c_lo;
+  int64_t x = 0, len = 0;
+  if (g < end) {
+    if (nc <= (uint32_t)kOffCache) {
+      uint32_t lo = 0, hi = nc;  // largest i < nc with offc[i] <= g
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offc[mid] <= g) lo = mid; else hi = mid;
+      }
+      contig = c_lo + lo;
+      x = (int64_t)(g - offc[lo]);
+      len = (int64_t)(offc[lo + 1] - offc[lo]);
+    } else {
+      contig = contig_of(a.offsets, a.n_contig, g);
+      x = (int64_t)(g - a.offsets[contig]);
+      len = (int64_t)(a.offsets[contig + 1] - a.offsets[contig]);
+    }
+  }
+  bool pv = g < end && x + 3 * K + 3 <= len, mv = g < end && x >= 3 && x + 3 * K <= len;
+  uint64_t key[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t cp = aa_p[t + 3 * j], cm = aa_m[t + 3 * j];
+    pv = pv && cp != 0u;
+    mv = mv && cm != 0u;
+    key[0] = (key[0] << 5) | cp;
+    key[1] |= (uint64_t)cm << (5 * j);
+  }
+  uint32_t bk[2], klo[2], khi[2];
+  bk[0] = pv ? home_bucket(key[0], K, M, nb) : kNone;
+  bk[1] = mv ? home_bucket(key[1], K, M, nb) : kNone;
+  uint4 q[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    klo[j] = (uint32_t)key[j];
+    khi[j] = (uint32_t)(key[j] >> 32) << 24;
+    const uint32_t b0 = quad_bcast<0>(bk[j]), b1 = quad_bcast<1>(bk[j]);
+    const uint32_t b2 = quad_bcast<2>(bk[j]), b3 = quad_bcast<3>(bk[j]);
+    const uint4* sp = reinterpret_cast<const uint4*>(a.slots) + part;
+    q[j][0] = sp[(uint64_t)(b0 == kNone ? 0u : b0) * 4];
+    q[j][1] = sp[(uint64_t)(b1 == kNone ? 0u : b1) * 4];
+    q[j][2] = sp[(uint64_t)(b2 == kNone ? 0u : b2) * 4];
+    q[j][3] = sp[(uint64_t)(b3 == kNone ? 0u : b3) * 4];
+  }
+  uint32_t word[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    word[j] = 0;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const uint32_t kl = rr == 0 ? quad_bcast<0>(klo[j]) : rr == 1 ? quad_bcast<1>(klo[j])
+                        : rr == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
+      const uint32_t kh = rr == 0 ? quad_bcast<0>(khi[j]) : rr == 1 ? quad_bcast<1>(khi[j])
+                        : rr == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
+      const uint32_t v = match_part(q[j][rr], kl, kh, part);
+      word[j] = part == rr ? v : word[j];
+    }
+  }
+  bool hit[2];
+  uint32_t fid[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t w = bk[j] != kNone ? word[j] : 0u;
+    hit[j] = (w & kWordFid) != 0u;
+    fid[j] = (w & kWordFid) - 1u;
+    if (w == 0x80000000u) {  // rare: the home bucket missed with the key's overflow bit set
+      uint32_t sid;
+      hit[j] = walk_chain(a.slots, nb, bk[j], key[j], fid[j], sid);
+    }
+  }
+  if (a.tally) {
+    if (hit[0] && fid[0] < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fid[0], 1u);
+    if (hit[1] && fid[1] < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fid[1], 1u);
+  }
+  // Block-local compaction in canonical order (position, '+' before '-').
+  const uint64_t bp = __ballot(hit[0]), bm = __ballot(hit[1]);
+  if (lane == 0) wave_tot[wave] = (uint32_t)(__popcll(bp) + __popcll(bm));
+  __syncthreads();
+  uint32_t o = popc_below(bp) + popc_below(bm), total = 0;
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    if (w < wave) o += wave_tot[w];
+    total += wave_tot[w];
+  }
+  uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
+  if (hit[0]) st[o++] = (r << 25) | fid[0];               // strand bit 24 = 0: '+'
+  if (hit[1]) st[o] = (r << 25) | (1ull << 24) | fid[1];  // '-'
+  if (t == 0) a.block_counts[blockIdx.x] = total;
+}
+
+// Emit pass: block b's staged hits go to out[prefix[b] ..], those past `cap` are dropped; the
+// last block publishes the total (the caller compares it with cap).
+__global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a) {
   const uint32_t n = a.block_counts[blockIdx.x];
-  if ((uint32_t)threadIdx.x >= n) return;
+  const uint64_t p0 = a.prefix[blockIdx.x];
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *a.n_hits = p0 + n;
   const uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+  const uint64_t base = a.offsets[0];
+  for (uint32_t i = threadIdx.x; i < n && p0 + i < a.cap; i += blockDim.x) {
     const uint64_t v = st[i];
-    const uint64_t g = v >> 25;
+    const uint64_t g = base + (v >> 25);
     const bool minus = (v >> 24) & 1u;
     const uint32_t c = contig_of(a.offsets, a.n_contig, g);
     const int64_t x = (int64_t)(g - a.offsets[c]);
@@ -1238,7 +1373,7 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a,
     h.strand = minus ? '-' : '+';
     h.frame = (uint8_t)((minus ? (len - 3 * a.k - x) : x) % 3 + 1);
     h.pad = 0;
-    out[prefix[blockIdx.x] + i] = h;
+    a.out[p0 + i] = h;
   }
 }
 
@@ -1390,9 +1525,43 @@ hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream) {
   KMA_DISPATCH_K(launch_long_k)
 }
 
-hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
-  hipLaunchKernelGGL(contigs_probe_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a);
+template <int K>
+static hipError_t launch_contigs_probe_k(const ContigArgs& a, uint64_t n_blocks,
+                                         hipStream_t stream) {
+  constexpr int M6 = K < 6 ? K : 6;
+  constexpr int M7 = K < 7 ? M6 : 7;
+  if (a.mlen == M7 && M7 != M6)
+    hipLaunchKernelGGL((contigs_probe_quad_kernel<K, M7>), dim3((unsigned)n_blocks), dim3(256),
+                       0, stream, a);
+  else if (a.mlen == M6)
+    hipLaunchKernelGGL((contigs_probe_quad_kernel<K, M6>), dim3((unsigned)n_blocks), dim3(256),
+                       0, stream, a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  // Quad form by default; KMA_CPROBE=lane selects the lane-per-bucket form (A/B).
+  static const bool lane_form = [] {
+    const char* e = getenv("KMA_CPROBE");
+    return e && e[0] == 'l';
+  }();
+  if (lane_form) {
+    hipLaunchKernelGGL(contigs_probe_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+  }
+  switch (a.k) {
+    case 1: return launch_contigs_probe_k<1>(a, n_blocks, stream);
+    case 2: return launch_contigs_probe_k<2>(a, n_blocks, stream);
+    case 3: return launch_contigs_probe_k<3>(a, n_blocks, stream);
+    case 4: return launch_contigs_probe_k<4>(a, n_blocks, stream);
+    case 5: return launch_contigs_probe_k<5>(a, n_blocks, stream);
+    case 6: return launch_contigs_probe_k<6>(a, n_blocks, stream);
+    case 7: return launch_contigs_probe_k<7>(a, n_blocks, stream);
+    case 8: return launch_contigs_probe_k<8>(a, n_blocks, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n, void* temp,
@@ -1400,10 +1569,8 @@ hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t
   return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, counts, prefix, (int)n, stream);
 }
 
-hipError_t launch_contigs(const ContigArgs& a, uint64_t n_blocks, const uint64_t* d_prefix,
-                          uint8_t* out_hits, hipStream_t stream) {
-  hipLaunchKernelGGL(contigs_emit_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a,
-                     d_prefix, reinterpret_cast<kma_hit*>(out_hits));
+hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  hipLaunchKernelGGL(contigs_emit_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

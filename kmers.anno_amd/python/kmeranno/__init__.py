@@ -30,7 +30,7 @@ EXPORTS = (
     "kma_table_device_ptr", "kma_workspace_create", "kma_workspace_reserve",
     "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
-    "kma_contig_window_count",
+    "kma_workspace_reserve_contigs", "kma_annotate_contigs_device", "kma_contig_window_count",
 )
 
 
@@ -92,6 +92,9 @@ def load(path: str | None = None):
                                                    _vp, _vp, _vp, _vp, _u32, _vp]
         L.kma_annotate_contigs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _vp, _u64,
                                            C.POINTER(_u64), _vp, _u32]
+        L.kma_workspace_reserve_contigs.argtypes = [_vp, _u64]
+        L.kma_annotate_contigs_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _vp,
+                                                  _u64, _vp, _vp, _u32, _vp]
         L.kma_contig_window_count.restype = _u64
         L.kma_contig_window_count.argtypes = [_u64p, _u32, _int]
         _lib = L
@@ -211,6 +214,9 @@ class Workspace:
     def reserve(self, n_residues: int):
         _check(load().kma_workspace_reserve(self._h, n_residues))
 
+    def reserve_contigs(self, n_bases: int):
+        _check(load().kma_workspace_reserve_contigs(self._h, n_bases))
+
     def timing(self, enable: bool = True):
         """Per-phase hipEvent timing of the device calls made with this workspace."""
         _check(load().kma_workspace_timing(self._h, int(enable)))
@@ -284,6 +290,15 @@ def annotate_contigs(table: SignatureTable, dna: np.ndarray, offsets: np.ndarray
             continue
         _check(rc)
         return hits[:nh.value], tally
+
+
+def annotate_contigs_device(table: SignatureTable, ws: Workspace, d_dna: int, d_offsets: int,
+                            n_contig: int, n_bases: int, genetic_code: int, d_hits: int, cap: int,
+                            d_n_hits: int, d_tally: int = 0, n_fid: int = 0, stream: int = 0):
+    """Device form of the 6-frame pass (asynchronous on `stream`; *d_n_hits gets the total)."""
+    _check(load().kma_annotate_contigs_device(table._h, ws._h, d_dna, d_offsets, n_contig,
+                                              n_bases, genetic_code, d_hits or None, cap,
+                                              d_n_hits, d_tally or None, n_fid, stream or None))
 
 
 def contig_window_count(offsets: np.ndarray, k: int = 8) -> int:

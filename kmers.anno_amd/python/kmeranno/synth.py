@@ -168,3 +168,113 @@ def random_contigs(total_bp: int, n_contig: int, seed: int, n_rate: float = 0.00
     offsets = np.zeros(n_contig + 1, np.uint64)
     offsets[1:] = np.cumsum(lens)
     return np.concatenate([dna, np.zeros(64, np.uint8)]), offsets
+
+
+# ---- config 3: 6-frame DNA with planted genes -------------------------------------------------
+# NCBI translation table 11 (= 1 for the amino-acid assignment) in TCAG codon order.
+_CODE11 = "FFLLSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG"
+_TCAG = np.frombuffer(b"tcag", np.uint8)
+
+
+def _codon_choices():
+    """aa byte -> array of codons (3 lower-case DNA bytes each) that encode it (code 11)."""
+    out = {}
+    for i, aa in enumerate(_CODE11):
+        codon = _TCAG[[i >> 4, (i >> 2) & 3, i & 3]]
+        out.setdefault(ord(aa), []).append(codon)
+    return {k: np.array(v, np.uint8) for k, v in out.items()}
+
+
+def reverse_translate(rng, prot: np.ndarray) -> np.ndarray:
+    """A random DNA coding sequence (lower case, code 11, ends with a stop codon) for prot."""
+    ch = _codon_choices()
+    cod = np.empty((len(prot) + 1, 3), np.uint8)
+    for aa in np.unique(prot):
+        m = np.flatnonzero(prot == aa)
+        opts = ch[int(aa)]
+        cod[m] = opts[rng.integers(0, len(opts), len(m))]
+    stops = ch[ord("*")]
+    cod[-1] = stops[rng.integers(0, len(stops))]
+    return cod.reshape(-1)
+
+
+def reverse_complement(dna: np.ndarray) -> np.ndarray:
+    comp = np.arange(256, dtype=np.uint8)
+    for a, b in (b"ac", b"ca", b"gt", b"tg", b"AC", b"CA", b"GT", b"TG"):
+        comp[a] = b
+    for a, b in (b"at", b"ta", b"AT", b"TA"):
+        comp[a] = b
+    return comp[dna[::-1]]
+
+
+@dataclass
+class ContigWorkload:
+    keys: np.ndarray       # uint64 [T] packed table kmers
+    fids: np.ndarray       # uint32 [T]
+    n_fid: int
+    dna: np.ndarray        # uint8 lower-case DNA, padded by 64 zero bytes
+    offsets: np.ndarray    # uint64 [n_contig + 1]
+    genes: np.ndarray      # int64 [n_gene, 4]: contig, start (0-based), strand (+1/-1), fid
+
+    @property
+    def n_contig(self) -> int:
+        return len(self.offsets) - 1
+
+
+def make_contig_workload(total_bp: int = 5_000_000, n_contig: int = 20, seed: int = 3,
+                         table_size: int = 10_000_000, n_fid: int = 10_000, k: int = 8,
+                         coding: float = 0.5, mutation: float = 0.10) -> ContigWorkload:
+    """Config 3: random contigs (log-uniform 50 kb..1 Mbp scaled to total_bp,
+    GC 0.5, 0.05% 'n') with genes planted over ~`coding` of the sequence: function prototypes
+    mutated at `mutation` per residue, reverse-translated with random synonymous codons
+    (code 11) and placed on either strand, non-overlapping."""
+    sig = make_table(table_size, n_fid, seed, k)
+    dna, offsets = random_contigs(total_bp, n_contig, seed)
+    rng = np.random.default_rng(seed * 7919 + 3)
+    mean_gene = 3 * 311
+    gap_mean = mean_gene * (1 - coding) / coding
+    genes = []
+    for c in range(n_contig):
+        lo, hi = int(offsets[c]), int(offsets[c + 1])
+        pos = lo + int(rng.exponential(gap_mean))
+        while True:
+            f = int(rng.integers(0, n_fid))
+            cds = reverse_translate(rng, _mutate(rng, sig.protos[f], mutation))
+            if pos + len(cds) > hi:
+                break
+            strand = 1 if rng.random() < 0.5 else -1
+            dna[pos:pos + len(cds)] = cds if strand > 0 else reverse_complement(cds)
+            genes.append((c, pos - lo, strand, f))
+            pos += len(cds) + int(rng.exponential(gap_mean))
+    return ContigWorkload(sig.keys, sig.fids, n_fid, dna, offsets,
+                          np.array(genes, np.int64).reshape(-1, 4))
+
+
+def probed_windows(dna: np.ndarray, offsets: np.ndarray, k: int = 8) -> int:
+    """Windows of the 6-frame extractor that are probed (no stop or X residue, within the end
+    exclusion of KmerReference.java:186-190), code 11."""
+    code = np.frombuffer(_CODE11.encode(), np.uint8)
+    lut = np.full(256, 4, np.uint8)
+    for i, b in enumerate(b"tcag"):
+        lut[b] = i
+        lut[b - 32] = i
+    total = 0
+    for c in range(len(offsets) - 1):
+        s = lut[dna[int(offsets[c]):int(offsets[c + 1])]].astype(np.int64)
+        n = len(s)
+        if n < 3 * k + 3:
+            continue
+        b0, b1, b2 = s[:-2], s[1:-1], s[2:]
+        bad_amb = (b0 | b1 | b2) >= 4
+        idx_p = np.where(bad_amb, 0, b0 * 16 + b1 * 4 + b2)
+        idx_m = np.where(bad_amb, 0, (b2 ^ 2) * 16 + (b1 ^ 2) * 4 + (b0 ^ 2))
+        bad_p = bad_amb | (code[idx_p] == ord("*"))
+        bad_m = bad_amb | (code[idx_m] == ord("*"))
+        m = len(bad_p)  # codon starts 0 .. n-3
+        for bad, lo, hi in ((bad_p, 0, n - 3 * k - 3), (bad_m, 3, n - 3 * k)):
+            w = np.zeros(m - 3 * (k - 1), bool)
+            for j in range(k):
+                w |= bad[3 * j:3 * j + len(w)]
+            x = np.arange(len(w))
+            total += int((~w & (x >= lo) & (x <= hi)).sum())
+    return total

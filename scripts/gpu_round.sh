@@ -18,11 +18,15 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -x -q -m gpu ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ${BENCH_ARGS:-} ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
             -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench3) run bench_c3 900 python bench.py --steps 20 --warmup 3 --workload c3 ;;
+    prof3) run prof_c3 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof3 -o run \
+            -- python3 bench.py --steps 10 --warmup 2 --workload c3 --no-cpu-baseline ;;
+    bench4) run bench_c4 900 python bench.py --steps 10 --warmup 2 --workload c4 --no-cpu-baseline ;;
     bench5) run bench_c5 900 python bench.py --steps 10 --warmup 2 --workload c5 --no-cpu-baseline ;;
     lf) for lf in 0.25 0.35 0.5; do
           run prof_c5_lf$lf 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5_lf$lf -o run \

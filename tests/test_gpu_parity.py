@@ -252,3 +252,51 @@ def test_workspace_phase_timing(kma):
                                          0, *[o.data_ptr() for o in outs], 0, 0, stream)
         assert e.value.code == kma.E_CAPACITY
         ws.close()
+
+
+def test_contigs_device_api_planted_genome(kma, oracle_c):
+    """kma_annotate_contigs_device on torch buffers over a synthetic config-3 genome (planted
+    genes on both strands, 'n' bases, offsets[0] != 0): hits equal the oracle's in canonical
+    order, the total is published even when it exceeds cap (hits past cap dropped), and the
+    tally is accumulated into."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_contig_workload(300_000, 6, 33, table_size=200_000, n_fid=500)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    e = oracle_c.annotate_contigs(oracle_c.Table(kmers, wl.fids.astype(np.int32)), wl.dna,
+                                  wl.offsets, 11, K)
+    assert len(e[0]) > 1000
+    dev = torch.device("cuda", 0)
+    # shift the genome by 5 bytes so that d_offsets[0] != 0
+    dna = np.concatenate([np.frombuffer(b"ggggg", np.uint8), wl.dna])
+    off = wl.offsets + np.uint64(5)
+    n_bases = int(off[-1] - off[0])
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        ws = kma.Workspace(0)
+        ws.reserve_contigs(n_bases)
+        d_dna = torch.from_numpy(dna).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        stream = torch.cuda.current_stream().cuda_stream
+        tally = torch.zeros(wl.n_contig * 500, dtype=torch.int32, device=dev)
+        d_nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        for cap in (len(e[0]) + 7, 100):
+            d_hits = torch.zeros(cap * kma.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), wl.n_contig,
+                                        n_bases, 11, d_hits.data_ptr(), cap, d_nh.data_ptr(),
+                                        tally.data_ptr(), 500, stream)
+            torch.cuda.synchronize()
+            assert int(d_nh.item()) == len(e[0])
+            hits = d_hits.cpu().numpy().view(kma.HIT_DTYPE)[:min(cap, len(e[0]))]
+            n = len(hits)
+            for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"],
+                             hits["fid"]), e):
+                assert (a == b[:n]).all()
+        expect = np.zeros((wl.n_contig, 500), np.int64)
+        np.add.at(expect, (e[0], e[4]), 2)  # two calls accumulated
+        assert (tally.cpu().numpy().reshape(wl.n_contig, 500) == expect).all()
+        with pytest.raises(kma.KmerAnnoError) as err:  # reservation too small
+            kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), wl.n_contig,
+                                        n_bases + 10**6, 11, 0, 0, d_nh.data_ptr(),
+                                        0, 0, stream)
+        assert err.value.code == kma.E_CAPACITY
+        ws.close()
