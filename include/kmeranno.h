@@ -213,6 +213,26 @@ int kma_annotate_contigs_device(const kma_table* table, kma_workspace* ws, const
                                 int genetic_code, kma_hit* d_hits, uint64_t cap,
                                 uint64_t* d_n_hits, uint32_t* d_tally, uint32_t n_fid,
                                 void* stream);
+/* ---- peg-kmer join of the projector (KmerProcessor.java:195-207) -----------------------------
+ * kma_peg_table_create: the singleton peg kmers of a close genome as a table whose fid is the
+ * peg index: every window i < L-K of every peg without 'X' (KmerReference.countPegKmers,
+ * KmerReference.java:124-147), counted by kmer over the whole batch; kmers seen exactly once
+ * (CountMap.getSingletons via getPegKmers, KmerProcessor.java:320-327) map to their peg.
+ * Built on the device (window packing, radix sort, singleton select, table build). Windows with
+ * bytes outside A-Z / '*' never equal a translated contig kmer and are left out.
+ * *n_windows (optional) receives the number of counted windows; table info n_entries the
+ * singletons. n_peg < 2^23.
+ * kma_connect_pegs: every location of a singleton in the new genome's 6-frame contig kmer map
+ * connected to its peg (framer.connect(pegId, loc)), i.e. hits with fid = peg index in the
+ * canonical order of kma_annotate_contigs. strict != 0 applies KmerFactory.Strict
+ * (KmerFactory.java:61-69): kmers with more than one location in the genome are dropped.
+ * Capacity handling as kma_annotate_contigs.                                                 */
+int kma_peg_table_create(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg, int k,
+                         int device, double load_factor, kma_table** out, uint64_t* n_windows);
+int kma_connect_pegs(const kma_table* peg_table, const uint8_t* dna, const uint64_t* offsets,
+                     uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
+                     uint64_t cap, uint64_t* n_hits);
+
 /* Window count of the 6-frame extractor before the '*'/'X' filter (for throughput metrics).  */
 uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k);
 

@@ -249,32 +249,18 @@ int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, uint32_t* d_wi
   return KMA_OK;
 }
 
-// Shared by both create forms: keys packed on the host with `lut`.
-int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, uint64_t n, int k,
-                     int device, double lf, const uint8_t lut[256], uint64_t n_skipped,
-                     kma_table** out) {
-  if (lf <= 0) lf = 0.5;
-  if (lf > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", lf);
-  for (uint64_t r = 0; r < n; ++r)
-    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^23-1",
-                                            fids[r], (unsigned long long)r);
+// Table from device-resident keys/fids (n rows; fids already checked against KMA_MAX_FID).
+int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, int k,
+                            int device, double lf, const uint8_t lut[256], kma_table** out) {
   const uint64_t nb = kma_table_buckets_for(n, lf);
   if (nb > kMaxBuckets)
     return fail(KMA_E_INVALID, "table too large: %llu buckets", (unsigned long long)nb);
-  DeviceScope ds(device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
-                                        hipGetErrorString(ds.err));
   DevBufs tmp;
-  uint64_t* d_keys;
-  uint32_t *d_fids, *d_winner, *d_status;
-  KMA_HIP(tmp.alloc(&d_keys, n * 8));
-  KMA_HIP(tmp.alloc(&d_fids, n * 4));
+  uint32_t *d_winner, *d_status;
   KMA_HIP(tmp.alloc(&d_winner, nb * kma::kSlotsPerBucket * 4));
   KMA_HIP(tmp.alloc(&d_status, 16));
   uint64_t* d_slots = nullptr;
   KMA_HIP(hipMalloc(&d_slots, nb * 64));
-  KMA_HIP(hipMemcpy(d_keys, keys.data(), n * 8, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemcpy(d_fids, fids, n * 4, hipMemcpyHostToDevice));
   int rc = build_on_device(d_slots, nb, k, d_winner, d_keys, d_fids, n, d_status, nullptr);
   uint32_t st[4] = {};
   if (rc == KMA_OK) {
@@ -288,13 +274,37 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
     return rc;
   }
   (*out)->info.n_rows = n;
-  (*out)->info.n_skipped = n_skipped;
   (*out)->info.n_entries = st[1];
   (*out)->info.max_probe = st[2];
   int ne = 0;
   for (int c = 0; c < 256; ++c)
     if (lut[c] >= 28) (*out)->info.extra_syms[lut[c] - 28] = (uint8_t)c, ++ne;
   (*out)->info.n_extra_syms = ne;
+  return KMA_OK;
+}
+
+// Shared by both create forms: keys packed on the host with `lut`.
+int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, uint64_t n, int k,
+                     int device, double lf, const uint8_t lut[256], uint64_t n_skipped,
+                     kma_table** out) {
+  if (lf <= 0) lf = 0.5;
+  if (lf > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", lf);
+  for (uint64_t r = 0; r < n; ++r)
+    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^23-1",
+                                            fids[r], (unsigned long long)r);
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  DevBufs tmp;
+  uint64_t* d_keys;
+  uint32_t* d_fids;
+  KMA_HIP(tmp.alloc(&d_keys, n * 8));
+  KMA_HIP(tmp.alloc(&d_fids, n * 4));
+  KMA_HIP(hipMemcpy(d_keys, keys.data(), n * 8, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_fids, fids, n * 4, hipMemcpyHostToDevice));
+  const int rc = create_from_device_keys(d_keys, d_fids, n, k, device, lf, lut, out);
+  if (rc != KMA_OK) return rc;
+  (*out)->info.n_skipped = n_skipped;
   return KMA_OK;
 }
 
@@ -849,6 +859,138 @@ int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t*
     return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
                 (unsigned long long)(out_hits ? cap : 0));
   if (tb) KMA_HIP(hipMemcpy(out_tally, d_tally, tb, hipMemcpyDeviceToHost));
+  if (nh == 0) return KMA_OK;
+  KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
+  rc = enqueue_contig_emit(a, d_out, nh, d_n, nullptr);
+  if (rc != KMA_OK) return rc;
+  KMA_HIP(hipMemcpy(out_hits, d_out, nh * sizeof(kma_hit), hipMemcpyDeviceToHost));
+  return KMA_OK;
+}
+
+int kma_peg_table_create(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg, int k,
+                         int device, double load_factor, kma_table** out,
+                         uint64_t* n_windows) {
+  if (!out) return fail(KMA_E_INVALID, "null argument");
+  *out = nullptr;
+  if (int rc = check_k(k)) return rc;
+  if (load_factor <= 0) load_factor = 0.5;
+  if (load_factor > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", load_factor);
+  if (n_peg > KMA_MAX_FID + 1u) return fail(KMA_E_INVALID, "more than 2^23 pegs");
+  if (n_peg && (!residues || !offsets)) return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t s = 0; s < n_peg; ++s)
+    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
+  const uint64_t base = n_peg ? offsets[0] : 0, total = n_peg ? offsets[n_peg] - base : 0;
+  uint8_t lut[256];
+  standard_lut(lut);
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  DevBufs b;
+  uint8_t *d_res, *d_lut, *d_flags;
+  uint64_t *d_off, *d_keys, *d_keys2, *d_n;
+  uint32_t *d_pegs, *d_pegs2;
+  const uint64_t nw = std::max<uint64_t>(total, 1);
+  KMA_HIP(b.alloc(&d_res, total + 64));
+  KMA_HIP(b.alloc(&d_off, (n_peg + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_lut, 256));
+  KMA_HIP(b.alloc(&d_keys, nw * 8));
+  KMA_HIP(b.alloc(&d_keys2, nw * 8));
+  KMA_HIP(b.alloc(&d_pegs, nw * 4));
+  KMA_HIP(b.alloc(&d_pegs2, nw * 4));
+  KMA_HIP(b.alloc(&d_flags, nw));
+  KMA_HIP(b.alloc(&d_n, 8));
+  KMA_HIP(hipMemset(d_n, 0, 8));
+  uint64_t n_sel = 0, windows = 0;
+  if (total) {
+    std::vector<uint64_t> rel(offsets, offsets + n_peg + 1);
+    for (auto& o : rel) o -= base;
+    for (uint32_t s = 0; s < n_peg; ++s) {
+      const uint64_t L = rel[s + 1] - rel[s];
+      if (L > (uint64_t)k) windows += L - k;
+    }
+    KMA_HIP(hipMemcpy(d_res, residues + base, total, hipMemcpyHostToDevice));
+    KMA_HIP(hipMemset(d_res + total, 0, 64));
+    KMA_HIP(hipMemcpy(d_off, rel.data(), (n_peg + 1) * 8ull, hipMemcpyHostToDevice));
+    KMA_HIP(hipMemcpy(d_lut, lut, 256, hipMemcpyHostToDevice));
+    KMA_HIP(kma::launch_peg_windows(d_res, d_off, n_peg, k, d_lut, d_keys, d_pegs, nullptr));
+    size_t t1 = 0, t2 = 0;
+    KMA_HIP(kma::launch_sort_pairs(nullptr, &t1, d_keys, d_keys2, d_pegs, d_pegs2, total, 5 * k,
+                                   nullptr));
+    KMA_HIP(kma::launch_select_flagged(nullptr, &t2, d_keys2, d_pegs2, d_flags, d_keys, d_pegs,
+                                       d_n, total, nullptr));
+    void* d_temp;
+    size_t tb = std::max(t1, t2);
+    KMA_HIP(b.alloc(&d_temp, tb));
+    KMA_HIP(kma::launch_sort_pairs(d_temp, &tb, d_keys, d_keys2, d_pegs, d_pegs2, total, 5 * k,
+                                   nullptr));
+    KMA_HIP(kma::launch_singleton_flags(d_keys2, total, d_flags, nullptr));
+    tb = std::max(t1, t2);
+    KMA_HIP(kma::launch_select_flagged(d_temp, &tb, d_keys2, d_pegs2, d_flags, d_keys, d_pegs,
+                                       d_n, total, nullptr));
+    KMA_HIP(hipMemcpy(&n_sel, d_n, 8, hipMemcpyDeviceToHost));
+  }
+  if (n_windows) *n_windows = windows;
+  const int rc = create_from_device_keys(d_keys, d_pegs, n_sel, k, device, load_factor, lut, out);
+  if (rc != KMA_OK) return rc;
+  (*out)->info.n_rows = windows;
+  return KMA_OK;
+}
+
+int kma_connect_pegs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
+                     uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
+                     uint64_t cap, uint64_t* n_hits) {
+  if (!strict)
+    return kma_annotate_contigs(t, dna, offsets, n_contig, genetic_code, out_hits, cap, n_hits,
+                                nullptr, 0);
+  if (!t || !n_hits) return fail(KMA_E_INVALID, "null argument");
+  const char* code = ncbi_code(genetic_code);
+  if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
+  *n_hits = 0;
+  if (n_contig == 0) return KMA_OK;
+  if (!dna || !offsets) return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t c = 0; c < n_contig; ++c)
+    if (offsets[c + 1] < offsets[c]) return fail(KMA_E_INVALID, "offsets decrease at %u", c);
+  const uint64_t base = offsets[0], total = offsets[n_contig] - base;
+  if (total >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
+  if (total == 0) return KMA_OK;
+  std::vector<uint64_t> rel(offsets, offsets + n_contig + 1);
+  for (auto& o : rel) o -= base;
+  DeviceScope ds(t->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  kma_workspace* ws = nullptr;
+  int rc = kma_workspace_create(t->device, &ws);
+  if (rc != KMA_OK) return rc;
+  std::unique_ptr<kma_workspace, int (*)(kma_workspace*)> ws_guard(ws, kma_workspace_destroy);
+  rc = kma_workspace_reserve_contigs(ws, total);
+  if (rc != KMA_OK) return rc;
+  DevBufs b;
+  uint8_t* d_dna;
+  uint64_t *d_off, *d_n;
+  uint32_t* d_count;
+  kma_hit* d_out = nullptr;
+  const uint64_t n_slots = t->n_buckets * kma::kSlotsPerBucket;
+  KMA_HIP(b.alloc(&d_dna, total + 64));
+  KMA_HIP(b.alloc(&d_off, (n_contig + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_n, 8));
+  KMA_HIP(b.alloc(&d_count, n_slots * 4));
+  KMA_HIP(hipMemcpy(d_dna, dna + base, total, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_dna + total, 0, 64));
+  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_contig + 1) * 8ull, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_count, 0, n_slots * 4));
+  kma::ContigArgs a = contig_args(t, ws, d_dna, d_off, n_contig, total, code, nullptr, 0);
+  a.slot_count = d_count;
+  a.strict_pass = 1;  // count every table key's locations
+  KMA_HIP(kma::launch_contigs_probe(a, contig_blocks(total), nullptr));
+  a.strict_pass = 2;  // keep keys with exactly one location
+  rc = enqueue_contigs(ws, a, nullptr);
+  if (rc == KMA_OK) rc = enqueue_contig_emit(a, nullptr, 0, d_n, nullptr);
+  if (rc != KMA_OK) return rc;
+  uint64_t nh = 0;
+  KMA_HIP(hipMemcpy(&nh, d_n, 8, hipMemcpyDeviceToHost));
+  *n_hits = nh;
+  if (nh > cap || (nh && !out_hits))
+    return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
+                (unsigned long long)(out_hits ? cap : 0));
   if (nh == 0) return KMA_OK;
   KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
   rc = enqueue_contig_emit(a, d_out, nh, d_n, nullptr);

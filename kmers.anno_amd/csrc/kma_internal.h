@@ -192,6 +192,11 @@ struct ContigArgs {
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order
   uint64_t cap;
   uint64_t* n_hits;            // emit pass: total hits (also when > cap)
+  // KmerFactory.Strict (peg join): pass 1 counts the locations of every table key
+  // (strict_pass = 1: atomicAdd per hit into slot_count[slot id], nothing else is meaningful),
+  // pass 2 keeps only hits whose key has exactly one location (strict_pass = 2).
+  uint32_t* slot_count;        // n_buckets * 8, zeroed before pass 1
+  int32_t strict_pass;         // 0 = off
   uint8_t codon_codes[64];     // by value (TCAG order): 5-bit aa code, 0 = stop
 };
 constexpr int kContigTile = 256;  // forward positions per block
@@ -210,5 +215,20 @@ hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
                               void* temp, size_t* temp_bytes, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
+// Peg-kmer singleton table (KmerReference.countPegKmers + CountMap.getSingletons): every
+// window i < L-K without 'X' of every peg -> (key or 0, peg index) per residue position; sort;
+// keep keys that occur exactly once.
+hipError_t launch_peg_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg,
+                              int k, const uint8_t* lut, uint64_t* keys, uint32_t* pegs,
+                              hipStream_t stream);
+hipError_t launch_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
+                             uint64_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
+                             uint64_t n, int key_bits, hipStream_t stream);
+hipError_t launch_singleton_flags(const uint64_t* sorted_keys, uint64_t n, uint8_t* flags,
+                                  hipStream_t stream);
+hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
+                                 const uint32_t* vals_in, const uint8_t* flags, uint64_t* keys_out,
+                                 uint32_t* vals_out, uint64_t* n_out, uint64_t n,
+                                 hipStream_t stream);
 
 }  // namespace kma

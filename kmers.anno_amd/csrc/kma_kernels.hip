@@ -16,13 +16,12 @@
 // buckets, not MFMA.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
-
-#include <cstdio>
-#include <cstdlib>
 
 namespace kma {
 namespace {
@@ -1321,15 +1320,22 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     }
   }
   bool hit[2];
-  uint32_t fid[2];
+  uint32_t fid[2], sid[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const uint32_t w = bk[j] != kNone ? word[j] : 0u;
     hit[j] = (w & kWordFid) != 0u;
     fid[j] = (w & kWordFid) - 1u;
-    if (w == 0x80000000u) {  // rare: the home bucket missed with the key's overflow bit set
-      uint32_t sid;
-      hit[j] = walk_chain(a.slots, nb, bk[j], key[j], fid[j], sid);
+    sid[j] = bk[j] * kSlotsPerBucket + ((w >> kSlotShift) & 7u);
+    if (w == 0x80000000u)  // rare: the home bucket missed with the key's overflow bit set
+      hit[j] = walk_chain(a.slots, nb, bk[j], key[j], fid[j], sid[j]);
+  }
+  if (a.strict_pass) {  // KmerFactory.Strict: a key's locations counted by its slot id
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (!hit[j]) continue;
+      if (a.strict_pass == 1) atomicAdd(a.slot_count + sid[j], 1u);
+      else hit[j] = a.slot_count[sid[j]] == 1u;
     }
   }
   if (a.tally) {
@@ -1349,6 +1355,53 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   if (hit[0]) st[o++] = (r << 25) | fid[0];               // strand bit 24 = 0: '+'
   if (hit[1]) st[o] = (r << 25) | (1ull << 24) | fid[1];  // '-'
   if (t == 0) a.block_counts[blockIdx.x] = total;
+}
+
+// Peg windows (KmerReference.countPegKmers, KmerReference.java:124-147): one wave per peg;
+// position i of peg s gets the packed key of window [i, i + K) if i < L - K (end exclusive)
+// and the window has no 'X' and only standard symbols (others can never equal a translated
+// contig kmer), else 0; every position of the batch is written.
+__global__ __launch_bounds__(256) void peg_windows_kernel(const uint8_t* __restrict__ residues,
+                                                          const uint64_t* __restrict__ offsets,
+                                                          uint32_t n_peg, int k,
+                                                          const uint8_t* __restrict__ lut_g,
+                                                          uint64_t* __restrict__ keys,
+                                                          uint32_t* __restrict__ pegs) {
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = threadIdx.x == 'X' ? 0 : lut_g[threadIdx.x];  // 'X' windows are skipped
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t o0 = offsets[0];
+  for (uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < n_peg;
+       s += (uint64_t)gridDim.x * 4) {
+    const uint64_t lo = offsets[s], hi = offsets[s + 1];
+    const int64_t end = (int64_t)(hi - lo) - k;  // windows i < end
+    for (uint64_t p = lo + lane; p < hi; p += 64) {
+      const int64_t i = (int64_t)(p - lo);
+      uint64_t key = 0;
+      if (i < end) {
+        bool ok = true;
+        for (int j = 0; j < k; ++j) {
+          const uint32_t c = lut[residues[p + j]];
+          ok = ok && c != 0u;
+          key = (key << 5) | c;
+        }
+        key = ok ? key : 0;
+      }
+      keys[p - o0] = key;
+      pegs[p - o0] = (uint32_t)s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void singleton_flags_kernel(const uint64_t* __restrict__ k,
+                                                              uint64_t n,
+                                                              uint8_t* __restrict__ flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256) {
+    const uint64_t v = k[i];
+    flags[i] = v != 0 && (i == 0 || k[i - 1] != v) && (i + 1 == n || k[i + 1] != v);
+  }
 }
 
 // Emit pass: block b's staged hits go to out[prefix[b] ..], those past `cap` are dropped; the
@@ -1547,7 +1600,7 @@ hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStrea
     const char* e = getenv("KMA_CPROBE");
     return e && e[0] == 'l';
   }();
-  if (lane_form) {
+  if (lane_form && !a.strict_pass) {
     hipLaunchKernelGGL(contigs_probe_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
   }
@@ -1567,6 +1620,54 @@ hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStrea
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n, void* temp,
                               size_t* temp_bytes, hipStream_t stream) {
   return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, counts, prefix, (int)n, stream);
+}
+
+hipError_t launch_peg_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg,
+                              int k, const uint8_t* lut, uint64_t* keys, uint32_t* pegs,
+                              hipStream_t stream) {
+  const unsigned g = (unsigned)std::min<uint64_t>(8192, ((uint64_t)n_peg + 3) / 4);
+  hipLaunchKernelGGL(peg_windows_kernel, dim3(g ? g : 1), dim3(256), 0, stream, residues,
+                     offsets, n_peg, k, lut, keys, pegs);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
+                             uint64_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
+                             uint64_t n, int key_bits, hipStream_t stream) {
+  return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_in, keys_out, vals_in,
+                                            vals_out, (int)n, 0, key_bits, stream);
+}
+
+hipError_t launch_singleton_flags(const uint64_t* sorted_keys, uint64_t n, uint8_t* flags,
+                                  hipStream_t stream) {
+  hipLaunchKernelGGL(singleton_flags_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                     sorted_keys, n, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
+                                 const uint32_t* vals_in, const uint8_t* flags, uint64_t* keys_out,
+                                 uint32_t* vals_out, uint64_t* n_out, uint64_t n,
+                                 hipStream_t stream) {
+  // Keys and values in one pass: select over an index-free zip is not needed, two passes over
+  // the same flags keep the order identical.
+  size_t need = 0;
+  hipError_t e = hipcub::DeviceSelect::Flagged(nullptr, need, keys_in, flags, keys_out, n_out,
+                                               (int)n, stream);
+  if (e != hipSuccess) return e;
+  size_t need2 = 0;
+  e = hipcub::DeviceSelect::Flagged(nullptr, need2, vals_in, flags, vals_out, n_out, (int)n,
+                                    stream);
+  if (e != hipSuccess) return e;
+  need = std::max(need, need2);
+  if (!temp) {
+    *temp_bytes = need;
+    return hipSuccess;
+  }
+  e = hipcub::DeviceSelect::Flagged(temp, need, keys_in, flags, keys_out, n_out, (int)n, stream);
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceSelect::Flagged(temp, need, vals_in, flags, vals_out, n_out, (int)n,
+                                       stream);
 }
 
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {

@@ -31,6 +31,7 @@ EXPORTS = (
     "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_workspace_reserve_contigs", "kma_annotate_contigs_device", "kma_contig_window_count",
+    "kma_peg_table_create", "kma_connect_pegs",
 )
 
 
@@ -95,6 +96,10 @@ def load(path: str | None = None):
         L.kma_workspace_reserve_contigs.argtypes = [_vp, _u64]
         L.kma_annotate_contigs_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _vp,
                                                   _u64, _vp, _vp, _u32, _vp]
+        L.kma_peg_table_create.argtypes = [_u8p, _u64p, _u32, _int, _int, C.c_double,
+                                           C.POINTER(_vp), C.POINTER(_u64)]
+        L.kma_connect_pegs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _int, _vp, _u64,
+                                       C.POINTER(_u64)]
         L.kma_contig_window_count.restype = _u64
         L.kma_contig_window_count.argtypes = [_u64p, _u32, _int]
         _lib = L
@@ -162,6 +167,17 @@ class SignatureTable:
         _check(load().kma_table_create_packed(keys, np.ascontiguousarray(fids, np.uint32),
                                               len(keys), k, device, load_factor, C.byref(h)))
         return cls(h)
+
+    @classmethod
+    def from_pegs(cls, residues, offsets, k: int = 8, device: int = 0, load_factor: float = 0.5):
+        """Singleton peg-kmer table of a close genome (fid = peg index); see kma_peg_table_create.
+        Returns (table, counted windows)."""
+        residues = np.ascontiguousarray(residues, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        h, nw = _vp(), _u64()
+        _check(load().kma_peg_table_create(residues, offsets, len(offsets) - 1, k, device,
+                                           load_factor, C.byref(h), C.byref(nw)))
+        return cls(h), nw.value
 
     @classmethod
     def wrap_device(cls, d_slots: int, n_buckets: int, k: int = 8, device: int = 0):
@@ -299,6 +315,25 @@ def annotate_contigs_device(table: SignatureTable, ws: Workspace, d_dna: int, d_
     _check(load().kma_annotate_contigs_device(table._h, ws._h, d_dna, d_offsets, n_contig,
                                               n_bases, genetic_code, d_hits or None, cap,
                                               d_n_hits, d_tally or None, n_fid, stream or None))
+
+
+def connect_pegs(peg_table: SignatureTable, dna: np.ndarray, offsets: np.ndarray,
+                 genetic_code: int = 11, strict: bool = False):
+    """KmerProcessor.java:195-207: (hits with fid = peg index) in canonical order."""
+    dna = np.ascontiguousarray(dna, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n_contig = len(offsets) - 1
+    cap = 1024
+    while True:
+        hits = np.empty(cap, HIT_DTYPE)
+        nh = _u64()
+        rc = load().kma_connect_pegs(peg_table._h, dna, offsets, n_contig, genetic_code,
+                                     int(strict), hits.ctypes.data, cap, C.byref(nh))
+        if rc == E_CAPACITY:
+            cap = nh.value
+            continue
+        _check(rc)
+        return hits[:nh.value]
 
 
 def contig_window_count(offsets: np.ndarray, k: int = 8) -> int:

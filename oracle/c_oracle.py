@@ -53,6 +53,10 @@ def lib():
         L.orc_peg_kmers.restype = C.c_uint64
         L.orc_peg_kmers.argtypes = [_u8p, _u64p, C.c_uint32, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_uint64]
+        L.orc_peg_connect.restype = C.c_uint64
+        L.orc_peg_connect.argtypes = [_u8p, _u64p, C.c_uint32, _u8p, _u64p, C.c_uint32, C.c_int,
+                                      C.c_int, C.c_int, _u32p, _i32p, _u8p, _u8p, _u32p,
+                                      C.c_uint64]
         _lib = L
     return _lib
 
@@ -141,3 +145,15 @@ def peg_kmers(residues: np.ndarray, offsets: np.ndarray, k: int = 8):
     lib().orc_peg_kmers(residues, offsets, n_seq, k, km.ctypes.data, pg.ctypes.data,
                         lf.ctypes.data, n)
     return km, pg, lf
+
+
+def peg_connect(residues, offsets, dna, doffsets, gcode: int = 11, k: int = 8, strict=False):
+    """Connections (contig, left, strand, frame, peg) of KmerProcessor.java:195-207, sorted."""
+    args = (residues, offsets, len(offsets) - 1, dna, doffsets, len(doffsets) - 1, gcode, k,
+            int(strict))
+    z32, zi, z8 = np.empty(1, np.uint32), np.empty(1, np.int32), np.empty(1, np.uint8)
+    n = lib().orc_peg_connect(*args, z32, zi, z8, z8, z32, 0)
+    ct, lf = np.empty(n, np.uint32), np.empty(n, np.int32)
+    sd, fr, pg = np.empty(n, np.uint8), np.empty(n, np.uint8), np.empty(n, np.uint32)
+    lib().orc_peg_connect(*args, ct, lf, sd, fr, pg, n)
+    return ct, lf, sd, fr, pg

@@ -398,3 +398,70 @@ uint64_t orc_peg_kmers(const uint8_t* residues, const uint64_t* offsets, uint32_
   }
   return n;
 }
+
+/* The peg-kmer join of the projector, KmerProcessor.java:195-207 with getPegKmers (:320-327),
+ * KmerReference.countPegKmers (:124-147) and KmerFactory.findKmers (KmerFactory.java:61-82):
+ *   1. count every peg window (i < L-K, no 'X') of the close genome by kmer text; keep the
+ *      kmers seen exactly once (CountMap.getSingletons) with the peg they came from;
+ *   2. the new genome's contig kmer map (getContigKmers); STRICT (strict != 0) drops kmers with
+ *      more than one location;
+ *   3. for every singleton peg kmer, every location of it in the map is connected to its peg
+ *      (framer.connect(pegId, loc)).
+ * The HashSet/HashMap iteration order of the Java loop carries no meaning (the framer sorts),
+ * so the connections are returned as (contig, left, strand, frame, peg) sorted canonically,
+ * like orc_annotate_contigs. Returns the number of connections. */
+uint64_t orc_peg_connect(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg,
+                         const uint8_t* dna, const uint64_t* doffsets, uint32_t n_contig,
+                         int gcode, int K, int strict, uint32_t* out_contig, int32_t* out_left,
+                         uint8_t* out_strand, uint8_t* out_frame, uint32_t* out_peg,
+                         uint64_t cap) {
+  const uint64_t np = orc_peg_kmers(residues, offsets, n_peg, K, 0, 0, 0, 0);
+  char* pk = (char*)malloc(np * (uint64_t)K + 1);
+  uint32_t* pp = (uint32_t*)malloc(sizeof(uint32_t) * (np + 1));
+  int32_t* pl = (int32_t*)malloc(sizeof(int32_t) * (np + 1));
+  orc_peg_kmers(residues, offsets, n_peg, K, pk, pp, pl, np);
+  /* CountMap: value = the peg of the first occurrence, -2 once seen again */
+  orc_table* pegs = orc_table_new(0, 0, 0, 0);
+  for (uint64_t r = 0; r < np; r++) {
+    const int32_t v = orc_table_get(pegs, pk + r * K, K);
+    orc_table_put(pegs, pk + r * K, K, v == -1 ? (int32_t)pp[r] : -2);
+  }
+  const uint64_t nc = orc_contig_kmers(dna, doffsets, n_contig, gcode, K, 0, 0, 0, 0, 0, 0);
+  if (nc == (uint64_t)-1) {
+    orc_table_free(pegs);
+    free(pk), free(pp), free(pl);
+    return nc;
+  }
+  char* ck = (char*)malloc(nc * (uint64_t)K + 1);
+  uint32_t* ct = (uint32_t*)malloc(sizeof(uint32_t) * (nc + 1));
+  int32_t* lf = (int32_t*)malloc(sizeof(int32_t) * (nc + 1));
+  uint8_t* st = (uint8_t*)malloc(nc + 1);
+  uint8_t* fr = (uint8_t*)malloc(nc + 1);
+  orc_contig_kmers(dna, doffsets, n_contig, gcode, K, ck, ct, lf, st, fr, nc);
+  orc_table* locs = orc_table_new(0, 0, 0, 0); /* kmer -> number of locations (STRICT) */
+  if (strict)
+    for (uint64_t r = 0; r < nc; r++) {
+      const int32_t v = orc_table_get(locs, ck + r * K, K);
+      orc_table_put(locs, ck + r * K, K, v < 0 ? 1 : v + 1);
+    }
+  orc_hit* hits = (orc_hit*)malloc(sizeof(orc_hit) * (nc + 1));
+  uint64_t nh = 0;
+  for (uint64_t r = 0; r < nc; r++) {
+    const int32_t v = orc_table_get(pegs, ck + r * K, K);
+    if (v < 0) continue; /* not a peg kmer, or not a singleton */
+    if (strict && orc_table_get(locs, ck + r * K, K) > 1) continue;
+    orc_hit h = {ct[r], lf[r], (uint32_t)v, st[r], fr[r]};
+    hits[nh++] = h;
+  }
+  qsort(hits, nh, sizeof(orc_hit), hit_cmp);
+  for (uint64_t i = 0; i < nh && i < cap; i++) {
+    out_contig[i] = hits[i].contig;
+    out_left[i] = hits[i].left;
+    out_strand[i] = hits[i].strand;
+    out_frame[i] = hits[i].frame;
+    out_peg[i] = hits[i].fid;
+  }
+  orc_table_free(pegs), orc_table_free(locs);
+  free(pk), free(pp), free(pl), free(ck), free(ct), free(lf), free(st), free(fr), free(hits);
+  return nh;
+}

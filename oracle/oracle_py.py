@@ -119,3 +119,24 @@ def peg_kmers(prots, k: int = 8):
             km = p[i:i + k]
             if "X" not in km:
                 yield km, pi, i + 1
+
+
+def peg_connect(prots, contigs, gcode: int = 11, k: int = 8, strict: bool = False):
+    """KmerProcessor.java:195-207: singleton peg kmers (CountMap.getSingletons of
+    countPegKmers) joined with the contig kmer map (KmerFactory STRICT drops kmers with more
+    than one location); every location of a singleton is connected to its peg. Returns
+    (contig, left, strand, frame, peg) sorted (contig, left, '+' first)."""
+    count, first = {}, {}
+    for km, pi, _ in peg_kmers(prots, k):
+        count[km] = count.get(km, 0) + 1
+        first.setdefault(km, pi)
+    singles = {km: first[km] for km, c in count.items() if c == 1}
+    locs = {}
+    for km, ci, left, strand, frame in contig_kmers(contigs, gcode, k):
+        locs.setdefault(km, []).append((ci, left, strand, frame))
+    if strict:
+        locs = {km: v for km, v in locs.items() if len(v) == 1}
+    out = [(ci, left, strand, frame, singles[km])
+           for km, v in locs.items() if km in singles for ci, left, strand, frame in v]
+    out.sort(key=lambda h: (h[0], h[1], h[2]))
+    return out

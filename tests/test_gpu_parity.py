@@ -300,3 +300,35 @@ def test_contigs_device_api_planted_genome(kma, oracle_c):
                                         0, 0, stream)
         assert err.value.code == kma.E_CAPACITY
         ws.close()
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_peg_connect_small_gto_vs_oracle(kma, oracle_c, small_gto, strict):
+    """A9, KmerProcessor.java:195-207: singleton peg kmers of a close genome (small.gto's pegs,
+    mutated 5%, plus exact copies of five pegs so that their kmers are no longer singletons,
+    and an 'X' run) joined with the 6-frame kmer map of small.gto's contigs, AGGRESSIVE and
+    STRICT: every (contig, left, strand, frame, peg) connection equals the oracle's."""
+    rng = np.random.default_rng(9)
+    prots = [f["protein_translation"] for f in small_gto["features"]
+             if f.get("protein_translation")]
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    close = []
+    for p in prots:
+        b = np.frombuffer(p.encode(), np.uint8).copy()
+        m = rng.random(len(b)) < 0.05
+        b[m] = aa[rng.integers(0, 20, int(m.sum()))]
+        close.append(b.tobytes().decode())
+    close[3] = close[3][:40] + "XXX" + close[3][40:]
+    close += prots[:5] + ["", "ACDEFGH", "ACDEFGHIK"]
+    res, off = oracle_c.pack_strings(close)
+    contigs = [c["dna"] for c in small_gto["contigs"]]
+    dna, doff = oracle_c.pack_strings(contigs)
+    e = oracle_c.peg_connect(res, off, dna, doff, 11, K, strict)
+    assert len(e[0]) > 10_000
+    t, n_win = kma.SignatureTable.from_pegs(res, off, K)
+    assert n_win == sum(max(len(p) - K, 0) for p in close)
+    with t:
+        hits = kma.connect_pegs(t, dna, doff, 11, strict)
+    assert len(hits) == len(e[0])
+    for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"], hits["fid"]), e):
+        assert (a == b).all()
