@@ -233,6 +233,21 @@ int kma_connect_pegs(const kma_table* peg_table, const uint8_t* dna, const uint6
                      uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
                      uint64_t cap, uint64_t* n_hits);
 
+/* ---- signature-table construction (BuildKmerProcessor.java:137-223, RoleCounter.java) -------
+ * After role resolution by the host (Feature.getUsefulRoles + the interesting-role filter):
+ * roles[s] >= 0 is the single good role of an interesting peg, -1 marks a protein buffered for
+ * the deletion pass (no good role), any other negative value a peg that is skipped (several
+ * good roles). A kmer of ProteinKmers (distinct windows, i = 0..L-K; KMA_F_END_EXCLUSIVE for
+ * i < L-K) is kept iff every interesting peg containing it has the same role (RoleCounter
+ * isGood) and no buffered protein contains it. Output: (packed key, role) rows sorted by key
+ * (the reference prints HashMap order: compare as sets); KMA_E_CAPACITY with *n_out = needed
+ * if cap is too small; KMA_E_ALPHABET if a counted window holds a byte outside A-Z / '*'.
+ * Roles < 2^24 - 1. Runs on the device: window packing, radix sort of key << 24 | role,
+ * unique, one-role filter, select.                                                          */
+int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const int32_t* roles,
+                         uint32_t n_seq, int k, uint32_t flags, int device, uint64_t* out_keys,
+                         uint32_t* out_roles, uint64_t cap, uint64_t* n_out);
+
 /* Window count of the 6-frame extractor before the '*'/'X' filter (for throughput metrics).  */
 uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k);
 

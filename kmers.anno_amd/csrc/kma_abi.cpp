@@ -999,4 +999,91 @@ int kma_connect_pegs(const kma_table* t, const uint8_t* dna, const uint64_t* off
   return KMA_OK;
 }
 
+int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const int32_t* roles,
+                         uint32_t n_seq, int k, uint32_t flags, int device, uint64_t* out_keys,
+                         uint32_t* out_roles, uint64_t cap, uint64_t* n_out) {
+  if (!n_out) return fail(KMA_E_INVALID, "null argument");
+  *n_out = 0;
+  if (int rc = check_k(k)) return rc;
+  if (flags & ~KMA_F_END_EXCLUSIVE) return fail(KMA_E_INVALID, "bad flags");
+  if (n_seq == 0) return KMA_OK;
+  if (!residues || !offsets || !roles) return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t s = 0; s < n_seq; ++s) {
+    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
+    if (roles[s] >= (int32_t)kma::kBuildNeg)
+      return fail(KMA_E_INVALID, "role %d of protein %u >= 2^24 - 1", roles[s], s);
+  }
+  const uint64_t base = offsets[0], total = offsets[n_seq] - base;
+  if (total == 0) return KMA_OK;
+  uint8_t lut[256];
+  standard_lut(lut);
+  std::vector<uint64_t> rel(offsets, offsets + n_seq + 1);
+  for (auto& o : rel) o -= base;
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  DevBufs b;
+  uint8_t *d_res, *d_lut, *d_flags;
+  uint64_t *d_off, *d_a, *d_b, *d_n;
+  int32_t* d_roles;
+  uint32_t* d_alpha;
+  KMA_HIP(b.alloc(&d_res, total + 64));
+  KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_roles, n_seq * 4ull));
+  KMA_HIP(b.alloc(&d_lut, 256));
+  KMA_HIP(b.alloc(&d_a, total * 8));
+  KMA_HIP(b.alloc(&d_b, total * 8));
+  KMA_HIP(b.alloc(&d_flags, total));
+  KMA_HIP(b.alloc(&d_n, 16));
+  KMA_HIP(b.alloc(&d_alpha, 4));
+  KMA_HIP(hipMemcpy(d_res, residues + base, total, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_res + total, 0, 64));
+  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_seq + 1) * 8ull, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_roles, roles, n_seq * 4ull, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_lut, lut, 256, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_alpha, 0, 4));
+  KMA_HIP(kma::launch_build_windows(d_res, d_off, n_seq, d_roles, k,
+                                    (flags & KMA_F_END_EXCLUSIVE) ? 1 : 0, d_lut, d_a, d_alpha,
+                                    nullptr));
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  const int bits = 24 + 5 * k;
+  KMA_HIP(kma::launch_sort_keys(nullptr, &t1, d_a, d_b, total, bits, nullptr));
+  KMA_HIP(kma::launch_unique(nullptr, &t2, d_b, d_a, d_n, total, nullptr));
+  KMA_HIP(kma::launch_select_flagged_keys(nullptr, &t3, d_a, d_flags, d_b, d_n + 1, total,
+                                          nullptr));
+  size_t tb = std::max(t1, std::max(t2, t3));
+  void* d_temp;
+  KMA_HIP(b.alloc(&d_temp, tb));
+  size_t t = tb;
+  KMA_HIP(kma::launch_sort_keys(d_temp, &t, d_a, d_b, total, bits, nullptr));  // a -> b
+  t = tb;
+  KMA_HIP(kma::launch_unique(d_temp, &t, d_b, d_a, d_n, total, nullptr));  // b -> a
+  uint64_t n_u = 0;
+  uint32_t alpha = 0;
+  KMA_HIP(hipMemcpy(&n_u, d_n, 8, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(&alpha, d_alpha, 4, hipMemcpyDeviceToHost));
+  if (alpha)
+    return fail(KMA_E_ALPHABET, "a protein window holds a byte outside A-Z and '*'");
+  uint64_t n_sel = 0;
+  if (n_u) {
+    KMA_HIP(kma::launch_signature_flags(d_a, d_n, n_u, d_flags, nullptr));
+    t = tb;
+    KMA_HIP(kma::launch_select_flagged_keys(d_temp, &t, d_a, d_flags, d_b, d_n + 1, n_u,
+                                            nullptr));  // a -> b
+    KMA_HIP(hipMemcpy(&n_sel, d_n + 1, 8, hipMemcpyDeviceToHost));
+  }
+  *n_out = n_sel;
+  if (n_sel > cap || (n_sel && (!out_keys || !out_roles)))
+    return fail(KMA_E_CAPACITY, "%llu signature kmers, capacity %llu",
+                (unsigned long long)n_sel, (unsigned long long)cap);
+  if (n_sel == 0) return KMA_OK;
+  std::vector<uint64_t> rows(n_sel);
+  KMA_HIP(hipMemcpy(rows.data(), d_b, n_sel * 8, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n_sel; ++i) {
+    out_keys[i] = rows[i] >> 24;
+    out_roles[i] = (uint32_t)(rows[i] & kma::kBuildNeg);
+  }
+  return KMA_OK;
+}
+
 }  // extern "C"

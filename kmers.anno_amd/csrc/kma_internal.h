@@ -226,6 +226,22 @@ hipError_t launch_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* key
                              uint64_t n, int key_bits, hipStream_t stream);
 hipError_t launch_singleton_flags(const uint64_t* sorted_keys, uint64_t n, uint8_t* flags,
                                   hipStream_t stream);
+// Signature build (BuildKmerProcessor): composite = key << 24 | role (0xFFFFFF = buffered
+// protein) per window of ProteinKmers; sort; unique; keep keys with one role and no buffered
+// occurrence.
+constexpr uint32_t kBuildNeg = 0xFFFFFFu;
+hipError_t launch_build_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq,
+                                const int32_t* roles, int k, int end_exclusive, const uint8_t* lut,
+                                uint64_t* out, uint32_t* alpha_flag, hipStream_t stream);
+hipError_t launch_sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
+                            uint64_t n, int bits, hipStream_t stream);
+hipError_t launch_unique(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
+                         uint64_t* n_out, uint64_t n, hipStream_t stream);
+hipError_t launch_signature_flags(const uint64_t* uniq, const uint64_t* n_uniq, uint64_t n_max,
+                                  uint8_t* flags, hipStream_t stream);
+hipError_t launch_select_flagged_keys(void* temp, size_t* temp_bytes, const uint64_t* in,
+                                      const uint8_t* flags, uint64_t* out, uint64_t* n_out,
+                                      uint64_t n, hipStream_t stream);
 hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
                                  const uint32_t* vals_in, const uint8_t* flags, uint64_t* keys_out,
                                  uint32_t* vals_out, uint64_t* n_out, uint64_t n,

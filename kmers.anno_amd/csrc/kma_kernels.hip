@@ -1404,6 +1404,64 @@ __global__ __launch_bounds__(256) void singleton_flags_kernel(const uint64_t* __
   }
 }
 
+// Signature build (BuildKmerProcessor.java:137-223). One wave per protein: the windows of
+// ProteinKmers (i = 0..L-K, or i < L-K with end_exclusive) of interesting pegs (role >= 0) and
+// buffered proteins (role -1) become key << 24 | role (kBuildNeg for buffered); every other
+// position gets 0. A window with a byte the standard alphabet cannot encode raises alpha_flag
+// (the host refuses the batch rather than drop a kmer the reference would keep).
+__global__ __launch_bounds__(256) void build_windows_kernel(const uint8_t* __restrict__ residues,
+                                                            const uint64_t* __restrict__ offsets,
+                                                            uint32_t n_seq,
+                                                            const int32_t* __restrict__ roles,
+                                                            int k, int end_exclusive,
+                                                            const uint8_t* __restrict__ lut_g,
+                                                            uint64_t* __restrict__ out,
+                                                            uint32_t* __restrict__ alpha_flag) {
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = lut_g[threadIdx.x];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t o0 = offsets[0];
+  for (uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < n_seq;
+       s += (uint64_t)gridDim.x * 4) {
+    const uint64_t lo = offsets[s], hi = offsets[s + 1];
+    const int32_t role = roles[s];
+    const int64_t n_win = (int64_t)(hi - lo) - k + (end_exclusive ? 0 : 1);
+    const bool counted = role >= -1;
+    const uint64_t tag = role >= 0 ? (uint64_t)role : (uint64_t)kBuildNeg;
+    bool bad = false;
+    for (uint64_t p = lo + lane; p < hi; p += 64) {
+      const int64_t i = (int64_t)(p - lo);
+      uint64_t v = 0;
+      if (counted && i < n_win) {
+        uint64_t key = 0;
+        bool ok = true;
+        for (int j = 0; j < k; ++j) {
+          const uint32_t c = lut[residues[p + j]];
+          ok = ok && c != 0u;
+          key = (key << 5) | c;
+        }
+        bad = bad || !ok;
+        v = ok ? (key << 24) | tag : 0;
+      }
+      out[p - o0] = v;
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(alpha_flag, 1u);
+  }
+}
+
+__global__ __launch_bounds__(256) void signature_flags_kernel(const uint64_t* __restrict__ u,
+                                                              const uint64_t* __restrict__ n_u,
+                                                              uint8_t* __restrict__ flags) {
+  const uint64_t n = *n_u;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256) {
+    const uint64_t v = u[i], key = v >> 24;
+    flags[i] = key != 0 && (v & kBuildNeg) != kBuildNeg && (i == 0 || (u[i - 1] >> 24) != key) &&
+               (i + 1 == n || (u[i + 1] >> 24) != key);
+  }
+}
+
 // Emit pass: block b's staged hits go to out[prefix[b] ..], those past `cap` are dropped; the
 // last block publishes the total (the caller compares it with cap).
 __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a) {
@@ -1668,6 +1726,38 @@ hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t*
   if (e != hipSuccess) return e;
   return hipcub::DeviceSelect::Flagged(temp, need, vals_in, flags, vals_out, n_out, (int)n,
                                        stream);
+}
+
+hipError_t launch_build_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq,
+                                const int32_t* roles, int k, int end_exclusive, const uint8_t* lut,
+                                uint64_t* out, uint32_t* alpha_flag, hipStream_t stream) {
+  const unsigned g = (unsigned)std::min<uint64_t>(8192, ((uint64_t)n_seq + 3) / 4);
+  hipLaunchKernelGGL(build_windows_kernel, dim3(g ? g : 1), dim3(256), 0, stream, residues,
+                     offsets, n_seq, roles, k, end_exclusive, lut, out, alpha_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
+                            uint64_t n, int bits, hipStream_t stream) {
+  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, (int)n, 0, bits, stream);
+}
+
+hipError_t launch_unique(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
+                         uint64_t* n_out, uint64_t n, hipStream_t stream) {
+  return hipcub::DeviceSelect::Unique(temp, *temp_bytes, in, out, n_out, (int)n, stream);
+}
+
+hipError_t launch_signature_flags(const uint64_t* uniq, const uint64_t* n_uniq, uint64_t n_max,
+                                  uint8_t* flags, hipStream_t stream) {
+  hipLaunchKernelGGL(signature_flags_kernel, dim3(grid_for(n_max)), dim3(256), 0, stream, uniq,
+                     n_uniq, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_select_flagged_keys(void* temp, size_t* temp_bytes, const uint64_t* in,
+                                      const uint8_t* flags, uint64_t* out, uint64_t* n_out,
+                                      uint64_t n, hipStream_t stream) {
+  return hipcub::DeviceSelect::Flagged(temp, *temp_bytes, in, flags, out, n_out, (int)n, stream);
 }
 
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {

@@ -31,7 +31,7 @@ EXPORTS = (
     "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_workspace_reserve_contigs", "kma_annotate_contigs_device", "kma_contig_window_count",
-    "kma_peg_table_create", "kma_connect_pegs",
+    "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures",
 )
 
 
@@ -96,6 +96,8 @@ def load(path: str | None = None):
         L.kma_workspace_reserve_contigs.argtypes = [_vp, _u64]
         L.kma_annotate_contigs_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _vp,
                                                   _u64, _vp, _vp, _u32, _vp]
+        L.kma_build_signatures.argtypes = [_u8p, _u64p, _i32p, _u32, _int, _u32, _int, _vp, _vp,
+                                           _u64, C.POINTER(_u64)]
         L.kma_peg_table_create.argtypes = [_u8p, _u64p, _u32, _int, _int, C.c_double,
                                            C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_connect_pegs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _int, _vp, _u64,
@@ -334,6 +336,25 @@ def connect_pegs(peg_table: SignatureTable, dna: np.ndarray, offsets: np.ndarray
             continue
         _check(rc)
         return hits[:nh.value]
+
+
+def build_signatures(residues: np.ndarray, offsets: np.ndarray, roles, k: int = 8,
+                     flags: int = 0, device: int = 0):
+    """BuildKmerProcessor's discriminating kmers on the GPU: (packed keys, roles), key order."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    roles = np.ascontiguousarray(roles, np.int32)
+    n = len(offsets) - 1
+    cap = 1 << 16
+    while True:
+        keys, rl, nout = np.empty(cap, np.uint64), np.empty(cap, np.uint32), _u64()
+        rc = load().kma_build_signatures(residues, offsets, roles, n, k, flags, device,
+                                         keys.ctypes.data, rl.ctypes.data, cap, C.byref(nout))
+        if rc == E_CAPACITY:
+            cap = nout.value
+            continue
+        _check(rc)
+        return keys[:nout.value], rl[:nout.value]
 
 
 def contig_window_count(offsets: np.ndarray, k: int = 8) -> int:

@@ -57,6 +57,9 @@ def lib():
         L.orc_peg_connect.argtypes = [_u8p, _u64p, C.c_uint32, _u8p, _u64p, C.c_uint32, C.c_int,
                                       C.c_int, C.c_int, _u32p, _i32p, _u8p, _u8p, _u32p,
                                       C.c_uint64]
+        L.orc_build.restype = C.c_uint64
+        L.orc_build.argtypes = [_u8p, _u64p, _i32p, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p,
+                                C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -157,3 +160,14 @@ def peg_connect(residues, offsets, dna, doffsets, gcode: int = 11, k: int = 8, s
     sd, fr, pg = np.empty(n, np.uint8), np.empty(n, np.uint8), np.empty(n, np.uint32)
     lib().orc_peg_connect(*args, ct, lf, sd, fr, pg, n)
     return ct, lf, sd, fr, pg
+
+
+def build_signatures(residues, offsets, roles, k: int = 8, flags: int = 0):
+    """BuildKmerProcessor's discriminating kmers: (kmers[n, k] bytes, roles[n]) in table order."""
+    roles = np.ascontiguousarray(roles, np.int32)
+    n_seq = len(offsets) - 1
+    n = lib().orc_build(residues, offsets, roles, n_seq, k, flags, None, None, 0)
+    km = np.empty((n, k), np.uint8)
+    rl = np.empty(n, np.int32)
+    lib().orc_build(residues, offsets, roles, n_seq, k, flags, km.ctypes.data, rl.ctypes.data, n)
+    return km, rl

@@ -465,3 +465,51 @@ uint64_t orc_peg_connect(const uint8_t* residues, const uint64_t* offsets, uint3
   free(pk), free(pp), free(pl), free(ck), free(ct), free(lf), free(st), free(fr), free(hits);
   return nh;
 }
+
+/* BuildKmerProcessor.runCommand (anno/BuildKmerProcessor.java:137-223) with RoleCounter
+ * (kmers/RoleCounter.java:30-55), after role resolution: role[s] >= 0 is the single good role
+ * of an interesting peg, -1 marks a buffered protein (no good role), anything else a peg with
+ * several good roles (skipped, :163-175). Pass 1: for every distinct kmer of every interesting
+ * peg (ProteinKmers set), kmerMap.computeIfAbsent(kmer, RoleCounter(role)).count(role); a kmer
+ * counted for a second role is bad and deleted (:178-188). Pass 2: every kmer of a buffered
+ * protein is removed (:191-205). Surviving (kmer, role) rows are written in table order (the
+ * reference prints HashMap order: compare as sets). Returns the number of rows. */
+uint64_t orc_build(const uint8_t* residues, const uint64_t* offsets, const int32_t* role,
+                   uint32_t n_seq, int K, uint32_t flags, char* out_kmers, int32_t* out_role,
+                   uint64_t cap) {
+  orc_table* m = orc_table_new(0, 0, 0, 0);
+  kmer_set set = {0};
+  for (uint32_t s = 0; s < n_seq; s++) {
+    if (role[s] < 0) continue;
+    const char* p = (const char*)residues + offsets[s];
+    kmer_set_build(&set, p, (int64_t)(offsets[s + 1] - offsets[s]), K, flags & ~ORC_F_MULTISET);
+    for (uint32_t j = 0; j < set.n; j++) {
+      const char* km = p + set.order[j];
+      const int32_t v = orc_table_get(m, km, K);
+      if (v == -1) orc_table_put(m, km, K, role[s]);       /* new RoleCounter(role), good hit */
+      else if (v >= 0 && v != role[s]) orc_table_put(m, km, K, -3); /* bad: another role */
+    }
+  }
+  for (uint32_t s = 0; s < n_seq; s++) {
+    if (role[s] != -1) continue;
+    const char* p = (const char*)residues + offsets[s];
+    kmer_set_build(&set, p, (int64_t)(offsets[s + 1] - offsets[s]), K, flags & ~ORC_F_MULTISET);
+    for (uint32_t j = 0; j < set.n; j++) {
+      const char* km = p + set.order[j];
+      if (orc_table_get(m, km, K) != -1) orc_table_put(m, km, K, -4); /* kmerMap.remove */
+    }
+  }
+  uint64_t n = 0;
+  for (uint64_t b = 0; b <= m->mask; b++)
+    for (orc_node* x = m->buckets[b]; x; x = x->next) {
+      if (x->value < 0) continue;
+      if (n < cap) {
+        memcpy(out_kmers + n * K, x->key, (size_t)K);
+        out_role[n] = x->value;
+      }
+      n++;
+    }
+  free(set.slots), free(set.order);
+  orc_table_free(m);
+  return n;
+}

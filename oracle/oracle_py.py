@@ -140,3 +140,23 @@ def peg_connect(prots, contigs, gcode: int = 11, k: int = 8, strict: bool = Fals
            for km, v in locs.items() if km in singles for ci, left, strand, frame in v]
     out.sort(key=lambda h: (h[0], h[1], h[2]))
     return out
+
+
+def build_signatures(prots, roles, k: int = 8, end_exclusive: bool = False):
+    """BuildKmerProcessor.java:137-223 + RoleCounter: roles[i] >= 0 = the single good role of
+    an interesting peg, -1 = a buffered protein, other = skipped. Returns {kmer: role}."""
+    first, bad = {}, set()
+    for p, r in zip(prots, roles):
+        if r < 0:
+            continue
+        for km in protein_kmers(p, k, end_exclusive, False):
+            if km not in first:
+                first[km] = r
+            elif first[km] != r:
+                bad.add(km)
+    keep = {km: r for km, r in first.items() if km not in bad}
+    for p, r in zip(prots, roles):
+        if r == -1:
+            for km in protein_kmers(p, k, end_exclusive, False):
+                keep.pop(km, None)
+    return keep
