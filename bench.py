@@ -44,7 +44,7 @@ BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probe
 GATHER_CEILING_GBS = 3544.2
 # Per-launch HBM traffic of K1 from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (scripts/
 # gpu_traffic.sh), calibrated on the gather bench (scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01b_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01c_traffic.json")
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
           "8-mer signature table, 1 MI355X per rank",
@@ -227,6 +227,12 @@ def bench_contigs(args, rank, world, dev, stream, sp):
         # one 8-B staged record per hit.
         alg_bytes = n_probe * BYTES_PER_LOOKUP + n_bases + 8 * n_hits
         achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
+        kname = f"contigs_probe_quad_kernel<{K}, {table.info.minimizer_len}>"
+        traffic = None
+        try:
+            traffic = json.load(open(TRAFFIC_FILE))["workloads"]["c3"][kname]["traffic_bytes"]
+        except (OSError, KeyError, ValueError):
+            pass
         out = {
             "metric": "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs "
                       "roofline",
@@ -244,8 +250,10 @@ def bench_contigs(args, rank, world, dev, stream, sp):
             "gpu_ms_per_step": gpu_ms / args.steps,
             "phases_ms": {"probe": k1_ms, "scan_emit": rest_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "contigs_probe_kernel (6-frame translate + 2 probes per base)",
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": f"{os.path.relpath(TRAFFIC_FILE, ROOT)} (rocprofv3 "
+                                           "FETCH_SIZE + WRITE_SIZE per launch, calibrated)",
+                         "kernel": f"{kname} (6-frame translate + 2 probes per base)",
                          "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
                          "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
         }
@@ -264,6 +272,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--load-factor", type=float, default=0.5)
+    ap.add_argument("--n-seq", type=int, default=0,
+                    help="override the workload's proteins per rank (tuning runs only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -286,6 +296,7 @@ def main():
         return
 
     n_seq, t_size, n_fid, seed = synth.CONFIGS[args.workload]
+    n_seq = args.n_seq or n_seq
     t0 = time.perf_counter()
     sig = synth.make_table(t_size, n_fid, seed, K)
     residues, offsets, _, _ = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17 + rank)
@@ -314,6 +325,7 @@ def main():
     elapsed, gpu_ms, k1_ms, k2_ms = timed(step, ws, args, world, stream, dev,
                                         before=d_tally.zero_, after=reduce)
 
+    fused = ws.protein_form(n_seq) == 1
     st = d_st.cpu().numpy()
     called = int((st == kmeranno.STATUS_CALLED).sum())
     if rank == 0:
@@ -325,11 +337,14 @@ def main():
         # position probed, + 1 B per residue streamed in.
         alg_bytes = n_pos * (BYTES_PER_LOOKUP + 4) + n_res
         achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
-        k1_name = os.environ.get("KMA_PROBE", "quad")
-        k1_name = {"lane": "probe_kernel", "run": "probe_run_kernel"}.get(k1_name,
-                                                                          "probe_quad_kernel")
         m = table.info.minimizer_len
-        k1_name = f"{k1_name}<{K}, {m}, 3>"
+        if fused:
+            k1_name = f"annotate_kernel<{K}, {m}, 4>"
+        else:
+            k1_name = os.environ.get("KMA_PROBE", "quad")
+            k1_name = {"lane": "probe_kernel", "run": "probe_run_kernel"}.get(
+                k1_name, "probe_quad_kernel")
+            k1_name = f"{k1_name}<{K}, {m}, 3>"
         traffic = None
         try:
             tr = json.load(open(TRAFFIC_FILE))["workloads"][args.workload][k1_name]
@@ -359,12 +374,15 @@ def main():
             "seqs_per_s": seqs_per_s,
             "called_per_batch": called,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"probe_K1": k1_ms, "vote_K2": k2_ms},
+            "phases_ms": ({"probe_vote_K12": k1_ms, "vote_long": k2_ms} if fused else
+                          {"probe_K1": k1_ms, "vote_K2": k2_ms}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": "profiles/r01b_traffic.json (rocprofv3 FETCH_SIZE + "
-                                           "WRITE_SIZE per launch, calibrated)",
-                         "kernel": f"{k1_name} (K1: every window's bucket gather)",
+                         "traffic_source": f"{os.path.relpath(TRAFFIC_FILE, ROOT)} (rocprofv3 "
+                                           "FETCH_SIZE + WRITE_SIZE per launch, calibrated)",
+                         "kernel": f"{k1_name} " + ("(K12: every window's bucket gather + the "
+                                                    "vote, fused)" if fused else
+                                                    "(K1: every window's bucket gather)"),
                          "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
                          "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
         }

@@ -167,6 +167,11 @@ int kma_workspace_destroy(kma_workspace* ws);
  * the recorded events (the last 256 calls), returns their count and summed milliseconds, and
  * clears the accumulators.                                                                  */
 int kma_workspace_timing(kma_workspace* ws, int enable);
+/* Which kernel form kma_annotate_proteins_device uses for a batch of n_seq proteins on this
+ * workspace's device: 1 = the fused probe + vote kernel (large batches), 0 = the two-kernel
+ * probe / vote pipeline (small batches, where the vote cannot hide behind other blocks'
+ * gathers). KMA_FUSED=0|1 in the environment forces one form. For reports and tuning.       */
+int kma_protein_form(const kma_workspace* ws, uint32_t n_seq);
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* probe_ms,
                               double* vote_ms);
 

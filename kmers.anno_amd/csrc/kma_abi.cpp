@@ -87,6 +87,15 @@ int segments_for(uint32_t n_seq) {
   return std::max(1, std::min(s, std::min<int>(kMaxSegments, (int)std::max<uint32_t>(1, n_seq))));
 }
 
+// Protein path form: the fused probe + vote kernel K12 for batches of at least
+// kma::fused_min_proteins proteins, else the two-kernel K1 / K2 pipeline. KMA_FUSED=1 / 0
+// forces one form (A/B runs; segmented overlap and the K1/K2 variants need the two-kernel form).
+bool fused_form(uint32_t n_seq, int n_cu) {
+  const char* e = getenv("KMA_FUSED");  // read per call: tests switch forms in one process
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return n_seq >= kma::fused_min_proteins(n_cu);
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -593,6 +602,12 @@ int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* prob
   return KMA_OK;
 }
 
+int kma_protein_form(const kma_workspace* ws, uint32_t n_seq) {
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  DeviceScope ds(ws->device);
+  return fused_form(n_seq, ws->n_cu) ? 1 : 0;
+}
+
 int kma_workspace_destroy(kma_workspace* ws) {
   if (!ws) return KMA_OK;
   DeviceScope ds(ws->device);
@@ -655,6 +670,19 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   if (ws->timing) {
     ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
     KMA_HIP(hipEventRecord(ev[0], s));
+  }
+  if (fused_form(n_seq, ws->n_cu)) {
+    // K12 (probe + vote in one kernel), then vote_long for the pending proteins.
+    a.seq_lo = 0;
+    a.seq_hi = n_seq;
+    a.reset_flag = 0;
+    KMA_HIP(hipMemsetAsync(ws->d_flag, 0, 8, s));  // pending-list lengths (K12 appends)
+    if (ev) KMA_HIP(hipEventRecord(ev[0], s));     // the probe phase is K12 alone
+    KMA_HIP(kma::launch_fused(a, ws->n_cu, s));
+    if (ev) KMA_HIP(hipEventRecord(ev[1], s));
+    KMA_HIP(kma::launch_long(a, ws->n_cu, s));
+    if (ev) KMA_HIP(hipEventRecord(ev[2], s));
+    return KMA_OK;
   }
   if (ev) {
     // Timing mode: the phases back to back on the call's stream, so their events bracket them.

@@ -211,6 +211,8 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
 hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K1
 hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream);   // K2 (segment)
 hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream);   // long proteins
+hipError_t launch_fused(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K12 = K1 + K2
+uint32_t fused_min_proteins(int n_cu);  // K12 is used for batches of at least this many proteins
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
                               void* temp, size_t* temp_bytes, hipStream_t stream);

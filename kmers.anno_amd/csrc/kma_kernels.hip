@@ -361,6 +361,93 @@ __device__ __forceinline__ void chain_flush(const ProteinArgs& a, const uint8_t*
   __builtin_amdgcn_wave_barrier();
 }
 
+// The K1 quad loop over positions g0 + j * 256 + t (j < U) in steps of `stride`, up to n_pos
+// (positions relative to offsets[0]); `cq` is the calling wave's chain queue.
+template <int K, int M, int U>
+__device__ __forceinline__ void probe_span(const ProteinArgs& a, const uint8_t* lut, uint64_t* cq,
+                                           const uint8_t* __restrict__ res, uint64_t g0,
+                                           uint64_t n_pos, uint64_t stride) {
+  const int t = threadIdx.x, part = t & 3;
+  uint32_t cn = 0;  // wave-uniform queue length
+  const uint64_t* __restrict__ slots = a.slots;
+  const uint32_t nb = a.n_buckets;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
+  // flight, so a wave's only exposed latency per step is the bucket gather.
+  WinWords ww[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t g = g0 + j * 256 + t;
+    ww[j] = window_words(res, g < n_pos ? g : 0);
+  }
+  for (; g0 < n_pos; g0 += stride) {
+    uint32_t klo[U], khi[U], bk[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      uint64_t key;
+      const bool ok = pack_window<K>(lut, funnel(ww[j].lo, ww[j].hi, ww[j].sh), key) &&
+                      g0 + j * 256 + t < n_pos;
+      klo[j] = (uint32_t)key;
+      khi[j] = (uint32_t)(key >> 32) << 24;
+      bk[j] = ok ? home_bucket(key, K, M, nb) : kNone;
+    }
+    // Cooperative loads: all 4U dwordx4 of the lane in flight before any compare. A window
+    // that does not probe reads bucket 0 (its result is discarded): no branch-merged loads.
+    uint4 q[U][4];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint32_t b0 = quad_bcast<0>(bk[j]), b1 = quad_bcast<1>(bk[j]);
+      const uint32_t b2 = quad_bcast<2>(bk[j]), b3 = quad_bcast<3>(bk[j]);
+      const uint4* base = reinterpret_cast<const uint4*>(slots) + part;
+      q[j][0] = base[(uint64_t)(b0 == kNone ? 0u : b0) * 4];
+      q[j][1] = base[(uint64_t)(b1 == kNone ? 0u : b1) * 4];
+      q[j][2] = base[(uint64_t)(b2 == kNone ? 0u : b2) * 4];
+      q[j][3] = base[(uint64_t)(b3 == kNone ? 0u : b3) * 4];
+    }
+    // Next step's residues (issued after the bucket loads: waiting for those leaves these in
+    // flight, vmcnt counts in order).
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t g = g0 + stride + j * 256 + t;
+      ww[j] = window_words(res, g < n_pos ? g : 0);
+    }
+    uint32_t word[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      word[j] = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t kl = r == 0 ? quad_bcast<0>(klo[j]) : r == 1 ? quad_bcast<1>(klo[j])
+                          : r == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
+        const uint32_t kh = r == 0 ? quad_bcast<0>(khi[j]) : r == 1 ? quad_bcast<1>(khi[j])
+                          : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
+        // Branch-free on purpose: a short-circuit here lets the compiler split the 16-byte
+        // load into a lazily loaded tail behind a branch and a vmcnt(0).
+        const uint32_t x = match_part(q[j][r], kl, kh, part);
+        word[j] = part == r ? x : word[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t g = g0 + j * 256 + t;
+      if (g < n_pos) {
+        const uint32_t w = bk[j] != kNone ? word[j] & kWordFid : 0u;
+        a.hits[g] = w;
+        // Slot ids only under hits (K2 reads them nowhere else): misses store nothing.
+        if (w) a.sids[g] = bk[j] * kSlotsPerBucket + ((word[j] >> kSlotShift) & 7u);
+      }
+      chain_push(cq, cn, bk[j] != kNone && word[j] == 0x80000000u, g);  // rare: chain walk
+    }
+    if (cn > kChainQ - 64 * U) {
+      chain_flush<K, M>(a, lut, res, cq, cn);
+      cn = 0;
+    }
+  }
+  if (cn) chain_flush<K, M>(a, lut, res, cq, cn);
+}
+
+// K1 kernel (two-kernel form, KMA_FUSED=0): the same loop as probe_span written out in the
+// kernel (the register allocation of the inlined function costs it one wave per SIMD).
 template <int K, int M, int U>
 __global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
@@ -768,20 +855,28 @@ __device__ __forceinline__ uint32_t dedupe_insert(uint32_t* set, uint32_t cap, c
 // with KMA_VOTE_TRACE builds), so every wave has all its loads in flight at once and blocks are
 // small enough (LDS, registers) for many to be resident.
 // ---------------------------------------------------------------------------------------------
-template <int K>
-__global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
+// K2's LDS (a struct so that the fused kernel can overlay it on K1's chain queues).
+template <int P>
+struct VoteSmem {
+  __attribute__((aligned(16))) uint32_t pool[kVotePool];
+  uint64_t pbase_w[P];  // word index of window 0
+  uint32_t pwin[P], chunk0[P + 1], pmin[P], pmax[P], phits[P], pcnt[P], pbase[P], pcap[P];
+  uint32_t pool_top;
+};
+
+// The vote of proteins [p0, p0 + np) by the block (np <= P).
+template <int K, int P>
+__device__ __forceinline__ void vote_group(const ProteinArgs& a, VoteSmem<P>& sm, uint32_t p0,
+                                           int np) {
   constexpr int W = kVoteWaves;
-  constexpr int P = kVoteProteins;
   constexpr int U = kVoteHold;
   static_assert(P <= 64 && (P & (P - 1)) == 0, "header is one wave; binary search needs 2^n");
-  __shared__ __attribute__((aligned(16))) uint32_t pool[kVotePool];
-  __shared__ uint64_t pbase_w[P];  // word index of window 0
-  __shared__ uint32_t pwin[P], chunk0[P + 1], pmin[P], pmax[P], phits[P], pcnt[P], pbase[P],
-      pcap[P];
-  __shared__ uint32_t pool_top;
+  uint32_t* pool = sm.pool;
+  uint64_t* pbase_w = sm.pbase_w;
+  uint32_t *pwin = sm.pwin, *chunk0 = sm.chunk0, *pmin = sm.pmin, *pmax = sm.pmax,
+           *phits = sm.phits, *pcnt = sm.pcnt, *pbase = sm.pbase, *pcap = sm.pcap;
+  uint32_t& pool_top = sm.pool_top;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t p0 = a.seq_lo + blockIdx.x * P;
-  const int np = (int)min<uint32_t>(P, a.seq_hi - p0);
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
 #ifdef KMA_VOTE_TRACE
   if (tid > 0 && tid < 7) a.scratch[blockIdx.x * 8 + tid] = 0;
@@ -955,6 +1050,43 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
   finish();
   KMA_TRACE_AT(6)
 #undef KMA_TRACE_AT
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
+  __shared__ VoteSmem<kVoteProteins> sm;
+  const uint32_t p0 = a.seq_lo + blockIdx.x * kVoteProteins;
+  vote_group<K, kVoteProteins>(a, sm, p0, (int)min<uint32_t>(kVoteProteins, a.seq_hi - p0));
+}
+
+// ---------------------------------------------------------------------------------------------
+// K12 — fused probe + vote (default). A block owns kVoteProteins consecutive proteins: it probes
+// every residue position of their span with K1's quad loop (words and slot ids to the
+// workspace, where they stay L2-resident), then votes them with K2's block logic. No second
+// kernel, no kernel boundary between the phases, and one block's vote (latency-bound LDS and
+// L2 work) overlaps the bucket gathers of the blocks around it. K1's chain queues and K2's
+// set pool share the block's LDS.
+// ---------------------------------------------------------------------------------------------
+template <int K, int M, int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(ProteinArgs a) {
+  constexpr int U = kProbeWin;
+  __shared__ uint8_t lut[256];
+  __shared__ union Smem {
+    uint64_t chain_q[4][kChainQ];
+    VoteSmem<P> vote;
+  } sm;
+  const int t = threadIdx.x;
+  lut[t] = a.lut[t];
+  const uint32_t p0 = a.seq_lo + blockIdx.x * P;
+  const int np = (int)min<uint32_t>(P, a.seq_hi - p0);
+  __syncthreads();
+  const uint64_t o0 = a.offsets[0];
+  const uint64_t n_all = a.n_residues >= (uint64_t)K ? a.n_residues - K + 1 : 0;
+  const uint64_t lo = a.offsets[p0] - o0, hi = a.offsets[p0 + np] - o0;
+  probe_span<K, M, U>(a, lut, sm.chain_q[t >> 6], a.residues + o0, lo, hi < n_all ? hi : n_all,
+                      256 * U);
+  __syncthreads();  // this block's words and slot ids are written (and visible to its waves)
+  vote_group<K, P>(a, sm.vote, p0, np);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1620,6 +1752,50 @@ static hipError_t launch_long_k(const ProteinArgs& a, int n_cu, hipStream_t stre
     case 8: return FN<8>(a, n_cu, stream);               \
     default: return hipErrorInvalidValue;                \
   }
+
+// Proteins per K12 block (KMA_FUSED_P=4|8 for A/B).
+static int fused_proteins() {
+  static const int p = [] {
+    const char* e = getenv("KMA_FUSED_P");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
+  return p;
+}
+
+template <int K, int P>
+static hipError_t launch_fused_kp(const ProteinArgs& a, hipStream_t stream) {
+  constexpr int M6 = K < 6 ? K : 6;
+  constexpr int M7 = K < 7 ? M6 : 7;
+  const unsigned blocks = (a.seq_hi - a.seq_lo + P - 1) / P;
+  if (!blocks) return hipSuccess;
+  if (a.mlen == M7 && M7 != M6)
+    hipLaunchKernelGGL((annotate_kernel<K, M7, P>), dim3(blocks), dim3(256), 0, stream, a);
+  else if (a.mlen == M6)
+    hipLaunchKernelGGL((annotate_kernel<K, M6, P>), dim3(blocks), dim3(256), 0, stream, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t launch_fused_k(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  return fused_proteins() == 8 ? launch_fused_kp<K, 8>(a, stream)
+                               : launch_fused_kp<K, 4>(a, stream);
+}
+
+// Batch size (proteins) from which K12 beats K1 + K2 (measured on MI355X, 10M-entry table:
+// equal at 20k proteins, +11% at 40k, +18% at 300k, -2% at 10k): K12's vote is latency-bound
+// and only hides behind other blocks' gathers when the grid is several resident
+// populations deep; 2.5 populations.
+uint32_t fused_min_proteins(int n_cu) {
+  static const unsigned bpc = resident_blocks(annotate_kernel<8, 6, 4>);
+  return (uint32_t)(2.5 * n_cu * bpc * fused_proteins());
+}
+
+hipError_t launch_fused(const ProteinArgs& a, int n_cu, hipStream_t stream) {
+  if (a.n_seq == 0) return hipSuccess;
+  KMA_DISPATCH_K(launch_fused_k)
+}
 
 hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream) {
   if (a.n_seq == 0) return hipSuccess;

@@ -31,7 +31,7 @@ EXPORTS = (
     "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_workspace_reserve_contigs", "kma_annotate_contigs_device", "kma_contig_window_count",
-    "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures",
+    "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures", "kma_protein_form",
 )
 
 
@@ -94,6 +94,7 @@ def load(path: str | None = None):
         L.kma_annotate_contigs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _vp, _u64,
                                            C.POINTER(_u64), _vp, _u32]
         L.kma_workspace_reserve_contigs.argtypes = [_vp, _u64]
+        L.kma_protein_form.argtypes = [_vp, _u32]
         L.kma_annotate_contigs_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _vp,
                                                   _u64, _vp, _vp, _u32, _vp]
         L.kma_build_signatures.argtypes = [_u8p, _u64p, _i32p, _u32, _int, _u32, _int, _vp, _vp,
@@ -231,6 +232,13 @@ class Workspace:
 
     def reserve(self, n_residues: int):
         _check(load().kma_workspace_reserve(self._h, n_residues))
+
+    def protein_form(self, n_seq: int) -> int:
+        """1 if a batch of n_seq proteins runs the fused probe + vote kernel, 0 if K1 + K2."""
+        rc = load().kma_protein_form(self._h, n_seq)
+        if rc < 0:
+            _check(rc)
+        return rc
 
     def reserve_contigs(self, n_bases: int):
         _check(load().kma_workspace_reserve_contigs(self._h, n_bases))

@@ -12,7 +12,7 @@ GB=kmers.anno_amd/build/kma_gather_bench
 for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
   tag=$(echo $c | cut -d' ' -f1)
   step pmc_gather_$tag 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_gather_$tag -o run -- $GB ${GATHER_MIB:-1536} quad 4
-  for wl in ${WLS:-c2 c5}; do
+  for wl in ${WLS:-c2 c3 c5}; do
     step pmc_${wl}_$tag 900 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${wl}_$tag -o run -- python3 bench.py --steps 3 --warmup 1 --workload $wl --no-cpu-baseline
   done
 done

@@ -20,7 +20,8 @@ def load(d):
         return {}
     per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in csv.DictReader(open(files[0])):
-        m = re.search(r"(probe_\w+_kernel<[^>]*>|vote_\w+kernel<[^>]*>|vote_kernel<[^>]*>|gather_\w+)",
+        m = re.search(r"(probe_\w+_kernel<[^>]*>|vote_\w+kernel<[^>]*>|vote_kernel<[^>]*>|"
+                      r"annotate_kernel<[^>]*>|contigs_\w+_kernel(?:<[^>]*>)?|gather_\w+)",
                       r["Kernel_Name"])
         if not m:
             continue
@@ -35,7 +36,7 @@ corr = lines * 64 / (g[gk]["FETCH_SIZE"] * 1024)
 out = {"calibration": {"kernel": gk, "lines_per_launch": lines,
                        "fetch_bytes": g[gk]["FETCH_SIZE"] * 1024, "factor": corr},
        "workloads": {}}
-for wl in ("c2", "c5"):
+for wl in ("c2", "c3", "c5"):
     f, w, t = (load(f"{root}/pmc_{wl}_{c}") for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum"))
     if not f:
         continue

@@ -18,6 +18,14 @@ pytestmark = pytest.mark.gpu
 K = 8
 
 
+@pytest.fixture(autouse=True, params=["0", "1"], ids=["K1+K2", "K12"])
+def protein_form(request, monkeypatch):
+    """Every test under both protein-path forms: the two-kernel K1 + K2 pipeline and the fused
+    K12 kernel (the library picks by batch size; KMA_FUSED forces one, read per call)."""
+    monkeypatch.setenv("KMA_FUSED", request.param)
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def kma(native_lib):
     import kmeranno
