@@ -1355,6 +1355,26 @@ __global__ __launch_bounds__(256) void contigs_probe_kernel(ContigArgs a) {
 // thread 0) and their offsets cached in LDS, so a position's contig costs no global loads.
 constexpr int kOffCache = 64;
 
+// contig_of by a whole wave, 64 candidates per dependent load: the largest c < n with
+// off[c] <= g (off[0] <= g), in ceil(log64 n) rounds (one for up to 64 contigs) instead of
+// log2 n dependent loads by one lane. Offsets are non-decreasing, so the lanes whose candidate
+// is <= g form a prefix.
+__device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ off, uint32_t n,
+                                                   uint64_t g) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t lo = 0, span = n;  // the answer lies in [lo, lo + span)
+  while (span > 1) {          // wave-uniform
+    const uint32_t step = (span + 63) / 64;
+    const uint32_t c = lo + lane * step;
+    const bool le = lane * step < span && off[c] <= g;
+    const uint32_t k = (uint32_t)__popcll(__ballot(le)) - 1u;  // lane 0's candidate is lo
+    const uint32_t nlo = lo + k * step;
+    span = min(step, lo + span - nlo);
+    lo = nlo;
+  }
+  return lo;
+}
+
 template <int K, int M>
 __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   constexpr int kSpan = kContigTile + 3 * K;
@@ -1368,10 +1388,14 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   const uint64_t base = a.offsets[0], end = base + a.total_bases;
   const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
   const uint32_t nb = a.n_buckets;
-  if (t == 0) {
+  if (wave < 2) {  // wave 0: the tile's first contig (and its offsets), wave 1: its last
     const uint64_t last = r0 + kContigTile < a.total_bases ? r0 + kContigTile : a.total_bases;
-    crange[0] = contig_of(a.offsets, a.n_contig, base + r0);
-    crange[1] = contig_of(a.offsets, a.n_contig, base + last - 1);
+    const uint32_t c = contig_of_wave(a.offsets, a.n_contig, base + (wave ? last - 1 : r0));
+    if (lane == 0) crange[wave] = c;
+    if (wave == 0) {  // offsets c .. c + 64 (clamped): the tile's contigs if they are <= 64
+      offc[lane] = a.offsets[min(c + lane, a.n_contig)];
+      if (lane == 0) offc[kOffCache] = a.offsets[min(c + kOffCache, a.n_contig)];
+    }
   }
   for (int i = t; i < kSpan; i += blockDim.x) {
     const uint64_t g = base + r0 + i;
@@ -1379,8 +1403,6 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   }
   __syncthreads();
   const uint32_t c_lo = crange[0], nc = crange[1] - c_lo + 1;  // contigs meeting the tile
-  if (nc <= (uint32_t)kOffCache)
-    for (uint32_t i = t; i <= nc; i += blockDim.x) offc[i] = a.offsets[c_lo + i];
   for (int i = t; i < kSpan - 2; i += blockDim.x) {
     const uint32_t b0 = bases[i], b1 = bases[i + 1], b2 = bases[i + 2];
     if ((b0 | b1 | b2) & 4u) {
