@@ -23,6 +23,14 @@
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
 
+// KMA_SGPR_CAP builds (A/B): cap the K1 / K12 SGPRs so that the hardware admits as many blocks
+// per CU as the occupancy API reports (it admits ⌊800 / (⌈sgpr/16⌉·16 + 16)⌋ 256-thread blocks).
+#ifdef KMA_SGPR_CAP
+#define KMA_SGPR_ATTR __attribute__((amdgpu_num_sgpr(88)))
+#else
+#define KMA_SGPR_ATTR
+#endif
+
 namespace kma {
 namespace {
 
@@ -449,7 +457,7 @@ __device__ __forceinline__ void probe_span(const ProteinArgs& a, const uint8_t* 
 // K1 kernel (two-kernel form, KMA_FUSED=0): the same loop as probe_span written out in the
 // kernel (the register allocation of the inlined function costs it one wave per SIMD).
 template <int K, int M, int U>
-__global__ __launch_bounds__(256) void probe_quad_kernel(ProteinArgs a) {
+__global__ __launch_bounds__(256) KMA_SGPR_ATTR void probe_quad_kernel(ProteinArgs a) {
   __shared__ uint8_t lut[256];
   __shared__ uint64_t chain_q[4][kChainQ];
   const int t = threadIdx.x, part = t & 3;
@@ -1068,7 +1076,7 @@ __global__ __launch_bounds__(64 * kVoteWaves) void vote_kernel(ProteinArgs a) {
 // set pool share the block's LDS.
 // ---------------------------------------------------------------------------------------------
 template <int K, int M, int P>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(ProteinArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) KMA_SGPR_ATTR void annotate_kernel(ProteinArgs a) {
   constexpr int U = kProbeWin;
   __shared__ uint8_t lut[256];
   __shared__ union Smem {
