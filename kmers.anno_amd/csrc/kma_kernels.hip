@@ -23,9 +23,12 @@
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
 
-// KMA_SGPR_CAP builds (A/B): cap the K1 / K12 SGPRs so that the hardware admits as many blocks
-// per CU as the occupancy API reports (it admits ⌊800 / (⌈sgpr/16⌉·16 + 16)⌋ 256-thread blocks).
-#ifdef KMA_SGPR_CAP
+// K1 / K12 SGPRs are capped so that the hardware admits as many 256-thread blocks per CU as the
+// occupancy API reports and the K1 grid assumes: it admits ⌊800 / (⌈sgpr/16⌉·16 + 16)⌋, so 98
+// SGPRs (uncapped K1) gave 6 blocks where the API said 7 and the "exactly resident" grid had a
+// 1/7 tail. Capped: 86 SGPRs (8 spilled to VGPR lanes, no scratch), 7 blocks; measured c2 K1
+// 47.5 -> 45.1 us, c5 unchanged (KMA_SGPR_UNCAPPED builds restore the old allocation for A/B).
+#ifndef KMA_SGPR_UNCAPPED
 #define KMA_SGPR_ATTR __attribute__((amdgpu_num_sgpr(88)))
 #else
 #define KMA_SGPR_ATTR
