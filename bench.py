@@ -3,16 +3,30 @@
 
 One step = one annotate pass (ProteinKmers extraction + table probe + vote, the loop of
 ApplyKmerProcessor.java:122-147) over one rank's batch of synthetic proteins already resident
-in HBM, through the C ABI's device entry point (libkmeranno.so). The per-function tallies of
-the APPLY report accumulate on device across steps and are reduced to rank 0 over RCCL once,
-inside the timed region (the only exchange step of the path). Scaling is weak: every rank
-annotates its own batch against its replica of the table (built on rank 0, broadcast).
+in HBM, through the C ABI's device entry point (libkmeranno.so: one kernel launch per pass).
+The per-function tallies of the APPLY report accumulate on device across steps and are reduced
+to rank 0 over RCCL once, inside the timed region (the only exchange step of the path).
 
-With --workload c3 one step is one 6-frame pass (KmerReference.java:157-203: translate both
-strands in three frames, skip '*'/'X' windows, probe the table, emit hits in canonical order)
-over a rank's resident synthetic genome (kma_annotate_contigs_device).
+Workloads (BASELINE.json configs; the default is c5, the north-star configuration):
+  c5  1M proteins per rank vs the 10^8-entry table (1.5 GiB: HBM random access). Weak scaling:
+      every rank its own batch, the table built on rank 0 and broadcast (RCCL over xGMI).
+  c2  10k proteins vs the 10^7-entry table (153 MiB: Infinity-Cache resident), weak scaling.
+  c4  ONE 1M-protein batch cut into residue-balanced shards across the ranks (strong
+      scaling), 10^7-entry table replicated.
+  c3  6-frame pass (KmerReference.java:157-203) over a rank's 5 Mbp synthetic genome.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
+Beside the timed steps, rank 0 of a 1-GPU run also reports
+  roofline      the kernel's algorithmic bytes / its hipEvent-timed duration against 8 TB/s,
+                its line-request rate against the random-64-B-gather ceiling measured live on a
+                buffer of the table's size (kma_gather_bench), and the PMC traffic per launch
+                from profiles/ (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, guide corrections);
+  e2e           the host entry point kma_annotate_proteins on the same batch from host memory
+                (H2D + kernel + D2H through pinned staging): the PCIe-inclusive rate;
+  cpu_baseline  the C restatement of the reference loop (oracle/kma_oracle.c) on all the box's
+                host cores (and on one core), on a bounded sample of the same batch and the
+                same full table.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c4]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0.
@@ -22,6 +36,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -38,20 +53,20 @@ from kmeranno import synth  # noqa: E402
 K = 8
 MIN_HITS = 5
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
-BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probe
-# kma_gather_bench, 1.5 GiB buffer, quad shape (profiles/r01_gather_bench.jsonl): random 64-B
-# lines beyond L2 are served at ~5.5e10/s on MI355X.
-GATHER_CEILING_GBS = 3544.2
-# Per-launch HBM traffic of K1 from rocprofv3 FETCH_SIZE + WRITE_SIZE passes (scripts/
-# gpu_traffic.sh), calibrated on the gather bench (scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01c_traffic.json")
+BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probed window
+MALL_BYTES = 256 << 20  # Infinity Cache: a table below it is served on-die (MI355X_MICROARCH.md)
+GATHER_BIN = os.path.join(ROOT, "kmers.anno_amd", "build", "kma_gather_bench")
+# Per-launch PMC traffic of the dominant kernels (scripts/gpu_traffic.sh + traffic_summary.py).
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
+METRIC = "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs roofline"
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
           "8-mer signature table, 1 MI355X per rank",
     "c3": "whole-contig 6-frame DNA->protein kmer annotation: 5 Mbp synthetic genome per rank "
           "(20 contigs, log-uniform 50 kb-1 Mbp, GC 0.5, 0.05% n, genes planted on both strands "
           "over ~50%, code 11) vs 10M-entry protein 8-mer table",
-    "c4": "1M-protein metagenome batch per rank vs 10M-entry table (replicated)",
+    "c4": "one 1M-protein metagenome batch input-sharded across the GPUs (residue-balanced), "
+          "10M-entry table replicated",
     "c5": "1M proteins per rank vs 10^8-entry multi-function signature table "
           "(HBM random access)",
 }
@@ -61,58 +76,85 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sig, residues, offsets, budget_s=10.0):
-    """The C oracle (scalar restatement of ApplyKmerProcessor's table load + loop: chained
-    String hash map + per-protein kmer set) timed on one host core over a bounded sample."""
+def host_threads() -> int:
+    """Threads the CPU baseline may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box; os.cpu_count() shows the whole machine there), else all cores here."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def oracle_table(keys, fids):
     from oracle import c_oracle
     c_oracle.build()
-    n = len(sig.keys)
+    n = len(keys)
     kmers = np.zeros((n, K), np.uint8)
     for j in range(K):
-        kmers[:, j] = ((sig.keys >> np.uint64(5 * (K - 1 - j))) & np.uint64(31)).astype(np.uint8) + 64
+        kmers[:, j] = ((keys >> np.uint64(5 * (K - 1 - j))) & np.uint64(31)).astype(np.uint8) + 64
     t0 = time.perf_counter()
     table = c_oracle.Table.from_buffer(kmers.tobytes(), np.arange(n + 1, dtype=np.uint64) * K,
-                                       sig.fids.astype(np.int32))
-    load_s = time.perf_counter() - t0
+                                       fids.astype(np.int32))
+    return table, time.perf_counter() - t0
+
+
+def cpu_baseline(keys, fids, residues, offsets, budget_s=8.0):
+    """The C oracle (scalar restatement of ApplyKmerProcessor's table load + loop: chained
+    String hash map + per-protein kmer set) over the FULL table, timed on all host cores
+    (pthreads over proteins) and on one core, each on a bounded leading sample of the batch."""
+    from oracle import c_oracle
+    table, load_s = oracle_table(keys, fids)
     lens = np.diff(offsets).astype(np.int64)
-    n_seq, lookups, reps = len(lens), 0, 0
-    # sample: leading proteins of the batch, doubled until the sample takes >= budget/4
-    take = min(n_seq, 500)
-    while True:
-        sub_off = offsets[:take + 1].copy()
-        t0 = time.perf_counter()
-        c_oracle.apply(table, residues, sub_off, K, MIN_HITS, 0)
-        dt = time.perf_counter() - t0
-        if dt >= budget_s / 4 or take == n_seq:
-            break
-        take = min(n_seq, take * 2)
-    wins = int(np.maximum(lens[:take] - K + 1, 0).sum())
-    total_t, reps = 0.0, 0
-    while total_t < budget_s and reps < 20:
-        t0 = time.perf_counter()
-        c_oracle.apply(table, residues, sub_off, K, MIN_HITS, 0)
-        total_t += time.perf_counter() - t0
-        reps += 1
-        lookups += wins
-    return {"value": lookups / total_t, "unit": "kmer lookups/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/kma_oracle.c orc_apply on the first {take} proteins of the rank-0 "
-                      f"batch ({wins} windows) x {reps} reps against the same {n}-entry table "
-                      f"(table load {load_s:.1f}s, untimed)"}
+    n_seq = len(lens)
+    threads = host_threads()
+
+    def rate(nt):
+        take = min(n_seq, 200 * nt)
+        while True:  # grow the sample until one pass takes >= budget / 4
+            sub = offsets[:take + 1].copy()
+            t0 = time.perf_counter()
+            c_oracle.apply_mt(table, residues, sub, K, MIN_HITS, 0, nt)
+            dt = time.perf_counter() - t0
+            if dt >= budget_s / 4 or take == n_seq:
+                break
+            take = min(n_seq, take * 2)
+        wins = int(np.maximum(lens[:take] - K + 1, 0).sum())
+        total, reps = 0.0, 0
+        while total < budget_s and reps < 20:
+            t0 = time.perf_counter()
+            c_oracle.apply_mt(table, residues, sub, K, MIN_HITS, 0, nt)
+            total += time.perf_counter() - t0
+            reps += 1
+        return wins * reps / total, take, wins, reps
+
+    v_all, take, wins, reps = rate(threads)
+    v_one, take1, _, _ = rate(1)
+    return {"value": v_all, "unit": "kmer lookups/s", "cores": threads, "kind": "port",
+            "single_core_value": v_one,
+            "host": {"cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+                     "threads_used": threads},
+            "sample": f"oracle/kma_oracle.c orc_apply_mt ({threads} pthreads over proteins) on "
+                      f"the first {take} proteins of the rank-0 batch ({wins} windows) x {reps} "
+                      f"reps, 1-core figure on the first {take1}; against the same "
+                      f"{len(keys)}-row table (String-keyed chained map, load {load_s:.1f}s, "
+                      f"untimed)"}
 
 
-def cpu_baseline_contigs(wl, budget_s=10.0):
+def cpu_baseline_contigs(wl, budget_s=8.0):
     """The C oracle's 6-frame pass (translate + processKmers window filter + String-keyed map
     probe per window, KmerReference.java:157-203) on one host core, over leading contigs."""
     from oracle import c_oracle
-    c_oracle.build()
-    n = len(wl.keys)
-    kmers = np.zeros((n, K), np.uint8)
-    for j in range(K):
-        kmers[:, j] = ((wl.keys >> np.uint64(5 * (K - 1 - j))) & np.uint64(31)).astype(np.uint8) + 64
-    t0 = time.perf_counter()
-    table = c_oracle.Table.from_buffer(kmers.tobytes(), np.arange(n + 1, dtype=np.uint64) * K,
-                                       wl.fids.astype(np.int32))
-    load_s = time.perf_counter() - t0
+    table, load_s = oracle_table(wl.keys, wl.fids)
     take, total_t, wins, reps = 1, 0.0, 0, 0
     while total_t < budget_s and reps < 50:
         off = wl.offsets[:take + 1].copy()
@@ -125,42 +167,93 @@ def cpu_baseline_contigs(wl, budget_s=10.0):
         if dt < budget_s / 8 and take < wl.n_contig:
             take += 1
     return {"value": wins / total_t, "unit": "kmer lookups/s", "cores": 1, "kind": "port",
+            "host": {"cpu_model": cpu_model(), "os_cpu_count": os.cpu_count()},
             "sample": f"oracle/kma_oracle.c orc_annotate_contigs on leading contigs of the rank-0 "
                       f"genome (1..{take} contigs per rep, {reps} reps, {wins} 6-frame windows) "
-                      f"against the same {n}-entry table (table load {load_s:.1f}s, untimed)"}
+                      f"against the same {len(wl.keys)}-row table (load {load_s:.1f}s, "
+                      f"untimed)"}
+
+
+def gather_ceiling(table_bytes: int):
+    """Random 64-byte line requests per second the chip serves from a buffer of the table's
+    size (kma_gather_bench, quad shape = the probe's; best of 2/4/8 lines in flight), measured
+    now, on this GPU: the request-rate ceiling of the probe. None if the binary is missing."""
+    if not os.path.exists(GATHER_BIN):
+        return None
+    mib = max(1, table_bytes >> 20)
+    best = None
+    for inflight in (2, 4, 8):
+        try:
+            r = subprocess.run([GATHER_BIN, str(mib), "quad", str(inflight)], capture_output=True,
+                               text=True, timeout=120, check=True)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+        except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+            continue
+        if best is None or d["lines_per_s"] > best["lines_per_s"]:
+            best = d
+    return best
+
+
+def pmc_traffic(workload: str, kernel: str):
+    """(traffic bytes per launch, fabric line requests per launch, source) from the committed
+    PMC summary, or (None, None, None)."""
+    try:
+        d = json.load(open(TRAFFIC_FILE))["workloads"][workload][kernel]
+        return d["traffic_bytes"], d.get("read_requests"), os.path.relpath(TRAFFIC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None, None
 
 
 def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
-    """Signature table built on rank 0's GPU, replicated over RCCL (xGMI) to the other ranks."""
+    """Signature table built on rank 0's GPU (size-derived layout; rebuilt flat if the
+    minimizer layout is crowded and flat halves the displaced keys — the library's own
+    creator rule), replicated over RCCL (xGMI) to the other ranks."""
     nb = kmeranno.buckets_for(t_size, load_factor)
-    slots = torch.empty(nb * 8, dtype=torch.int64, device=dev)
+    slots = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int64, device=dev)
+    layout = torch.zeros(1, dtype=torch.int32, device=dev)
     if rank == 0:
-        winner = torch.empty(nb * 8, dtype=torch.int32, device=dev)
+        winner = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int32, device=dev)
         status = torch.zeros(4, dtype=torch.int32, device=dev)
         keys = torch.from_numpy(keys_np.view(np.int64)).to(dev)
         fids = torch.from_numpy(fids_np.view(np.int32)).to(dev)
-        tb = torch.cuda.Event(enable_timing=True)
-        te = torch.cuda.Event(enable_timing=True)
-        tb.record()
-        kmeranno.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
-                              fids.data_ptr(), t_size, status.data_ptr(), sp, k=K)
-        te.record()
-        torch.cuda.synchronize()
-        st = status.cpu().numpy()
-        assert st[0] == 0, "table full"
-        log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 64 / 2**20:.0f} MiB), "
-            f"max probe {st[2]}, built in {tb.elapsed_time(te):.1f} ms")
+
+        def build(m):
+            tb, te = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            tb.record()
+            kmeranno.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
+                                  fids.data_ptr(), len(keys_np), status.data_ptr(), sp, k=K,
+                                  layout=m)
+            te.record()
+            torch.cuda.synchronize()
+            st = status.cpu().numpy().astype(np.int64)
+            assert st[0] == 0, "table full"
+            return st, tb.elapsed_time(te)
+
+        m = kmeranno.layout_for(K, nb)
+        st, ms = build(m)
+        if m and (st[3] > 0.15 * st[1] or st[2] > 32):
+            sf, msf = build(0)
+            if 2 * sf[3] < st[3] or (st[2] > 32 and 2 * sf[2] < st[2]):
+                m, st, ms = 0, sf, msf
+            else:
+                st, ms = build(m)
+        layout.fill_(m)
+        log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 8 * kmeranno.bucket_slots() / 2**20:.0f} MiB), "
+            f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
+            f"built in {ms:.1f} ms")
         del winner, keys, fids
     if world > 1:
         kdist.broadcast_table(slots, src=0)  # RCCL over xGMI
+        dist.broadcast(layout, src=0)
         torch.cuda.synchronize()
-    return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index), slots
+    m = int(layout.item())
+    return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m), slots
 
 
 def timed(step, ws, args, world, stream, dev, before=None, after=None):
     """W warmup steps, then exactly K steps between barrier + synchronize; then the same K steps
-    again with the library's per-phase hipEvents. Max over ranks of (wall s, GPU ms, probe ms
-    per call, rest ms per call)."""
+    again with the library's hipEvents around its kernels. Max over ranks of (wall s, GPU ms,
+    main-kernel ms per call, rest ms per call)."""
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -185,13 +278,41 @@ def timed(step, ws, args, world, stream, dev, before=None, after=None):
     ws.timing(True)
     for _ in range(args.steps):
         step()
-    n_t, probe_ms, rest_ms = ws.timing_read()
+    n_t, kern_ms, rest_ms = ws.timing_read()
     ws.timing(False)
-    stats = torch.tensor([elapsed, gpu_ms, probe_ms / max(n_t, 1), rest_ms / max(n_t, 1)],
+    stats = torch.tensor([elapsed, gpu_ms, kern_ms / max(n_t, 1), rest_ms / max(n_t, 1)],
                          dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
     return stats.tolist()
+
+
+def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
+    """The dominant kernel's line: algorithmic bytes / duration against the 8 TB/s spec, and the
+    line-request rate against the live random-gather ceiling of a buffer of the table's size."""
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic, reqs, src = pmc_traffic(workload, kernel)
+    ceil = gather_ceiling(table_bytes) if live else None
+    out = {"bound": "hbm" if table_bytes > MALL_BYTES else "infinity-cache",
+           "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "
+                              "(MI355X_MICROARCH.md HBM section; Infinity-Cache hits included)")
+           if src else None,
+           "kernel": kernel, "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
+           "alg_bytes_rule": kind, "windows_per_launch": windows,
+           "table_bytes": table_bytes}
+    if ceil:
+        out["measured_random_64B_ceiling"] = {"lines_per_s": ceil["lines_per_s"],
+                                              "GBps": ceil["GBps"], "buffer_MiB":
+                                              ceil["buffer_MiB"], "inflight": ceil["inflight"]}
+        out["windows_per_s_frac_of_ceiling"] = windows / (kernel_ms * 1e-3) / ceil["lines_per_s"]
+        if reqs:
+            rate = reqs / (kernel_ms * 1e-3)
+            out["line_requests_per_launch"] = reqs
+            out["line_requests_per_s"] = rate
+            out["requests_frac_of_ceiling"] = rate / ceil["lines_per_s"]
+    return out
 
 
 def bench_contigs(args, rank, world, dev, stream, sp):
@@ -218,26 +339,15 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                          n_bases, 11, d_hits.data_ptr(), cap, d_nh.data_ptr(),
                                          0, 0, sp)
 
-    elapsed, gpu_ms, k1_ms, rest_ms = timed(step, ws, args, world, stream, dev)
+    elapsed, gpu_ms, k_ms, rest_ms = timed(step, ws, args, world, stream, dev)
     n_hits = int(d_nh.item())
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
         value = n_win * args.steps * world / elapsed
-        # Probe kernel algorithmic bytes: one 64-B bucket per probed window, 1 B per base read,
-        # one 8-B staged record per hit.
-        alg_bytes = n_probe * BYTES_PER_LOOKUP + n_bases + 8 * n_hits
-        achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
         kname = f"contigs_probe_quad_kernel<{K}, {table.info.minimizer_len}>"
-        traffic = None
-        try:
-            traffic = json.load(open(TRAFFIC_FILE))["workloads"]["c3"][kname]["traffic_bytes"]
-        except (OSError, KeyError, ValueError):
-            pass
         out = {
-            "metric": "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs "
-                      "roofline",
-            "value": value, "unit": "kmer lookups/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+            "metric": METRIC, "value": value, "unit": "kmer lookups/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (seeded; SURVEY.md §8(d) config 3 generator)",
             "config": {"workload": f"c3: {WORKLOADS['c3']}", "bases_per_gpu": n_bases,
@@ -248,14 +358,12 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                        "parallelism": f"genome-shard x{world}, table replicated (RCCL broadcast)"},
             "seqs_per_s": n_contig * args.steps * world / elapsed,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"probe": k1_ms, "scan_emit": rest_ms},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": f"{os.path.relpath(TRAFFIC_FILE, ROOT)} (rocprofv3 "
-                                           "FETCH_SIZE + WRITE_SIZE per launch, calibrated)",
-                         "kernel": f"{kname} (6-frame translate + 2 probes per base)",
-                         "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
-                         "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
+            "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
+            # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 8 B per staged hit
+            "roofline": roofline("probed windows x 64 B + bases + hits x 8 B", "c3",
+                                 f"{kname} (6-frame translate + 2 probes per base)", k_ms,
+                                 n_probe * BYTES_PER_LOOKUP + n_bases + 8 * n_hits,
+                                 table.info.bytes, n_probe),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_contigs(wl)
@@ -265,16 +373,30 @@ def bench_contigs(args, rank, world, dev, stream, sp):
     del slots
 
 
+def e2e_host(table, residues, offsets, n_fid, reps=3):
+    """kma_annotate_proteins from host memory (H2D + kernel + D2H through the table's pooled
+    pinned staging): best of `reps` calls after one warmup call, in ms."""
+    kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid)
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid)
+        best = min(best, time.perf_counter() - t0)
+    return best * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
     ap.add_argument("--load-factor", type=float, default=0.5)
     ap.add_argument("--n-seq", type=int, default=0,
                     help="override the workload's proteins per rank (tuning runs only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the gather ceiling and the host-path (e2e) measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -297,13 +419,21 @@ def main():
 
     n_seq, t_size, n_fid, seed = synth.CONFIGS[args.workload]
     n_seq = args.n_seq or n_seq
+    strong = args.workload == "c4"
     t0 = time.perf_counter()
-    sig = synth.make_table(t_size, n_fid, seed, K)
-    residues, offsets, _, _ = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17 + rank)
+    sig = synth.make_table(t_size, n_fid, seed, K, protos_only=rank != 0)
+    qseed = seed * 1_000_003 + 17 + (0 if strong else rank)
+    residues, offsets, _, _ = synth.make_queries(sig, n_seq, qseed)
+    batch_windows = int(np.maximum(np.diff(offsets).astype(np.int64) - K + 1, 0).sum())
+    batch_seqs = len(offsets) - 1
+    lo = 0
+    if strong:  # this rank's residue-balanced contiguous shard of the one batch
+        residues, offsets, lo = kdist.shard(residues, offsets, world, rank)
+    n_seq = len(offsets) - 1
     lens = np.diff(offsets).astype(np.int64)
     n_win = int(np.maximum(lens - K + 1, 0).sum())
-    log(f"[rank {rank}] workload {args.workload}: {t_size} table rows, {n_seq} proteins, "
-        f"{n_win} windows, generated in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] workload {args.workload}: {t_size} table rows, {n_seq} proteins "
+        f"(from {lo}), {n_win} windows, generated in {time.perf_counter() - t0:.1f}s")
     table, slots = build_table(sig.keys, sig.fids, t_size, args.load_factor, dev, sp, rank, world)
     n_res = int(offsets[-1] - offsets[0])
     ws = kmeranno.Workspace(local, n_res)
@@ -322,72 +452,51 @@ def main():
 
     # per-function tallies of the whole job -> rank 0, inside the timed region
     reduce = (lambda: kdist.reduce_tallies(d_tally, dst=0)) if world > 1 else None
-    elapsed, gpu_ms, k1_ms, k2_ms = timed(step, ws, args, world, stream, dev,
-                                        before=d_tally.zero_, after=reduce)
-
-    fused = ws.protein_form(n_seq) == 1
+    elapsed, gpu_ms, k_ms, _ = timed(step, ws, args, world, stream, dev, before=d_tally.zero_,
+                                     after=reduce)
     st = d_st.cpu().numpy()
     called = int((st == kmeranno.STATUS_CALLED).sum())
     if rank == 0:
-        total_lookups = n_win * args.steps * world
+        total_lookups = (batch_windows if strong else n_win * world) * args.steps
         value = total_lookups / elapsed
-        seqs_per_s = n_seq * args.steps * world / elapsed
-        n_pos = max(n_res - K + 1, 0)
-        # K1 algorithmic bytes per launch: one 64-B bucket line + the 4-B result word per residue
-        # position probed, + 1 B per residue streamed in.
-        alg_bytes = n_pos * (BYTES_PER_LOOKUP + 4) + n_res
-        achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
-        m = table.info.minimizer_len
-        if fused:
-            k1_name = f"annotate_kernel<{K}, {m}, 4>"
-        else:
-            k1_name = os.environ.get("KMA_PROBE", "quad")
-            k1_name = {"lane": "probe_kernel", "run": "probe_run_kernel"}.get(
-                k1_name, "probe_quad_kernel")
-            k1_name = f"{k1_name}<{K}, {m}, 3>"
-        traffic = None
-        try:
-            tr = json.load(open(TRAFFIC_FILE))["workloads"][args.workload][k1_name]
-            traffic = tr["traffic_bytes"]
-        except (OSError, KeyError, ValueError):
-            pass
+        seqs = batch_seqs if strong else n_seq * world
+        kname = f"annotate_kernel<{K}, {table.info.minimizer_len}, 4>"
         out = {
-            "metric": "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs "
-                      "roofline",
-            "value": value,
-            "unit": "kmer lookups/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
+            "metric": METRIC, "value": value, "unit": "kmer lookups/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (seeded; SURVEY.md §8(d) generator)",
             "config": {"workload": f"{args.workload}: {WORKLOADS[args.workload]}",
                        "proteins_per_gpu": n_seq, "windows_per_gpu": n_win,
+                       "batch_windows": batch_windows if strong else n_win * world,
                        "table_entries": t_size, "functions": n_fid, "k": K,
                        "load_factor": args.load_factor, "min_hits": MIN_HITS,
-                       "parallelism": f"input-shard x{world}, table replicated (RCCL broadcast), "
-                                      "tally reduce (RCCL)"},
-            "seqs_per_s": seqs_per_s,
+                       "table_layout_m": table.info.minimizer_len,
+                       "parallelism": (f"input-shard x{world} of one batch" if strong else
+                                       f"input-shard x{world}") +
+                                      ", table replicated (RCCL broadcast), tally reduce (RCCL)"},
+            "seqs_per_s": seqs * args.steps / elapsed,
             "called_per_batch": called,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": ({"probe_vote_K12": k1_ms, "vote_long": k2_ms} if fused else
-                          {"probe_K1": k1_ms, "vote_K2": k2_ms}),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": f"{os.path.relpath(TRAFFIC_FILE, ROOT)} (rocprofv3 "
-                                           "FETCH_SIZE + WRITE_SIZE per launch, calibrated)",
-                         "kernel": f"{k1_name} " + ("(K12: every window's bucket gather + the "
-                                                    "vote, fused)" if fused else
-                                                    "(K1: every window's bucket gather)"),
-                         "kernel_ms": k1_ms, "alg_bytes_per_launch": alg_bytes,
-                         "measured_random_64B_ceiling_GBps": GATHER_CEILING_GBS},
+            "phases_ms": {"annotate_kernel": k_ms},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(sig, residues, offsets)
+        # one 64-B bucket line per probed window + 1 B per residue streamed in;
+        # rank 0's shard (the kernel time is the max over ranks)
+        out["roofline"] = roofline("windows x 64 B + residues", args.workload,
+                                   kname + " (the whole protein path: probe + sets + vote)",
+                                   k_ms, n_win * BYTES_PER_LOOKUP + n_res, table.info.bytes,
+                                   n_win, live=not args.no_extras)
+        if world == 1:
+            if not args.no_extras:
+                ms = e2e_host(table, residues, offsets, n_fid)
+                out["e2e_host_call"] = {
+                    "entry": "kma_annotate_proteins (host buffers: pinned staging, H2D, kernel, "
+                             "D2H, on the table's pooled stream)",
+                    "ms": ms, "lookups_per_s": n_win / (ms * 1e-3),
+                    "seqs_per_s": n_seq / (ms * 1e-3)}
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(sig.keys, sig.fids, residues, offsets)
         print(json.dumps(out), flush=True)
     ws.close()
     table.close()

@@ -14,6 +14,9 @@
  *   - the 6-frame contig kmer extractor
  *       proteins/kmers/KmerReference.java:157-203, KmerPosition.java:50-93
  *                                                              -> kma_annotate_contigs*
+ *   - ProteinKmers.distance of the gene-copy command
+ *       genome/compare/GeneCopyProcessor.java:129-162          -> kma_protein_distances,
+ *                                                                 kma_protein_best_match
  *
  * A Java host would bind these through one JNI class; the C++ CLI under
  * kmers.anno_amd/host and the Python ctypes module under kmers.anno_amd/python bind them
@@ -26,8 +29,14 @@
  *   - "Host" entry points take host buffers owned by the caller and are synchronous.
  *     "_device" entry points take device buffers on the table's device and are asynchronous
  *     on the given stream; they never allocate, free or synchronise (graph-capturable).
- *   - A table is immutable after creation; concurrent annotate calls on one table are
- *     allowed as long as each uses its own kma_workspace.
+ *   - A table is immutable after creation (replicas aside); concurrent annotate calls on one
+ *     table are allowed. Host entry points take a per-device context (stream, workspace,
+ *     pinned staging) from the table's pool for the call and wait on that stream only;
+ *     _device calls must each use their own kma_workspace.
+ *   - A table may hold replicas on several devices (kma_table_create_replicated /
+ *     kma_table_replicate): host entry points then cut a batch into residue- (base-) balanced
+ *     contiguous shards, one host thread per replica, and sum the tallies; _device calls use
+ *     the replica on their workspace's device.
  */
 #ifndef KMERANNO_H
 #define KMERANNO_H
@@ -39,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 1
+#define KMA_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -62,7 +71,8 @@ extern "C" {
 #define KMA_STATUS_CALLED 1
 #define KMA_STATUS_AMBIGUOUS 2
 #define KMA_STATUS_BELOW_MIN 3
-#define KMA_STATUS_TOO_LONG 4 /* protein beyond the dedupe capacity (> 2^17 windows); fid -1 */
+/* (ABI 1 had KMA_STATUS_TOO_LONG = 4 for proteins beyond 2^16 windows; every protein length
+ * is voted exactly since ABI 2.)                                                              */
 
 /* ---- extraction flags (kma_annotate_proteins*) ---------------------------------------------
  * Default (0) is the restatement of org.theseed.sequence.ProteinKmers used by `apply`: the SET
@@ -83,6 +93,7 @@ extern "C" {
 #define KMA_MAX_K 8
 #define KMA_MAX_FID ((1u << 23) - 1u)
 
+
 typedef struct kma_table kma_table;         /* opaque: a signature table resident on one GPU */
 typedef struct kma_workspace kma_workspace; /* opaque: per-stream scratch for _device calls  */
 
@@ -90,14 +101,18 @@ typedef struct kma_table_info {
   uint64_t n_rows;       /* rows passed to create                                          */
   uint64_t n_skipped;    /* rows whose kmer length != K (can never match; still "loaded")  */
   uint64_t n_entries;    /* distinct keys stored (duplicates resolved last-wins)           */
-  uint64_t n_buckets;    /* 64-byte buckets of 8 slots                                     */
-  uint64_t bytes;        /* device bytes of the slot array = n_buckets * 64                */
+  uint64_t n_buckets;    /* buckets of kma_bucket_slots() 8-byte slots                     */
+  uint64_t bytes;        /* device bytes of the slot array = n_buckets * slots * 8          */
   int32_t k;             /* kmer length                                                    */
   int32_t device;        /* HIP device ordinal                                             */
   uint32_t max_probe;    /* longest bucket chain a stored key needs (1 = home bucket)      */
   uint32_t n_extra_syms; /* bytes mapped to codes 28..31                                   */
   uint8_t extra_syms[4];
-  int32_t minimizer_len; /* m: a key's home bucket is a hash of its minimizer m-mer        */
+  int32_t minimizer_len; /* layout: a key's home bucket is a hash of its minimizer m-mer;
+                            0 = flat (hash of the whole key)                               */
+  uint64_t n_displaced;  /* keys stored past their home bucket (overflow chains)            */
+  int32_t n_replicas;    /* devices holding a copy of the slot array                        */
+  int32_t reserved;
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -136,44 +151,63 @@ int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t
                             int device, double load_factor, kma_table** out);
 int kma_table_info_get(const kma_table* table, kma_table_info* out);
 int kma_table_destroy(kma_table* table);
+/* u64 slots per bucket of this build: 8 (64-byte buckets, the default) or 16 (128-byte). */
+int kma_bucket_slots(void);
+/* The table's layout choice: minimizer layouts (m = min(K,6) up to 2^22 buckets, else
+ * min(K,7)); when more than 15% of the keys land past their home bucket or a chain exceeds 32
+ * buckets (keys that pile onto few minimizers), the creators above also build the table flat
+ * (layout 0) and keep it if it halves the displaced keys or the longest chain.
+ * kma_table_layout_for gives the size-derived layout (KMA_MINIMIZER=0|6|7 in the environment
+ * forces one).                                                                                */
+int kma_table_layout_for(int k, uint64_t n_buckets);
+
+/* ---- replicas (the table replicated on every device of the node) -------------
+ * kma_table_create_replicated: kma_table_create on device_ids[0], then kma_table_replicate on
+ * the others. kma_table_replicate: copy replica 0's slot array to each listed device (a peer
+ * copy over xGMI between MI355X GPUs; a device may be listed twice — two replicas on one GPU,
+ * each served by its own host thread and stream). kma_table_replicas: the replica count and
+ * (up to cap) their devices, in shard order.                                                  */
+int kma_table_create_replicated(const char* text, const uint64_t* offsets, const uint32_t* fids,
+                                uint64_t n, int k, int n_devices, const int* device_ids,
+                                double load_factor, kma_table** out);
+int kma_table_replicate(kma_table* table, int n_devices, const int* device_ids);
+int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap);
 
 /* Device-resident construction for hosts that own device memory (e.g. a torch allocation
  * that is later broadcast over RCCL to the other GPUs of the node).
  *   kma_table_buckets_for : bucket count for n keys at the load factor
- *   kma_table_build_device: d_slots (n_buckets*64 bytes) and d_winner (n_buckets*8 u32) are
- *                           caller scratch; keys/fids are device arrays of K-mers (the layout
- *                           depends on K); builds on `stream`; d_status (4 u32) receives
- *                           {table full, entries, max probe}; fids are masked to 23 bits.
- *   kma_table_wrap_device : adopt an already-built slot array (not owned, not freed).        */
+ *   kma_table_build_device: d_slots (n_buckets * S * 8 bytes) and d_winner (n_buckets * S u32,
+ *                           S = kma_bucket_slots()) are
+ *                           caller scratch; keys/fids are device arrays of K-mers; layout -1 =
+ *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7); builds on
+ *                           `stream`; d_status (4 u32) receives {table full, entries, longest
+ *                           chain, displaced keys} (a caller may rebuild with layout 0 when
+ *                           displaced keys are many); fids are masked to 23 bits.
+ *   kma_table_wrap_device : adopt an already-built slot array of that layout (not owned).    */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
-int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
-                           const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
-                           uint32_t* d_status, void* stream);
-int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device,
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
+                           uint32_t* d_winner, const uint64_t* d_keys, const uint32_t* d_fids,
+                           uint64_t n, uint32_t* d_status, void* stream);
+int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, int device,
                           kma_table** out);
 /* Raw view of the slot array (device pointer) — what an RCCL broadcast moves.               */
 int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes);
 
 /* ---- workspaces -----------------------------------------------------------------------------
  * Per-stream scratch of the _device entry points. kma_workspace_reserve sizes it for calls of
- * up to n_residues residues (8 bytes per residue of HBM: K1 words and slot ids); it is the
- * only call that allocates.                                                                  */
+ * up to n_residues residues (< 2^32 - 128; 8 bytes per residue of HBM: the distinct-kmer sets
+ * of proteins too long for the kernel's LDS); it is the only call that allocates.            */
 int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_destroy(kma_workspace* ws);
-/* Per-phase device timing of the _device calls made with this workspace: with enable = 1 each
- * call records hipEvents on its stream around the probe phase (every window's table lookup)
- * and the vote phase (set semantics + vote; for kma_annotate_contigs_device: scan + emit). Not for graph capture. _read synchronises on
- * the recorded events (the last 256 calls), returns their count and summed milliseconds, and
- * clears the accumulators.                                                                  */
+/* Device timing of the _device calls made with this workspace: with enable = 1 each call
+ * records hipEvents on its stream around its main kernel (proteins: the whole path in one
+ * kernel; contigs: the 6-frame probe) and the rest (contigs: scan + emit; proteins: nothing).
+ * Not for graph capture. _read synchronises on the recorded events (the last 256 calls),
+ * returns their count and summed milliseconds, and clears the accumulators.                  */
 int kma_workspace_timing(kma_workspace* ws, int enable);
-/* Which kernel form kma_annotate_proteins_device uses for a batch of n_seq proteins on this
- * workspace's device: 1 = the fused probe + vote kernel (large batches), 0 = the two-kernel
- * probe / vote pipeline (small batches, where the vote cannot hide behind other blocks'
- * gathers). KMA_FUSED=0|1 in the environment forces one form. For reports and tuning.       */
-int kma_protein_form(const kma_workspace* ws, uint32_t n_seq);
-int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* probe_ms,
-                              double* vote_ms);
+int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
+                              double* rest_ms);
 
 /* ---- protein annotation (ApplyKmerProcessor.java:118-148) ----------------------------------
  * residues: raw ASCII proteins concatenated; sequence s is residues[offsets[s]..offsets[s+1]).
@@ -184,10 +218,10 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                           uint32_t* out_tally, uint32_t n_fid);
-/* Device form: every pointer is device memory on the table's device; `d_residues` is 8-byte
- * aligned and readable for 32 bytes past offsets[n_seq]; n_residues = offsets[n_seq] -
- * offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is accumulated into, not
- * cleared. Asynchronous on `stream`.                                                          */
+/* Device form: every pointer is device memory on the workspace's device (the table has a
+ * replica there); `d_residues` is 8-byte aligned and readable for 32 bytes past offsets[n_seq]; n_residues =
+ * offsets[n_seq] - offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is
+ * accumulated into, not cleared. One kernel launch, asynchronous on `stream`.                */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
                                  uint32_t n_seq, uint64_t n_residues, int min_hits,
@@ -252,6 +286,28 @@ int kma_connect_pegs(const kma_table* peg_table, const uint8_t* dna, const uint6
 int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const int32_t* roles,
                          uint32_t n_seq, int k, uint32_t flags, int device, uint64_t* out_keys,
                          uint32_t* out_roles, uint64_t cap, uint64_t* n_out);
+
+/* ---- ProteinKmers.distance (genome/compare/GeneCopyProcessor.java:129-162) -----------------
+ * One batch of proteins (residues, offsets, n_seq); pair i compares proteins pair_a[i] and
+ * pair_b[i]. Sets are ProteinKmers of kmer size k (2..12, GeneCopyProcessor -K): the distinct
+ * substrings at i = 0 .. L-k (KMA_F_END_EXCLUSIVE: i < L-k). out_sim[i] = |A n B|; out_size
+ * (optional, n_seq) = |S| of every protein; out_dist (optional) = 1 - |A n B| / |A u B| in
+ * double, 1.0 when the sets share nothing (SequenceKmers.distance, external, restated).
+ * KMA_E_ALPHABET if a window holds a byte outside A-Z / '*'. Runs on the device: window keys,
+ * segmented radix sort per protein, a binary-search intersection per pair; synchronous.     */
+int kma_protein_distances(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq, int k,
+                          uint32_t flags, const uint32_t* pair_a, const uint32_t* pair_b,
+                          uint64_t n_pairs, int device, uint32_t* out_sim, uint32_t* out_size,
+                          double* out_dist);
+/* GeneCopyProcessor's choice (:135-146) for n_query queries: query[q] against the candidates
+ * cand[cand_off[q] .. cand_off[q+1]) in order, starting from fDist = max_dist, keeps the LAST
+ * candidate with distance <= the running best (`f2Dist <= fDist`). out_best[q] = that
+ * candidate's protein index or -1; out_best_dist[q] (optional) = its distance (max_dist if
+ * none).                                                                                      */
+int kma_protein_best_match(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq, int k,
+                           uint32_t flags, const uint32_t* query, const uint64_t* cand_off,
+                           const uint32_t* cand, uint32_t n_query, double max_dist, int device,
+                           int32_t* out_best, double* out_best_dist);
 
 /* Window count of the 6-frame extractor before the '*'/'X' filter (for throughput metrics).  */
 uint64_t kma_contig_window_count(const uint64_t* offsets, uint32_t n_contig, int k);

@@ -1,8 +1,13 @@
 // gather_bench.hip — measured random-access roofline for the signature-table probe
 // (SURVEY.md §8(d)): GUPS-style reads of 64-byte lines at uniformly random line indices of a
-// buffer of a given size. Two access shapes:
-//   lane  — one lane reads a whole line (4 x dwordx4, the K1 probe shape),
-//   quad  — four adjacent lanes read one line together (one dwordx4 each),
+// buffer of a given size. Three access shapes:
+//   lane  — one lane reads a whole line (4 x dwordx4),
+//   quad  — four adjacent lanes read one line together (one dwordx4 each: the probe shape),
+//   oct   — eight adjacent lanes read one aligned 128-byte line (one dwordx4 each): is a
+//           128-byte bucket as cheap as a 64-byte one at the memory side (128-B L2 lines)?
+//   quad2 — four adjacent lanes read one 128-byte line as two 64-byte halves (two dwordx4
+//           each, one instruction per half),
+//   hex   — sixteen adjacent lanes read one aligned 256-byte span (one dwordx4 each).
 // with `inflight` independent lines per lane (lane) or per quad (quad) before any is consumed,
 // plain or non-temporal loads, and `bpc` resident 256-thread blocks per CU.
 //
@@ -86,6 +91,67 @@ __global__ __launch_bounds__(256) void gather_quad(const uint4* __restrict__ buf
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+template <int I, bool NT>
+__global__ __launch_bounds__(256) void gather_oct(const uint4* __restrict__ buf, uint32_t n_lines,
+                                                  uint32_t* __restrict__ sink, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t oct = tid >> 3, part = tid & 7;
+  const uint32_t n128 = n_lines / 2;
+  uint32_t acc = 0;
+  for (int r = 0; r < kSteps; r += I) {
+    uint4 v[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const uint32_t line = (uint32_t)(((uint64_t)mix32(oct * 0x9E3779B1u + (r + j) * 0x85EBCA77u + salt) * n128) >> 32);
+      v[j] = ld<NT>(buf + (uint64_t)line * 8 + part);
+    }
+#pragma unroll
+    for (int j = 0; j < I; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int I, bool NT>
+__global__ __launch_bounds__(256) void gather_quad2(const uint4* __restrict__ buf, uint32_t n_lines,
+                                                    uint32_t* __restrict__ sink, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t quad = tid >> 2, part = tid & 3;
+  const uint32_t n128 = n_lines / 2;
+  uint32_t acc = 0;
+  for (int r = 0; r < kSteps; r += I) {
+    uint4 v[I][2];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const uint32_t line = (uint32_t)(((uint64_t)mix32(quad * 0x9E3779B1u + (r + j) * 0x85EBCA77u + salt) * n128) >> 32);
+      v[j][0] = ld<NT>(buf + (uint64_t)line * 8 + part);
+      v[j][1] = ld<NT>(buf + (uint64_t)line * 8 + 4 + part);
+    }
+#pragma unroll
+    for (int j = 0; j < I; ++j) acc ^= v[j][0].x ^ v[j][1].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int I, bool NT>
+__global__ __launch_bounds__(256) void gather_hex(const uint4* __restrict__ buf, uint32_t n_lines,
+                                                  uint32_t* __restrict__ sink, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t hex = tid >> 4, part = tid & 15;
+  const uint32_t n256 = n_lines / 4;
+  uint32_t acc = 0;
+  for (int r = 0; r < kSteps; r += I) {
+    uint4 v[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const uint32_t line = (uint32_t)(((uint64_t)mix32(hex * 0x9E3779B1u + (r + j) * 0x85EBCA77u + salt) * n256) >> 32);
+      v[j] = ld<NT>(buf + (uint64_t)line * 16 + part);
+    }
+#pragma unroll
+    for (int j = 0; j < I; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <class F>
 double time_kernel(F launch, double bytes) {
   hipEvent_t a, b;
@@ -108,11 +174,13 @@ double time_kernel(F launch, double bytes) {
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    std::fprintf(stderr, "usage: %s <buffer_MiB> <lane|quad> <inflight> [nt] [bpc]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s <buffer_MiB> <lane|quad|oct> <inflight> [nt] [bpc]\n",
+                 argv[0]);
     return 1;
   }
   const uint64_t mib = std::strtoull(argv[1], nullptr, 10);
-  const bool quad = !std::strcmp(argv[2], "quad");
+  const bool quad = !std::strcmp(argv[2], "quad"), oct = !std::strcmp(argv[2], "oct");
+  const bool quad2 = !std::strcmp(argv[2], "quad2"), hex = !std::strcmp(argv[2], "hex");
   const int inflight = std::atoi(argv[3]);
   const bool nt = argc > 4 && std::atoi(argv[4]);
   const int bpc = argc > 5 ? std::atoi(argv[5]) : 8;
@@ -126,19 +194,23 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(buf, 1, bytes));
   const uint32_t n_lines = (uint32_t)(bytes / 64);
   const int blocks = n_cu * bpc;
-  const double lines = (double)blocks * 256 * kSteps / (quad ? 4 : 1);
+  // requests (lines of the shape's size: 128 B for oct, else 64 B)
+  const double lines =
+      (double)blocks * 256 * kSteps / (hex ? 16 : oct ? 8 : (quad || quad2) ? 4 : 1);
+  const double line_bytes = hex ? 256 : (oct || quad2) ? 128 : 64;
   double gbs = 0;
 #define RUN(KERNEL, I, NTV)                                                                   \
   gbs = time_kernel([&](uint32_t salt) {                                                      \
     hipLaunchKernelGGL((KERNEL<I, NTV>), dim3(blocks), dim3(256), 0, 0, buf, n_lines, sink,   \
                        salt);                                                                 \
-  }, lines * 64)
+  }, lines * line_bytes)
 #define CASES(KERNEL)                                           \
   if (inflight == 1) { if (nt) RUN(KERNEL, 1, true); else RUN(KERNEL, 1, false); } \
   else if (inflight == 2) { if (nt) RUN(KERNEL, 2, true); else RUN(KERNEL, 2, false); } \
   else if (inflight == 4) { if (nt) RUN(KERNEL, 4, true); else RUN(KERNEL, 4, false); } \
   else if (inflight == 8) { if (nt) RUN(KERNEL, 8, true); else RUN(KERNEL, 8, false); }
-  if (quad) { CASES(gather_quad) } else { CASES(gather_lane) }
+  if (hex) { CASES(gather_hex) } else if (quad2) { CASES(gather_quad2) }
+  else if (oct) { CASES(gather_oct) } else if (quad) { CASES(gather_quad) } else { CASES(gather_lane) }
   if (gbs == 0) {
     std::fprintf(stderr, "unsupported inflight %d\n", inflight);
     return 1;
@@ -146,8 +218,9 @@ int main(int argc, char** argv) {
   std::printf("{\"buffer_MiB\": %llu, \"shape\": \"%s\", \"inflight\": %d, \"nt\": %d, "
               "\"blocks_per_cu\": %d, \"GBps\": %.1f, \"lines_per_s\": %.4g, "
               "\"lines_per_launch\": %.0f}\n",
-              (unsigned long long)mib, quad ? "quad" : "lane", inflight, (int)nt, bpc, gbs,
-              gbs * 1e9 / 64, lines);
+              (unsigned long long)mib,
+              hex ? "hex" : quad2 ? "quad2" : oct ? "oct" : quad ? "quad" : "lane", inflight, (int)nt,
+              bpc, gbs, gbs * 1e9 / line_bytes, lines);
   CHECK(hipFree(buf));
   return 0;
 }

@@ -1,102 +1,59 @@
 // kma_abi.cpp — the C ABI of libkmeranno.so (declared in include/kmeranno.h).
 //
 // Host-side orchestration only: argument checks, key packing, device allocation and copies,
-// and kernel launches (kma_kernels.hip). No compute falls back to the CPU: without a usable
-// HIP device every entry point that needs one returns KMA_E_DEVICE.
+// replica management and kernel launches (kma_kernels.hip). No compute falls back to the CPU:
+// without a usable HIP device every entry point that needs one returns KMA_E_DEVICE.
+//
+// Host entry points (kma_annotate_proteins / kma_annotate_contigs) reuse per-table host
+// contexts — a stream, a workspace, device buffers and pinned staging buffers per device —
+// taken from the table's pool for the duration of one call, so a per-genome caller pays no
+// allocation and concurrent callers never synchronise each other (each waits on its own
+// stream only). A table may be replicated on several devices; a host call then cuts its batch
+// into residue-balanced contiguous shards, one host thread per replica.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/kmeranno.h"
+#include "kma_distance.h"
 #include "kma_internal.h"
 
+namespace {
+// KMA_MINIMIZER=0|6|7 forces a table layout (tests run every layout in one process, so the
+// variable is read per table, not cached). -1 = not forced.
+int forced_layout() {
+  const char* e = getenv("KMA_MINIMIZER");
+  if (!e || !*e) return -1;
+  const int v = atoi(e);
+  return (v == 0 || v == 6 || v == 7) ? v : -1;
+}
+}  // namespace
+
 int kma::minimizer_len(int k, uint64_t n_buckets) {
-  static const int forced = [] {
-    const char* e = getenv("KMA_MINIMIZER");
-    return e ? atoi(e) : 0;
-  }();
   const int m6 = k < 6 ? k : 6, m7 = k < 7 ? k : 7;
-  if (forced == 6) return m6;
-  if (forced == 7) return m7;
-  return n_buckets <= (1ull << 22) ? m6 : m7;
-}
-
-constexpr uint64_t kHitsPad = 64;
-// A protein goes to vote_long_kernel only if its set needs more than K2's LDS gives one
-// protein (>= 3/4 kWaveSet - 256, resp. > kVotePool / 2 hits), so it has more than 128 windows.
-static_assert(kma::kWaveSet >= 512 && kma::kVotePool >= 256, "pending list bound");
-// Two lists of up to n_residues / 128 + 32 records each (a list entry has > 128 windows).
-uint64_t pending_cap(uint64_t n_residues) { return 2 * (n_residues / 128 + 32); }
-
-struct kma_table {
-  int device = 0;
-  int k = 8;
-  int mlen = 6;  // minimizer length of the layout (kma::minimizer_len)
-  uint64_t n_buckets = 0;
-  uint64_t* d_slots = nullptr;
-  bool owned = false;
-  uint8_t* d_lut = nullptr;
-  uint8_t lut[256] = {};
-  kma_table_info info = {};
-};
-
-struct kma_workspace {
-  int device = 0;
-  int n_cu = 256;
-  uint32_t* d_flag = nullptr;
-  uint64_t* d_scratch = nullptr;
-  uint32_t* d_hits = nullptr;  // K1 words (fid + 1), then K1 slot ids: u32 per residue each
-  kma::PendingRec* d_pending = nullptr;  // K2 -> vote_long list (> 128 windows each)
-  uint64_t hits_cap = 0;
-  // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
-  uint64_t* d_cstage = nullptr;
-  uint32_t* d_ccounts = nullptr;
-  uint64_t* d_cprefix = nullptr;
-  void* d_ctemp = nullptr;
-  size_t ctemp_bytes = 0;
-  uint64_t contig_cap = 0;  // bases
-  // Segmented overlap: K2 of segment i on `side` while K1 of segment i + 1 runs on the call's
-  // stream (fork/join through events, graph-capturable).
-  hipStream_t side = nullptr;
-  std::vector<hipEvent_t> seg_ev;  // fork, per-segment K1 done, join
-  // Per-phase timing (kma_workspace_timing): a ring of (start, after K1, end) event triples.
-  bool timing = false;
-  std::vector<hipEvent_t> events;
-  uint32_t n_timed = 0;
-};
-constexpr uint32_t kTimingRing = 256;
-constexpr int kMaxSegments = 8;
-
-// Segments per call (K2 of a segment may run beside K1 of the next); KMA_SEGMENTS overrides.
-int segments_for(uint32_t n_seq) {
-  static const int forced = [] {
-    const char* e = getenv("KMA_SEGMENTS");
-    return e ? atoi(e) : 0;
-  }();
-  // Measured on MI355X (r01): K1 fills every CU, so K2 on the side stream does not overlap it
-  // and each extra segment adds a K1 ramp; default 1.
-  int s = forced > 0 ? forced : 1;
-  return std::max(1, std::min(s, std::min<int>(kMaxSegments, (int)std::max<uint32_t>(1, n_seq))));
-}
-
-// Protein path form: the fused probe + vote kernel K12 for batches of at least
-// kma::fused_min_proteins proteins, else the two-kernel K1 / K2 pipeline. KMA_FUSED=1 / 0
-// forces one form (A/B runs; segmented overlap and the K1/K2 variants need the two-kernel form).
-bool fused_form(uint32_t n_seq, int n_cu) {
-  const char* e = getenv("KMA_FUSED");  // read per call: tests switch forms in one process
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-  return n_seq >= kma::fused_min_proteins(n_cu);
+  const int f = forced_layout();
+  if (f == 0) return 0;
+  if (f == 6) return m6;
+  if (f == 7) return m7;
+  return n_buckets <= kma::kMinimizer6Buckets ? m6 : m7;
 }
 
 namespace {
+
+constexpr uint64_t kResPad = 64;            // workspace positions past the last residue
+constexpr uint64_t kMaxResidues = (1ull << 32) - 2 * kResPad;  // positions are u32 in kernels
+using kma::kMaxBuckets;
+constexpr uint32_t kTimingRing = 256;
 
 thread_local std::string g_err;
 
@@ -131,7 +88,7 @@ struct DeviceScope {
   }
 };
 
-// Device buffers freed on scope exit (host entry points only).
+// Device buffers freed on scope exit (one-shot builders only).
 struct DevBufs {
   std::vector<void*> p;
   ~DevBufs() {
@@ -144,6 +101,48 @@ struct DevBufs {
     if (e == hipSuccess) p.push_back(q);
     *out = static_cast<T*>(q);
     return e;
+  }
+};
+
+// A device buffer that only grows (host contexts).
+template <class T>
+struct Grow {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t reserve(size_t n) {
+    if (p && n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n + n / 4, 256);
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+// Pinned host staging that only grows.
+struct Pinned {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (p && n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n + n / 4, 4096);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
   }
 };
 
@@ -215,42 +214,193 @@ const char* ncbi_code(int gc) {
   }
 }
 
-int make_table_object(int device, int k, uint64_t n_buckets, uint64_t* d_slots, bool owned,
-                      const uint8_t lut[256], kma_table** out) {
-  kma_table* t = new kma_table();
-  t->device = device;
-  t->k = k;
-  t->mlen = kma::minimizer_len(k, n_buckets);
-  t->n_buckets = n_buckets;
-  t->d_slots = d_slots;
-  t->owned = owned;
-  std::memcpy(t->lut, lut, 256);
-  hipError_t e = hipMalloc(&t->d_lut, 256);
-  if (e == hipSuccess) e = hipMemcpy(t->d_lut, lut, 256, hipMemcpyHostToDevice);
+// Contiguous shards [b[i], b[i+1]) of n units (proteins, contigs) with near-equal payload
+// (residues, bases): cut where the payload prefix crosses i/parts of the total.
+std::vector<uint32_t> shard_bounds(const uint64_t* off, uint32_t n, int parts) {
+  std::vector<uint32_t> b(parts + 1, 0);
+  b[parts] = n;
+  const uint64_t base = off[0], total = off[n] - base;
+  for (int i = 1; i < parts; ++i) {
+    const uint64_t target = base + (uint64_t)((double)total * i / parts);
+    const uint64_t* it = std::lower_bound(off + 1, off + n + 1, target);
+    b[i] = std::max(b[i - 1], std::min(n, (uint32_t)(it - off)));
+  }
+  return b;
+}
+
+}  // namespace
+
+// ---- objects ---------------------------------------------------------------------------------
+struct kma_workspace {
+  int device = 0;
+  int n_cu = 256;
+  uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
+  uint64_t res_cap = 0;        // residues per call
+  // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
+  uint64_t* d_cstage = nullptr;
+  uint32_t* d_ccounts = nullptr;
+  uint64_t* d_cprefix = nullptr;
+  void* d_ctemp = nullptr;
+  size_t ctemp_bytes = 0;
+  uint64_t contig_cap = 0;  // bases
+  // Per-phase timing (kma_workspace_timing): a ring of (start, after the main kernel, end).
+  bool timing = false;
+  std::vector<hipEvent_t> events;
+  uint32_t n_timed = 0;
+};
+
+namespace {
+// One replica of a table's slot array on one device.
+struct Replica {
+  int device = 0;
+  uint64_t* d_slots = nullptr;
+  bool owned = false;
+  uint8_t* d_lut = nullptr;
+};
+
+// Per-call resources of the host entry points on one device (kept in the table's pool).
+struct HostCtx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  kma_workspace* ws = nullptr;
+  Grow<uint8_t> d_in;     // residues / DNA (+ padding)
+  Grow<uint64_t> d_off;   // offsets
+  Grow<uint8_t> d_out;    // outputs (fid, count, tally, status / hit count, tally)
+  Grow<uint32_t> d_aux;   // 6-frame STRICT: locations per table slot
+  Grow<kma_hit> d_hits;   // 6-frame hits
+  Pinned h_in, h_out;     // pinned staging for both directions
+};
+}  // namespace
+
+struct kma_table {
+  int k = 8;
+  int mlen = 6;  // layout: minimizer length, 0 = flat
+  uint64_t n_buckets = 0;
+  uint8_t lut[256] = {};
+  kma_table_info info = {};
+  std::vector<Replica> reps;
+  std::mutex pool_mu;
+  std::vector<HostCtx*> idle;  // host contexts not in use
+};
+
+extern "C" int kma_workspace_destroy(kma_workspace* ws);
+extern "C" int kma_workspace_create(int device, kma_workspace** out);
+
+namespace {
+
+void destroy_ctx(HostCtx* c) {
+  DeviceScope ds(c->device);
+  if (c->ws) kma_workspace_destroy(c->ws);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  c->d_in.release();
+  c->d_off.release();
+  c->d_out.release();
+  c->d_aux.release();
+  c->d_hits.release();
+  c->h_in.release();
+  c->h_out.release();
+  delete c;
+}
+
+// Take a host context for `device` from the table's pool (or make one).
+int acquire_ctx(kma_table* t, int device, HostCtx** out) {
+  {
+    std::lock_guard<std::mutex> g(t->pool_mu);
+    for (size_t i = 0; i < t->idle.size(); ++i)
+      if (t->idle[i]->device == device) {
+        *out = t->idle[i];
+        t->idle.erase(t->idle.begin() + i);
+        return KMA_OK;
+      }
+  }
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
+  HostCtx* c = new HostCtx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
-    if (t->d_lut) (void)hipFree(t->d_lut);
-    delete t;
+    delete c;
+    return fail(KMA_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  if (int rc = kma_workspace_create(device, &c->ws)) {
+    destroy_ctx(c);
+    return rc;
+  }
+  *out = c;
+  return KMA_OK;
+}
+void release_ctx(kma_table* t, HostCtx* c) {
+  std::lock_guard<std::mutex> g(t->pool_mu);
+  t->idle.push_back(c);
+}
+struct CtxGuard {
+  kma_table* t;
+  HostCtx* c;
+  ~CtxGuard() {
+    if (c) release_ctx(t, c);
+  }
+};
+
+const Replica* replica_on(const kma_table* t, int device) {
+  for (const Replica& r : t->reps)
+    if (r.device == device) return &r;
+  return nullptr;
+}
+
+int add_replica(kma_table* t, int device, uint64_t* d_slots, bool owned) {
+  Replica r;
+  r.device = device;
+  r.d_slots = d_slots;
+  r.owned = owned;
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
+  hipError_t e = hipMalloc(&r.d_lut, 256);
+  if (e == hipSuccess) e = hipMemcpy(r.d_lut, t->lut, 256, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (r.d_lut) (void)hipFree(r.d_lut);
     return fail(KMA_E_DEVICE, "table LUT upload: %s", hipGetErrorString(e));
   }
-  t->info.n_buckets = n_buckets;
-  t->info.bytes = n_buckets * 64;
-  t->info.k = k;
-  t->info.device = device;
-  t->info.minimizer_len = t->mlen;
-  *out = t;
+  t->reps.push_back(r);
+  t->info.n_replicas = (int32_t)t->reps.size();
   return KMA_OK;
 }
 
-constexpr uint64_t kMaxBuckets = 1ull << 29;  // slot index and bucket index stay 32-bit
+kma_table* new_table(int device, int k, int m, uint64_t n_buckets, const uint8_t lut[256]) {
+  kma_table* t = new kma_table();
+  t->k = k;
+  t->mlen = m;
+  t->n_buckets = n_buckets;
+  std::memcpy(t->lut, lut, 256);
+  t->info.n_buckets = n_buckets;
+  t->info.bytes = n_buckets * kma::kBucketBytes;
+  t->info.k = k;
+  t->info.device = device;
+  t->info.minimizer_len = m;
+  int ne = 0;
+  for (int c = 0; c < 256; ++c)
+    if (lut[c] >= 28) t->info.extra_syms[lut[c] - 28] = (uint8_t)c, ++ne;
+  t->info.n_extra_syms = ne;
+  return t;
+}
 
-int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
+void free_table(kma_table* t) {
+  for (HostCtx* c : t->idle) destroy_ctx(c);
+  for (Replica& r : t->reps) {
+    DeviceScope ds(r.device);
+    if (r.owned && r.d_slots) (void)hipFree(r.d_slots);
+    if (r.d_lut) (void)hipFree(r.d_lut);
+  }
+  delete t;
+}
+
+int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m, uint32_t* d_winner,
                     const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, uint32_t* d_status,
                     hipStream_t s) {
-  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than 2^29 buckets");
-  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * 64, s));
+  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than %llu buckets",
+                                          (unsigned long long)kMaxBuckets);
+  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * kma::kBucketBytes, s));
   KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::kSlotsPerBucket * sizeof(uint32_t), s));
   KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
-  const int m = kma::minimizer_len(k, n_buckets);
   KMA_HIP(kma::launch_build_insert(d_slots, d_winner, (uint32_t)n_buckets, k, m, d_keys, n,
                                    d_status, s));
   KMA_HIP(kma::launch_build_finalize(d_slots, d_winner, d_fids, (uint32_t)n_buckets, k, m,
@@ -258,7 +408,12 @@ int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, uint32_t* d_wi
   return KMA_OK;
 }
 
-// Table from device-resident keys/fids (n rows; fids already checked against KMA_MAX_FID).
+// Table from device-resident keys/fids on `device` (n rows; fids already checked). The layout
+// is the size-derived minimizer layout; when that one is crowded (more than kMaxDisplaced of
+// the keys past their home bucket, or a chain longer than kMaxChain: keys piling onto few
+// minimizers) the table is also built flat and the flat one kept if it halves the displaced
+// keys or the longest chain. At high load factors both layouts displace many keys and the
+// minimizer one stays. KMA_MINIMIZER forces a layout.
 int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, int k,
                             int device, double lf, const uint8_t lut[256], kma_table** out) {
   const uint64_t nb = kma_table_buckets_for(n, lf);
@@ -268,27 +423,52 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
   uint32_t *d_winner, *d_status;
   KMA_HIP(tmp.alloc(&d_winner, nb * kma::kSlotsPerBucket * 4));
   KMA_HIP(tmp.alloc(&d_status, 16));
+  auto build = [&](int m, uint64_t** slots, uint32_t st[4]) -> int {
+    KMA_HIP(hipMalloc(slots, nb * kma::kBucketBytes));
+    int rc = build_on_device(*slots, nb, k, m, d_winner, d_keys, d_fids, n, d_status, nullptr);
+    if (rc == KMA_OK) {
+      hipError_t e = hipMemcpy(st, d_status, 16, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) rc = fail(KMA_E_DEVICE, "build: %s", hipGetErrorString(e));
+      else if (st[0]) rc = fail(KMA_E_TABLE_FULL, "signature table full");
+    }
+    if (rc != KMA_OK) {
+      (void)hipFree(*slots);
+      *slots = nullptr;
+    }
+    return rc;
+  };
+  int m = kma::minimizer_len(k, nb);
   uint64_t* d_slots = nullptr;
-  KMA_HIP(hipMalloc(&d_slots, nb * 64));
-  int rc = build_on_device(d_slots, nb, k, d_winner, d_keys, d_fids, n, d_status, nullptr);
   uint32_t st[4] = {};
-  if (rc == KMA_OK) {
-    hipError_t e = hipMemcpy(st, d_status, 16, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = fail(KMA_E_DEVICE, "build: %s", hipGetErrorString(e));
-    else if (st[0]) rc = fail(KMA_E_TABLE_FULL, "signature table full");
+  if (int rc = build(m, &d_slots, st)) return rc;
+  const bool crowded = st[3] > kma::kMaxDisplaced * std::max<uint32_t>(st[1], 1) ||
+                       st[2] > kma::kMaxChain;
+  if (m != 0 && crowded && forced_layout() < 0) {
+    uint64_t* d_flat = nullptr;
+    uint32_t sf[4] = {};
+    if (int rc = build(0, &d_flat, sf)) {
+      (void)hipFree(d_slots);
+      return rc;
+    }
+    const bool better = 2ull * sf[3] < st[3] || (st[2] > kma::kMaxChain && 2 * sf[2] < st[2]);
+    (void)hipFree(better ? d_slots : d_flat);
+    if (better) {
+      d_slots = d_flat;
+      std::memcpy(st, sf, sizeof st);
+      m = 0;
+    }
   }
-  if (rc == KMA_OK) rc = make_table_object(device, k, nb, d_slots, true, lut, out);
-  if (rc != KMA_OK) {
+  kma_table* t = new_table(device, k, m, nb, lut);
+  if (int rc = add_replica(t, device, d_slots, true)) {
     (void)hipFree(d_slots);
+    delete t;
     return rc;
   }
-  (*out)->info.n_rows = n;
-  (*out)->info.n_entries = st[1];
-  (*out)->info.max_probe = st[2];
-  int ne = 0;
-  for (int c = 0; c < 256; ++c)
-    if (lut[c] >= 28) (*out)->info.extra_syms[lut[c] - 28] = (uint8_t)c, ++ne;
-  (*out)->info.n_extra_syms = ne;
+  t->info.n_rows = n;
+  t->info.n_entries = st[1];
+  t->info.max_probe = st[2];
+  t->info.n_displaced = st[3];
+  *out = t;
   return KMA_OK;
 }
 
@@ -314,6 +494,28 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
   const int rc = create_from_device_keys(d_keys, d_fids, n, k, device, lf, lut, out);
   if (rc != KMA_OK) return rc;
   (*out)->info.n_skipped = n_skipped;
+  return KMA_OK;
+}
+
+// Run f(i) for i in [0, n) on n threads (inline for one) and return the first failure, with
+// its message moved to the calling thread (kma_last_error is thread-local).
+template <class F>
+int fan_out(int n, F f) {
+  if (n == 1) return f(0);
+  std::vector<int> rc(n, KMA_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] {
+      rc[i] = f(i);
+      if (rc[i] != KMA_OK) msg[i] = g_err;
+    });
+  for (auto& x : th) x.join();
+  for (int i = 0; i < n; ++i)
+    if (rc[i] != KMA_OK) {
+      g_err = msg[i];
+      return rc[i];
+    }
   return KMA_OK;
 }
 
@@ -343,6 +545,10 @@ uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor) {
   uint64_t nb = (uint64_t)((slots + kma::kSlotsPerBucket - 1) / kma::kSlotsPerBucket);
   return nb < 1 ? 1 : nb;
 }
+
+int kma_table_layout_for(int k, uint64_t n_buckets) { return kma::minimizer_len(k, n_buckets); }
+
+int kma_bucket_slots(void) { return kma::kSlotsPerBucket; }
 
 int kma_pack_kmers(const kma_table* table, const char* text, const uint64_t* offsets, uint64_t n,
                    uint64_t* out_keys) {
@@ -392,6 +598,62 @@ int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t
   return create_from_keys(kv, fids, n, k, device, load_factor, lut, skipped, out);
 }
 
+int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
+  if (!t || n_devices < 0 || (n_devices && !device_ids) || t->reps.empty())
+    return fail(KMA_E_INVALID, "null argument");
+  const Replica& src = t->reps[0];
+  const uint64_t bytes = t->n_buckets * kma::kBucketBytes;
+  for (int i = 0; i < n_devices; ++i) {
+    const int dev = device_ids[i];
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || dev < 0 || dev >= n_dev)
+      return fail(KMA_E_INVALID, "device %d not present", dev);
+    uint64_t* d = nullptr;
+    {
+      DeviceScope ds(dev);
+      if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", dev);
+      KMA_HIP(hipMalloc(&d, bytes));
+      // Device 0's replica to this device: a peer copy (xGMI between MI355X GPUs).
+      hipError_t e = dev == src.device
+                         ? hipMemcpy(d, src.d_slots, bytes, hipMemcpyDeviceToDevice)
+                         : hipMemcpyPeer(d, dev, src.d_slots, src.device, bytes);
+      if (e != hipSuccess) {
+        (void)hipFree(d);
+        return fail(KMA_E_DEVICE, "replica copy to device %d: %s", dev, hipGetErrorString(e));
+      }
+    }
+    if (int rc = add_replica(t, dev, d, true)) {
+      DeviceScope ds(dev);
+      (void)hipFree(d);
+      return rc;
+    }
+  }
+  return KMA_OK;
+}
+
+int kma_table_create_replicated(const char* text, const uint64_t* offsets, const uint32_t* fids,
+                                uint64_t n, int k, int n_devices, const int* device_ids,
+                                double load_factor, kma_table** out) {
+  if (!out || n_devices < 1 || !device_ids) return fail(KMA_E_INVALID, "null argument");
+  *out = nullptr;
+  kma_table* t = nullptr;
+  if (int rc = kma_table_create(text, offsets, fids, n, k, device_ids[0], load_factor, &t))
+    return rc;
+  if (int rc = kma_table_replicate(t, n_devices - 1, device_ids + 1)) {
+    free_table(t);
+    return rc;
+  }
+  *out = t;
+  return KMA_OK;
+}
+
+int kma_table_replicas(const kma_table* t, int* n, int* device_ids, int cap) {
+  if (!t || !n) return fail(KMA_E_INVALID, "null argument");
+  *n = (int)t->reps.size();
+  for (int i = 0; i < *n && i < cap && device_ids; ++i) device_ids[i] = t->reps[i].device;
+  return KMA_OK;
+}
+
 int kma_table_info_get(const kma_table* table, kma_table_info* out) {
   if (!table || !out) return fail(KMA_E_INVALID, "null argument");
   *out = table->info;
@@ -400,38 +662,48 @@ int kma_table_info_get(const kma_table* table, kma_table_info* out) {
 
 int kma_table_destroy(kma_table* table) {
   if (!table) return KMA_OK;
-  DeviceScope ds(table->device);
-  if (table->owned && table->d_slots) (void)hipFree(table->d_slots);
-  if (table->d_lut) (void)hipFree(table->d_lut);
-  delete table;
+  free_table(table);
   return KMA_OK;
 }
 
-int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, uint32_t* d_winner,
-                           const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
-                           uint32_t* d_status, void* stream) {
+int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
+                           uint32_t* d_winner, const uint64_t* d_keys, const uint32_t* d_fids,
+                           uint64_t n, uint32_t* d_status, void* stream) {
   if (!d_slots || !d_winner || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
     return fail(KMA_E_INVALID, "null argument");
   if (int rc = check_k(k)) return rc;
-  return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, d_winner, d_keys, d_fids,
-                         n, d_status, static_cast<hipStream_t>(stream));
+  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout;
+  if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
+    return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
+  return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, m, d_winner, d_keys,
+                         d_fids, n, d_status, static_cast<hipStream_t>(stream));
 }
 
-int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int device, kma_table** out) {
+int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, int device,
+                          kma_table** out) {
   if (!d_slots || !out || !n_buckets) return fail(KMA_E_INVALID, "null argument");
-  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than 2^29 buckets");
+  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than %llu buckets",
+                                          (unsigned long long)kMaxBuckets);
   if (int rc = check_k(k)) return rc;
-  DeviceScope ds(device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", device);
+  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout;
+  if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
+    return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
   uint8_t lut[256];
   standard_lut(lut);
-  return make_table_object(device, k, n_buckets, static_cast<uint64_t*>(d_slots), false, lut, out);
+  kma_table* t = new_table(device, k, m, n_buckets, lut);
+  if (int rc = add_replica(t, device, static_cast<uint64_t*>(d_slots), false)) {
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return KMA_OK;
 }
 
 int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes) {
-  if (!table || !d_slots || !bytes) return fail(KMA_E_INVALID, "null argument");
-  *d_slots = table->d_slots;
-  *bytes = table->n_buckets * 64;
+  if (!table || !d_slots || !bytes || table->reps.empty())
+    return fail(KMA_E_INVALID, "null argument");
+  *d_slots = table->reps[0].d_slots;
+  *bytes = table->n_buckets * kma::kBucketBytes;
   return KMA_OK;
 }
 
@@ -459,13 +731,11 @@ void codon_codes(const char* code, uint8_t out[64]) {
     out[i] = (code[i] == '*' || code[i] == 'X') ? 0 : (uint8_t)(code[i] - 'A' + 1);
 }
 
-// The 6-frame pass: probe + block compaction and the block-count scan (enqueue_contigs), then
-// the canonical-order emit (enqueue_contig_emit; with out = null it only publishes the count).
-kma::ContigArgs contig_args(const kma_table* t, kma_workspace* ws, const uint8_t* d_dna,
-                            const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,
-                            const char* code, uint32_t* d_tally, uint32_t n_fid) {
+kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace* ws,
+                            const uint8_t* d_dna, const uint64_t* d_offsets, uint32_t n_contig,
+                            uint64_t n_bases, const char* code, uint32_t* d_tally, uint32_t n_fid) {
   kma::ContigArgs a{};
-  a.slots = t->d_slots;
+  a.slots = r.d_slots;
   a.n_buckets = (uint32_t)t->n_buckets;
   a.dna = d_dna;
   a.offsets = d_offsets;
@@ -482,20 +752,110 @@ kma::ContigArgs contig_args(const kma_table* t, kma_workspace* ws, const uint8_t
   return a;
 }
 
-int enqueue_contigs(kma_workspace* ws, const kma::ContigArgs& a, hipStream_t s) {
-  const uint64_t nb = contig_blocks(a.total_bases);
-  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
-  size_t tb = ws->ctemp_bytes;
-  KMA_HIP(kma::launch_contig_scan(ws->d_ccounts, ws->d_cprefix, nb, ws->d_ctemp, &tb, s));
-  return KMA_OK;
-}
-
 int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
                         hipStream_t s) {
   a.out = d_hits;
   a.cap = d_hits ? cap : 0;
   a.n_hits = d_n_hits;
   KMA_HIP(kma::launch_contigs_emit(a, contig_blocks(a.total_bases), s));
+  return KMA_OK;
+}
+
+// The protein path on one replica (device buffers, asynchronous on s).
+int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws,
+                         const uint8_t* d_residues, const uint64_t* d_offsets, uint32_t n_seq,
+                         uint64_t n_residues, int min_hits, uint32_t flags, int32_t* d_fid,
+                         int32_t* d_count, uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
+                         hipStream_t s) {
+  kma::ProteinArgs a{};
+  a.slots = r.d_slots;
+  a.n_buckets = (uint32_t)t->n_buckets;
+  a.lut = r.d_lut;
+  a.residues = d_residues;
+  a.offsets = d_offsets;
+  a.n_seq = n_seq;
+  a.n_residues = (uint32_t)n_residues;
+  a.k = t->k;
+  a.mlen = t->mlen;
+  a.min_hits = min_hits;
+  a.flags = flags;
+  a.out_fid = d_fid;
+  a.out_count = d_count;
+  a.out_status = d_status;
+  a.tally = d_tally;
+  a.n_fid = d_tally ? n_fid : 0;
+  a.gset = ws->d_gset;
+  hipEvent_t* ev = nullptr;
+  if (ws->timing) {
+    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
+    KMA_HIP(hipEventRecord(ev[0], s));
+  }
+  KMA_HIP(kma::launch_annotate(a, s));
+  if (ev) {
+    KMA_HIP(hipEventRecord(ev[1], s));
+    KMA_HIP(hipEventRecord(ev[2], s));
+  }
+  return KMA_OK;
+}
+
+int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
+  if (!t) return fail(KMA_E_INVALID, "null table");
+  if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
+  if (flags & ~(KMA_F_END_EXCLUSIVE | KMA_F_MULTISET)) return fail(KMA_E_INVALID, "bad flags");
+  return KMA_OK;
+}
+
+// One shard [lo, hi) of a host protein call on replica r (host buffers, synchronous).
+int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
+                  const uint64_t* offsets, uint32_t lo, uint32_t hi, int min_hits,
+                  uint32_t flags, int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
+                  uint32_t* tally, uint32_t n_fid) {
+  const uint32_t n = hi - lo;
+  if (n == 0) return KMA_OK;
+  const uint64_t base = offsets[lo], nres = offsets[hi] - base;
+  if (nres > kMaxResidues)
+    return fail(KMA_E_INVALID, "%llu residues in one device call (limit 2^32 - 128)",
+                (unsigned long long)nres);
+  HostCtx* c = nullptr;
+  if (int rc = acquire_ctx(t, r.device, &c)) return rc;
+  CtxGuard guard{t, c};
+  DeviceScope ds(r.device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r.device);
+  const size_t in_bytes = (nres + kResPad + 7) & ~7ull;
+  const size_t off_bytes = (n + 1) * 8ull;
+  const size_t out_bytes = n * 9ull + (tally ? n_fid * 4ull : 0) + 16;
+  KMA_HIP(c->d_in.reserve(in_bytes));
+  KMA_HIP(c->d_off.reserve(n + 1));
+  KMA_HIP(c->d_out.reserve(out_bytes));
+  KMA_HIP(c->h_in.reserve(in_bytes + off_bytes));
+  KMA_HIP(c->h_out.reserve(out_bytes));
+  if (int rc = kma_workspace_reserve(c->ws, nres)) return rc;
+  // Stage: residues (zero padded) then rebased offsets, in one pinned buffer.
+  uint8_t* hin = c->h_in.p;
+  std::memcpy(hin, residues + base, nres);
+  std::memset(hin + nres, 0, in_bytes - nres);
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
+  for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
+  hipStream_t s = c->stream;
+  KMA_HIP(hipMemcpyAsync(c->d_in.p, hin, in_bytes, hipMemcpyHostToDevice, s));
+  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, s));
+  uint8_t* dout = c->d_out.p;
+  int32_t* d_fid = reinterpret_cast<int32_t*>(dout);
+  int32_t* d_cnt = d_fid + n;
+  uint32_t* d_tally = tally ? reinterpret_cast<uint32_t*>(d_cnt + n) : nullptr;
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_cnt + n) + (tally ? n_fid * 4ull : 0);
+  if (d_tally) KMA_HIP(hipMemsetAsync(d_tally, 0, n_fid * 4ull, s));
+  if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p, n, nres, min_hits, flags,
+                                    d_fid, d_cnt, d_st, d_tally, n_fid, s))
+    return rc;
+  KMA_HIP(hipMemcpyAsync(c->h_out.p, dout, out_bytes - 16, hipMemcpyDeviceToHost, s));
+  KMA_HIP(hipStreamSynchronize(s));
+  const uint8_t* hout = c->h_out.p;
+  std::memcpy(out_fid + lo, hout, n * 4ull);
+  std::memcpy(out_count + lo, hout + n * 4ull, n * 4ull);
+  const uint8_t* ht = hout + n * 8ull;
+  std::memcpy(out_status + lo, ht + (tally ? n_fid * 4ull : 0), n);
+  if (tally) std::memcpy(tally, ht, n_fid * 4ull);
   return KMA_OK;
 }
 }  // namespace
@@ -531,18 +891,8 @@ int kma_workspace_create(int device, kma_workspace** out) {
   if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
       n_cu > 0)
     w->n_cu = n_cu;
-  hipError_t e = hipMalloc(&w->d_flag, 16);
-  if (e == hipSuccess) e = hipMemset(w->d_flag, 0, 16);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
-  w->seg_ev.assign(kMaxSegments + 2, nullptr);
-  for (auto& ev : w->seg_ev)
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  if (e == hipSuccess)
-    e = hipMalloc(&w->d_scratch, (size_t)kma::kFallbackBlocks * kma::kFallbackCap * 8);
-  if (e == hipSuccess) e = hipMalloc(&w->d_hits, 2 * kHitsPad * 4);  // reserve() grows it
-  if (e == hipSuccess) e = hipMalloc(&w->d_pending, pending_cap(0) * sizeof(kma::PendingRec));
+  hipError_t e = hipMalloc(&w->d_gset, 2 * kResPad * 4);  // reserve() grows it
   if (e != hipSuccess) {
-    if (w->d_flag) (void)hipFree(w->d_flag);
     delete w;
     return fail(KMA_E_NOMEM, "workspace: %s", hipGetErrorString(e));
   }
@@ -552,19 +902,17 @@ int kma_workspace_create(int device, kma_workspace** out) {
 
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
-  if (ws->d_hits && n_residues <= ws->hits_cap) return KMA_OK;
+  if (n_residues > kMaxResidues)
+    return fail(KMA_E_INVALID, "%llu residues in one call (limit 2^32 - 128)",
+                (unsigned long long)n_residues);
+  if (ws->d_gset && n_residues <= ws->res_cap) return KMA_OK;
   DeviceScope ds(ws->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
-  if (ws->d_hits) (void)hipFree(ws->d_hits);
-  ws->d_hits = nullptr;
-  ws->hits_cap = 0;
-  if (ws->d_pending) (void)hipFree(ws->d_pending);
-  ws->d_pending = nullptr;
-  // Padded by kHitsPad words (never empty): K2 may read word 0 for a chunk past the end.
-  // hits then slot ids, each n_residues + kHitsPad words
-  KMA_HIP(hipMalloc(&ws->d_hits, 2 * (n_residues + kHitsPad) * 4));
-  KMA_HIP(hipMalloc(&ws->d_pending, pending_cap(n_residues) * sizeof(kma::PendingRec)));
-  ws->hits_cap = n_residues;
+  if (ws->d_gset) (void)hipFree(ws->d_gset);
+  ws->d_gset = nullptr;
+  ws->res_cap = 0;
+  KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
+  ws->res_cap = n_residues;
   return KMA_OK;
 }
 
@@ -580,9 +928,9 @@ int kma_workspace_timing(kma_workspace* ws, int enable) {
   return KMA_OK;
 }
 
-int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* probe_ms,
-                              double* vote_ms) {
-  if (!ws || !n_calls || !probe_ms || !vote_ms) return fail(KMA_E_INVALID, "null argument");
+int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
+                              double* rest_ms) {
+  if (!ws || !n_calls || !kernel_ms || !rest_ms) return fail(KMA_E_INVALID, "null argument");
   DeviceScope ds(ws->device);
   const uint32_t n = std::min(ws->n_timed, kTimingRing);
   double p = 0, v = 0;
@@ -596,29 +944,17 @@ int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* prob
     v += b;
   }
   *n_calls = n;
-  *probe_ms = p;
-  *vote_ms = v;
+  *kernel_ms = p;
+  *rest_ms = v;
   ws->n_timed = 0;
   return KMA_OK;
-}
-
-int kma_protein_form(const kma_workspace* ws, uint32_t n_seq) {
-  if (!ws) return fail(KMA_E_INVALID, "null workspace");
-  DeviceScope ds(ws->device);
-  return fused_form(n_seq, ws->n_cu) ? 1 : 0;
 }
 
 int kma_workspace_destroy(kma_workspace* ws) {
   if (!ws) return KMA_OK;
   DeviceScope ds(ws->device);
   for (auto& e : ws->events) (void)hipEventDestroy(e);
-  for (auto& e : ws->seg_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (ws->side) (void)hipStreamDestroy(ws->side);
-  (void)hipFree(ws->d_flag);
-  (void)hipFree(ws->d_scratch);
-  if (ws->d_hits) (void)hipFree(ws->d_hits);
-  if (ws->d_pending) (void)hipFree(ws->d_pending);
+  if (ws->d_gset) (void)hipFree(ws->d_gset);
   free_contig_scratch(ws);
   delete ws;
   return KMA_OK;
@@ -629,161 +965,48 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
                                  int min_hits, uint32_t flags, int32_t* d_fid, int32_t* d_count,
                                  uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
                                  void* stream) {
-  if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
-  if (ws->device != t->device) return fail(KMA_E_INVALID, "workspace on another device");
-  if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
-  if (flags & ~(KMA_F_END_EXCLUSIVE | KMA_F_MULTISET)) return fail(KMA_E_INVALID, "bad flags");
+  if (int rc = check_protein_call(t, min_hits, flags)) return rc;
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  const Replica* r = replica_on(t, ws->device);
+  if (!r) return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d",
+                      ws->device);
   if (n_seq == 0) return KMA_OK;
   if (!d_residues || !d_offsets || !d_fid || !d_count || !d_status)
     return fail(KMA_E_INVALID, "null device buffer");
   if ((uintptr_t)d_residues & 7) return fail(KMA_E_INVALID, "residues must be 8-byte aligned");
-  if (n_residues > ws->hits_cap)
+  if (n_residues > ws->res_cap)
     return fail(KMA_E_CAPACITY, "workspace reserved for %llu residues, call needs %llu",
-                (unsigned long long)ws->hits_cap, (unsigned long long)n_residues);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  DeviceScope ds(t->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  kma::ProteinArgs a{};
-  a.slots = t->d_slots;
-  a.n_buckets = (uint32_t)t->n_buckets;
-  a.lut = t->d_lut;
-  a.residues = d_residues;
-  a.offsets = d_offsets;
-  a.n_seq = n_seq;
-  a.n_residues = n_residues;
-  a.k = t->k;
-  a.mlen = t->mlen;
-  a.min_hits = min_hits;
-  a.flags = flags;
-  a.out_fid = d_fid;
-  a.out_count = d_count;
-  a.out_status = d_status;
-  a.tally = d_tally;
-  a.n_fid = d_tally ? n_fid : 0;
-  a.hits = ws->d_hits;
-  a.sids = ws->d_hits + ws->hits_cap + kHitsPad;
-  a.overflow_flag = ws->d_flag;
-  a.pending = ws->d_pending;
-  a.pending_half = (uint32_t)(pending_cap(ws->hits_cap) / 2);
-  a.scratch = ws->d_scratch;
-  hipEvent_t* ev = nullptr;
-  if (ws->timing) {
-    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
-    KMA_HIP(hipEventRecord(ev[0], s));
-  }
-  if (fused_form(n_seq, ws->n_cu)) {
-    // K12 (probe + vote in one kernel), then vote_long for the pending proteins.
-    a.seq_lo = 0;
-    a.seq_hi = n_seq;
-    a.reset_flag = 0;
-    KMA_HIP(hipMemsetAsync(ws->d_flag, 0, 16, s));  // pending-list lengths (K12 appends);
-    // the whole 16-B flag block: a byte count 8 over a multiple of 16 costs ~2 us per call
-    if (ev) KMA_HIP(hipEventRecord(ev[0], s));     // the probe phase is K12 alone
-    KMA_HIP(kma::launch_fused(a, ws->n_cu, s));
-    if (ev) KMA_HIP(hipEventRecord(ev[1], s));
-    KMA_HIP(kma::launch_long(a, ws->n_cu, s));
-    if (ev) KMA_HIP(hipEventRecord(ev[2], s));
-    return KMA_OK;
-  }
-  if (ev) {
-    // Timing mode: the phases back to back on the call's stream, so their events bracket them.
-    a.seq_lo = 0;
-    a.seq_hi = n_seq;
-    a.reset_flag = 1;
-    KMA_HIP(kma::launch_probe(a, ws->n_cu, s));
-    KMA_HIP(hipEventRecord(ev[1], s));
-    KMA_HIP(kma::launch_vote(a, ws->n_cu, s));
-    KMA_HIP(kma::launch_long(a, ws->n_cu, s));
-    KMA_HIP(hipEventRecord(ev[2], s));
-    return KMA_OK;
-  }
-  const int S = segments_for(n_seq);
-  if (S > 1) {
-    KMA_HIP(hipEventRecord(ws->seg_ev[0], s));  // fork: the side stream sees prior work
-    KMA_HIP(hipStreamWaitEvent(ws->side, ws->seg_ev[0], 0));
-  }
-  for (int i = 0; i < S; ++i) {
-    a.seq_lo = (uint32_t)((uint64_t)n_seq * i / S);
-    a.seq_hi = (uint32_t)((uint64_t)n_seq * (i + 1) / S);
-    a.reset_flag = i == 0;
-    KMA_HIP(kma::launch_probe(a, ws->n_cu, s));
-    if (S > 1) {
-      KMA_HIP(hipEventRecord(ws->seg_ev[1 + i], s));
-      KMA_HIP(hipStreamWaitEvent(ws->side, ws->seg_ev[1 + i], 0));
-      KMA_HIP(kma::launch_vote(a, ws->n_cu, ws->side));
-    } else {
-      KMA_HIP(kma::launch_vote(a, ws->n_cu, s));
-#ifdef KMA_VOTE_TRACE  // experiment builds only: per-block phase clocks of K2 -> file
-      if (const char* f = getenv("KMA_TRACE_FILE")) {
-        const uint64_t nb = (n_seq + kma::kVoteProteins - 1) / kma::kVoteProteins;
-        std::vector<uint64_t> tr(nb * 8);
-        KMA_HIP(hipStreamSynchronize(s));
-        KMA_HIP(hipMemcpy(tr.data(), ws->d_scratch, tr.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE* o = fopen(f, "wb")) {
-          fwrite(tr.data(), 8, tr.size(), o);
-          fclose(o);
-        }
-      }
-#endif
-    }
-  }
-  if (S > 1) {
-    KMA_HIP(hipEventRecord(ws->seg_ev[kMaxSegments + 1], ws->side));  // join
-    KMA_HIP(hipStreamWaitEvent(s, ws->seg_ev[kMaxSegments + 1], 0));
-  }
-  a.seq_lo = 0;
-  a.seq_hi = n_seq;
-  KMA_HIP(kma::launch_long(a, ws->n_cu, s));
-  return KMA_OK;
+                (unsigned long long)ws->res_cap, (unsigned long long)n_residues);
+  DeviceScope ds(r->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r->device);
+  return annotate_proteins_on(t, *r, ws, d_residues, d_offsets, n_seq, n_residues, min_hits,
+                              flags, d_fid, d_count, d_status, d_tally, n_fid,
+                              static_cast<hipStream_t>(stream));
 }
 
-int kma_annotate_proteins(const kma_table* t, const uint8_t* residues, const uint64_t* offsets,
+int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const uint64_t* offsets,
                           uint32_t n_seq, int min_hits, uint32_t flags, int32_t* out_fid,
                           int32_t* out_count, uint8_t* out_status, uint32_t* out_tally,
                           uint32_t n_fid) {
-  if (!t) return fail(KMA_E_INVALID, "null table");
-  if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
+  if (int rc = check_protein_call(tc, min_hits, flags)) return rc;
+  kma_table* t = const_cast<kma_table*>(tc);  // only the context pool is touched
   if (n_seq == 0) return KMA_OK;
   if (!residues || !offsets || !out_fid || !out_count || !out_status)
     return fail(KMA_E_INVALID, "null argument");
   for (uint32_t s = 0; s < n_seq; ++s)
     if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
-  DeviceScope ds(t->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  const uint64_t base = offsets[0], nres = offsets[n_seq] - base;
-  std::vector<uint64_t> rel(offsets, offsets + n_seq + 1);
-  for (auto& o : rel) o -= base;
-  DevBufs b;
-  uint8_t *d_res, *d_st;
-  uint64_t* d_off;
-  int32_t *d_fid, *d_cnt;
-  uint32_t* d_tally = nullptr;
-  KMA_HIP(b.alloc(&d_res, nres + 32));
-  KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
-  KMA_HIP(b.alloc(&d_fid, n_seq * 4ull));
-  KMA_HIP(b.alloc(&d_cnt, n_seq * 4ull));
-  KMA_HIP(b.alloc(&d_st, n_seq));
-  KMA_HIP(hipMemcpy(d_res, residues + base, nres, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemset(d_res + nres, 0, 32));
-  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_seq + 1) * 8ull, hipMemcpyHostToDevice));
-  if (out_tally && n_fid) {
-    KMA_HIP(b.alloc(&d_tally, n_fid * 4ull));
-    KMA_HIP(hipMemcpy(d_tally, out_tally, n_fid * 4ull, hipMemcpyHostToDevice));
-  }
-  kma_workspace* ws = nullptr;
-  if (int rc = kma_workspace_create(t->device, &ws)) return rc;
-  int rc = kma_workspace_reserve(ws, nres);
-  if (rc == KMA_OK)
-    rc = kma_annotate_proteins_device(t, ws, d_res, d_off, n_seq, nres, min_hits, flags, d_fid,
-                                      d_cnt, d_st, d_tally, d_tally ? n_fid : 0, nullptr);
-  hipError_t e = rc == KMA_OK ? hipDeviceSynchronize() : hipSuccess;
-  kma_workspace_destroy(ws);
+  const bool tally = out_tally && n_fid;
+  const int nr = (int)std::min<uint64_t>(t->reps.size(), n_seq);
+  const std::vector<uint32_t> b = shard_bounds(offsets, n_seq, nr);
+  std::vector<std::vector<uint32_t>> part(tally ? nr : 0, std::vector<uint32_t>(n_fid));
+  const int rc = fan_out(nr, [&](int i) {
+    return protein_shard(t, t->reps[i], residues, offsets, b[i], b[i + 1], min_hits, flags,
+                         out_fid, out_count, out_status, tally ? part[i].data() : nullptr,
+                         n_fid);
+  });
   if (rc != KMA_OK) return rc;
-  if (e != hipSuccess) return fail(KMA_E_DEVICE, "annotate: %s", hipGetErrorString(e));
-  KMA_HIP(hipMemcpy(out_fid, d_fid, n_seq * 4ull, hipMemcpyDeviceToHost));
-  KMA_HIP(hipMemcpy(out_count, d_cnt, n_seq * 4ull, hipMemcpyDeviceToHost));
-  KMA_HIP(hipMemcpy(out_status, d_st, n_seq, hipMemcpyDeviceToHost));
-  if (d_tally) KMA_HIP(hipMemcpy(out_tally, d_tally, n_fid * 4ull, hipMemcpyDeviceToHost));
+  for (int i = 0; i < (tally ? nr : 0); ++i)  // the tally reduce of the replicas
+    for (uint32_t f = 0; f < n_fid; ++f) out_tally[f] += part[i][f];
   return KMA_OK;
 }
 
@@ -803,13 +1026,15 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
                                 uint64_t* d_n_hits, uint32_t* d_tally, uint32_t n_fid,
                                 void* stream) {
   if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
-  if (ws->device != t->device) return fail(KMA_E_INVALID, "workspace on another device");
+  const Replica* r = replica_on(t, ws->device);
+  if (!r) return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d",
+                      ws->device);
   const char* code = ncbi_code(genetic_code);
   if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
   if (!d_n_hits) return fail(KMA_E_INVALID, "null n_hits");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DeviceScope ds(t->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
+  DeviceScope ds(r->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r->device);
   if (n_contig == 0 || n_bases == 0) {
     KMA_HIP(hipMemsetAsync(d_n_hits, 0, 8, s));
     return KMA_OK;
@@ -819,7 +1044,7 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
     return fail(KMA_E_CAPACITY, "workspace reserved for %llu bases, call needs %llu",
                 (unsigned long long)ws->contig_cap, (unsigned long long)n_bases);
   const kma::ContigArgs a =
-      contig_args(t, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid);
+      contig_args(t, *r, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid);
   hipEvent_t* ev = nullptr;  // timing mode: (start, after the probe kernel, end)
   if (ws->timing) {
     ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
@@ -835,65 +1060,160 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
   return rc;
 }
 
-int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
-                         uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
-                         uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid) {
-  if (!t || !n_hits) return fail(KMA_E_INVALID, "null argument");
+}  // extern "C"
+
+namespace {
+// One shard [lo, hi) of a host 6-frame call on replica r. out_hits == null: count the shard's
+// hits into *n_hits and accumulate the tally rows of its contigs (tally = the caller's rows
+// lo..hi); else emit the *n_hits hits (contig indices relative to lo) into *out_hits.
+// strict: the KmerFactory.Strict two-pass form of the peg join (single replica).
+int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint64_t* offsets,
+                 uint32_t lo, uint32_t hi, int genetic_code, bool strict,
+                 std::vector<kma_hit>* out_hits, uint64_t* n_hits, uint32_t* tally,
+                 uint32_t n_fid) {
+  const uint32_t n = hi - lo;
+  const uint64_t base = offsets[lo], total = offsets[hi] - base;
+  if (!out_hits) *n_hits = 0;
+  if (n == 0 || total == 0) return KMA_OK;
   const char* code = ncbi_code(genetic_code);
-  if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
+  HostCtx* c = nullptr;
+  if (int rc = acquire_ctx(t, r.device, &c)) return rc;
+  CtxGuard guard{t, c};
+  DeviceScope ds(r.device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r.device);
+  if (int rc = kma_workspace_reserve_contigs(c->ws, total)) return rc;
+  const size_t in_bytes = (total + 64 + 7) & ~7ull, off_bytes = (n + 1) * 8ull;
+  const size_t tb = tally ? (size_t)n * n_fid * 4 : 0;
+  KMA_HIP(c->d_in.reserve(in_bytes));
+  KMA_HIP(c->d_off.reserve(n + 1));
+  KMA_HIP(c->h_in.reserve(in_bytes + off_bytes + tb));
+  uint8_t* hin = c->h_in.p;
+  std::memcpy(hin, dna + base, total);
+  std::memset(hin + total, 0, in_bytes - total);
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
+  for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
+  hipStream_t s = c->stream;
+  KMA_HIP(hipMemcpyAsync(c->d_in.p, hin, in_bytes, hipMemcpyHostToDevice, s));
+  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, s));
+  // d_out: [n_hits u64, pad | tally]; slot counts (strict) in d_aux; hits in d_hits.
+  KMA_HIP(c->d_out.reserve(16 + tb));
+  uint64_t* d_n = reinterpret_cast<uint64_t*>(c->d_out.p);
+  uint32_t* d_tally = tally ? reinterpret_cast<uint32_t*>(c->d_out.p + 16) : nullptr;
+  if (tb) {
+    uint8_t* ht = hin + in_bytes + off_bytes;
+    std::memcpy(ht, tally, tb);
+    KMA_HIP(hipMemcpyAsync(d_tally, ht, tb, hipMemcpyHostToDevice, s));
+  }
+  kma::ContigArgs a =
+      contig_args(t, r, c->ws, c->d_in.p, c->d_off.p, n, total, code, d_tally, n_fid);
+  const uint64_t nb = contig_blocks(total);
+  if (strict) {
+    const uint64_t n_slots = t->n_buckets * kma::kSlotsPerBucket;
+    KMA_HIP(c->d_aux.reserve(n_slots));
+    KMA_HIP(hipMemsetAsync(c->d_aux.p, 0, n_slots * 4, s));
+    a.slot_count = c->d_aux.p;
+    a.strict_pass = 1;  // count every table key's locations
+    KMA_HIP(kma::launch_contigs_probe(a, nb, s));
+    a.strict_pass = 2;  // keep keys with exactly one location
+  }
+  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
+  size_t stb = c->ws->ctemp_bytes;
+  KMA_HIP(kma::launch_contig_scan(c->ws->d_ccounts, c->ws->d_cprefix, nb, c->ws->d_ctemp, &stb, s));
+  if (!out_hits) {  // pass 1: count (and tally)
+    if (int rc = enqueue_contig_emit(a, nullptr, 0, d_n, s)) return rc;
+    KMA_HIP(c->h_out.reserve(16 + tb));
+    KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
+    if (tb) KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, d_tally, tb, hipMemcpyDeviceToHost, s));
+    KMA_HIP(hipStreamSynchronize(s));
+    std::memcpy(n_hits, c->h_out.p, 8);
+    if (tb) std::memcpy(tally, c->h_out.p + 16, tb);
+    return KMA_OK;
+  }
+  // pass 2: emit into d_hits (sized by pass 1's count, passed in *n_hits)
+  const uint64_t cap = *n_hits;
+  KMA_HIP(c->d_hits.reserve(std::max<uint64_t>(cap, 1)));
+  if (int rc = enqueue_contig_emit(a, c->d_hits.p, cap, d_n, s)) return rc;
+  KMA_HIP(c->h_out.reserve(16 + cap * sizeof(kma_hit)));
+  KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
+  KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, c->d_hits.p, cap * sizeof(kma_hit),
+                         hipMemcpyDeviceToHost, s));
+  KMA_HIP(hipStreamSynchronize(s));
+  uint64_t nh = 0;
+  std::memcpy(&nh, c->h_out.p, 8);
+  if (nh != cap) return fail(KMA_E_DEVICE, "6-frame pass: %llu hits, then %llu",
+                             (unsigned long long)cap, (unsigned long long)nh);
+  out_hits->resize(nh);
+  std::memcpy(out_hits->data(), c->h_out.p + 16, nh * sizeof(kma_hit));
+  return KMA_OK;
+}
+
+int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offsets,
+                          uint32_t n_contig, int genetic_code, bool strict, kma_hit* out_hits,
+                          uint64_t cap, uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid) {
+  if (!t || !n_hits) return fail(KMA_E_INVALID, "null argument");
+  if (!ncbi_code(genetic_code))
+    return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
   *n_hits = 0;
   if (n_contig == 0) return KMA_OK;
   if (!dna || !offsets) return fail(KMA_E_INVALID, "null argument");
   for (uint32_t c = 0; c < n_contig; ++c)
     if (offsets[c + 1] < offsets[c]) return fail(KMA_E_INVALID, "offsets decrease at %u", c);
-  const uint64_t base = offsets[0], total = offsets[n_contig] - base;
-  if (total >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
-  if (total == 0) return KMA_OK;
-  std::vector<uint64_t> rel(offsets, offsets + n_contig + 1);
-  for (auto& o : rel) o -= base;
-  DeviceScope ds(t->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  kma_workspace* ws = nullptr;
-  int rc = kma_workspace_create(t->device, &ws);
+  if (offsets[n_contig] - offsets[0] >= (1ull << 39))
+    return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
+  const bool tally = out_tally && n_fid;
+  const int nr = strict ? 1 : (int)std::min<uint64_t>(t->reps.size(), n_contig);
+  const std::vector<uint32_t> b = shard_bounds(offsets, n_contig, nr);
+  // Pass 1 counts (and tallies into copies: nothing is written on KMA_E_CAPACITY); pass 2
+  // emits. A shard's hits are produced only if the whole call fits in cap.
+  std::vector<uint64_t> nh(nr, 0);
+  std::vector<std::vector<uint32_t>> tal(tally ? nr : 0);
+  for (int i = 0; i < (tally ? nr : 0); ++i)
+    tal[i].assign(out_tally + (uint64_t)b[i] * n_fid, out_tally + (uint64_t)b[i + 1] * n_fid);
+  int rc = fan_out(nr, [&](int i) {
+    return contig_shard(t, t->reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
+                        nullptr, &nh[i], tally ? tal[i].data() : nullptr, n_fid);
+  });
   if (rc != KMA_OK) return rc;
-  std::unique_ptr<kma_workspace, int (*)(kma_workspace*)> ws_guard(ws, kma_workspace_destroy);
-  rc = kma_workspace_reserve_contigs(ws, total);
-  if (rc != KMA_OK) return rc;
-  DevBufs b;
-  uint8_t* d_dna;
-  uint64_t *d_off, *d_n;
-  uint32_t* d_tally = nullptr;
-  kma_hit* d_out = nullptr;
-  KMA_HIP(b.alloc(&d_dna, total + 64));
-  KMA_HIP(b.alloc(&d_off, (n_contig + 1) * 8ull));
-  KMA_HIP(b.alloc(&d_n, 8));
-  KMA_HIP(hipMemcpy(d_dna, dna + base, total, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemset(d_dna + total, 0, 64));
-  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_contig + 1) * 8ull, hipMemcpyHostToDevice));
-  const uint64_t tb = out_tally && n_fid ? (uint64_t)n_contig * n_fid * 4 : 0;
-  if (tb) {
-    KMA_HIP(b.alloc(&d_tally, tb));
-    KMA_HIP(hipMemcpy(d_tally, out_tally, tb, hipMemcpyHostToDevice));
-  }
-  const kma::ContigArgs a =
-      contig_args(t, ws, d_dna, d_off, n_contig, total, code, d_tally, n_fid);
-  rc = enqueue_contigs(ws, a, nullptr);
-  if (rc == KMA_OK) rc = enqueue_contig_emit(a, nullptr, 0, d_n, nullptr);  // count only
-  if (rc != KMA_OK) return rc;
-  uint64_t nh = 0;
-  KMA_HIP(hipMemcpy(&nh, d_n, 8, hipMemcpyDeviceToHost));
-  *n_hits = nh;
-  // On KMA_E_CAPACITY nothing is written (the tally neither), so the caller can retry.
-  if (nh > cap || (nh && !out_hits))
-    return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
+  uint64_t total = 0;
+  for (uint64_t x : nh) total += x;
+  *n_hits = total;
+  if (total > cap || (total && !out_hits))
+    return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)total,
                 (unsigned long long)(out_hits ? cap : 0));
-  if (tb) KMA_HIP(hipMemcpy(out_tally, d_tally, tb, hipMemcpyDeviceToHost));
-  if (nh == 0) return KMA_OK;
-  KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
-  rc = enqueue_contig_emit(a, d_out, nh, d_n, nullptr);
+  for (int i = 0; i < (tally ? nr : 0); ++i)
+    std::copy(tal[i].begin(), tal[i].end(), out_tally + (uint64_t)b[i] * n_fid);
+  if (total == 0) return KMA_OK;
+  std::vector<std::vector<kma_hit>> hv(nr);
+  rc = fan_out(nr, [&](int i) {
+    if (nh[i] == 0) return KMA_OK;
+    return contig_shard(t, t->reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
+                        &hv[i], &nh[i], nullptr, 0);
+  });
   if (rc != KMA_OK) return rc;
-  KMA_HIP(hipMemcpy(out_hits, d_out, nh * sizeof(kma_hit), hipMemcpyDeviceToHost));
+  uint64_t o = 0;
+  for (int i = 0; i < nr; ++i)
+    for (const kma_hit& h : hv[i]) {
+      out_hits[o] = h;
+      out_hits[o++].contig += b[i];
+    }
   return KMA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kma_annotate_contigs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
+                         uint32_t n_contig, int genetic_code, kma_hit* out_hits, uint64_t cap,
+                         uint64_t* n_hits, uint32_t* out_tally, uint32_t n_fid) {
+  return annotate_contigs_host(const_cast<kma_table*>(t), dna, offsets, n_contig, genetic_code,
+                               false, out_hits, cap, n_hits, out_tally, n_fid);
+}
+
+int kma_connect_pegs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
+                     uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
+                     uint64_t cap, uint64_t* n_hits) {
+  return annotate_contigs_host(const_cast<kma_table*>(t), dna, offsets, n_contig, genetic_code,
+                               strict != 0, out_hits, cap, n_hits, nullptr, 0);
 }
 
 int kma_peg_table_create(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg, int k,
@@ -962,69 +1282,6 @@ int kma_peg_table_create(const uint8_t* residues, const uint64_t* offsets, uint3
   const int rc = create_from_device_keys(d_keys, d_pegs, n_sel, k, device, load_factor, lut, out);
   if (rc != KMA_OK) return rc;
   (*out)->info.n_rows = windows;
-  return KMA_OK;
-}
-
-int kma_connect_pegs(const kma_table* t, const uint8_t* dna, const uint64_t* offsets,
-                     uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
-                     uint64_t cap, uint64_t* n_hits) {
-  if (!strict)
-    return kma_annotate_contigs(t, dna, offsets, n_contig, genetic_code, out_hits, cap, n_hits,
-                                nullptr, 0);
-  if (!t || !n_hits) return fail(KMA_E_INVALID, "null argument");
-  const char* code = ncbi_code(genetic_code);
-  if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
-  *n_hits = 0;
-  if (n_contig == 0) return KMA_OK;
-  if (!dna || !offsets) return fail(KMA_E_INVALID, "null argument");
-  for (uint32_t c = 0; c < n_contig; ++c)
-    if (offsets[c + 1] < offsets[c]) return fail(KMA_E_INVALID, "offsets decrease at %u", c);
-  const uint64_t base = offsets[0], total = offsets[n_contig] - base;
-  if (total >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
-  if (total == 0) return KMA_OK;
-  std::vector<uint64_t> rel(offsets, offsets + n_contig + 1);
-  for (auto& o : rel) o -= base;
-  DeviceScope ds(t->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", t->device);
-  kma_workspace* ws = nullptr;
-  int rc = kma_workspace_create(t->device, &ws);
-  if (rc != KMA_OK) return rc;
-  std::unique_ptr<kma_workspace, int (*)(kma_workspace*)> ws_guard(ws, kma_workspace_destroy);
-  rc = kma_workspace_reserve_contigs(ws, total);
-  if (rc != KMA_OK) return rc;
-  DevBufs b;
-  uint8_t* d_dna;
-  uint64_t *d_off, *d_n;
-  uint32_t* d_count;
-  kma_hit* d_out = nullptr;
-  const uint64_t n_slots = t->n_buckets * kma::kSlotsPerBucket;
-  KMA_HIP(b.alloc(&d_dna, total + 64));
-  KMA_HIP(b.alloc(&d_off, (n_contig + 1) * 8ull));
-  KMA_HIP(b.alloc(&d_n, 8));
-  KMA_HIP(b.alloc(&d_count, n_slots * 4));
-  KMA_HIP(hipMemcpy(d_dna, dna + base, total, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemset(d_dna + total, 0, 64));
-  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_contig + 1) * 8ull, hipMemcpyHostToDevice));
-  KMA_HIP(hipMemset(d_count, 0, n_slots * 4));
-  kma::ContigArgs a = contig_args(t, ws, d_dna, d_off, n_contig, total, code, nullptr, 0);
-  a.slot_count = d_count;
-  a.strict_pass = 1;  // count every table key's locations
-  KMA_HIP(kma::launch_contigs_probe(a, contig_blocks(total), nullptr));
-  a.strict_pass = 2;  // keep keys with exactly one location
-  rc = enqueue_contigs(ws, a, nullptr);
-  if (rc == KMA_OK) rc = enqueue_contig_emit(a, nullptr, 0, d_n, nullptr);
-  if (rc != KMA_OK) return rc;
-  uint64_t nh = 0;
-  KMA_HIP(hipMemcpy(&nh, d_n, 8, hipMemcpyDeviceToHost));
-  *n_hits = nh;
-  if (nh > cap || (nh && !out_hits))
-    return fail(KMA_E_CAPACITY, "%llu hits, capacity %llu", (unsigned long long)nh,
-                (unsigned long long)(out_hits ? cap : 0));
-  if (nh == 0) return KMA_OK;
-  KMA_HIP(b.alloc(&d_out, nh * sizeof(kma_hit)));
-  rc = enqueue_contig_emit(a, d_out, nh, d_n, nullptr);
-  if (rc != KMA_OK) return rc;
-  KMA_HIP(hipMemcpy(out_hits, d_out, nh * sizeof(kma_hit), hipMemcpyDeviceToHost));
   return KMA_OK;
 }
 
@@ -1111,6 +1368,118 @@ int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const
   for (uint64_t i = 0; i < n_sel; ++i) {
     out_keys[i] = rows[i] >> 24;
     out_roles[i] = (uint32_t)(rows[i] & kma::kBuildNeg);
+  }
+  return KMA_OK;
+}
+
+// ---- ProteinKmers.distance (GeneCopyProcessor.java:129-162) ------------------------------------
+int kma_protein_distances(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq, int k,
+                          uint32_t flags, const uint32_t* pair_a, const uint32_t* pair_b,
+                          uint64_t n_pairs, int device, uint32_t* out_sim, uint32_t* out_size,
+                          double* out_dist) {
+  if (k < 2 || k > 12) return fail(KMA_E_INVALID, "kmer size %d outside 2..12", k);
+  if (flags & ~KMA_F_END_EXCLUSIVE) return fail(KMA_E_INVALID, "bad flags");
+  if (n_pairs && (!pair_a || !pair_b || !out_sim)) return fail(KMA_E_INVALID, "null argument");
+  if (n_seq && (!residues || !offsets)) return fail(KMA_E_INVALID, "null argument");
+  for (uint64_t i = 0; i < n_pairs; ++i)
+    if (pair_a[i] >= n_seq || pair_b[i] >= n_seq)
+      return fail(KMA_E_INVALID, "pair %llu indexes a protein >= %u", (unsigned long long)i,
+                  n_seq);
+  for (uint32_t s = 0; s < n_seq; ++s)
+    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
+  const uint64_t base = n_seq ? offsets[0] : 0, total = n_seq ? offsets[n_seq] - base : 0;
+  if (total >= (1ull << 31)) return fail(KMA_E_INVALID, "more than 2^31 residues in one call");
+  if (n_seq == 0 || (n_pairs == 0 && !out_size)) return KMA_OK;
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  std::vector<uint64_t> rel(offsets, offsets + n_seq + 1);
+  for (auto& o : rel) o -= base;
+  DevBufs b;
+  uint8_t* d_res;
+  uint64_t *d_off, *d_keys, *d_sorted;
+  uint32_t *d_size, *d_pa, *d_pb, *d_sim, *d_alpha;
+  const uint64_t nw = std::max<uint64_t>(total, 1), np = std::max<uint64_t>(n_pairs, 1);
+  KMA_HIP(b.alloc(&d_res, total + 64));
+  KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
+  KMA_HIP(b.alloc(&d_keys, nw * 8));
+  KMA_HIP(b.alloc(&d_sorted, nw * 8));
+  KMA_HIP(b.alloc(&d_size, n_seq * 4ull));
+  KMA_HIP(b.alloc(&d_pa, np * 4));
+  KMA_HIP(b.alloc(&d_pb, np * 4));
+  KMA_HIP(b.alloc(&d_sim, np * 4));
+  KMA_HIP(b.alloc(&d_alpha, 4));
+  KMA_HIP(hipMemcpy(d_res, residues + base, total, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(d_res + total, 0, 64));
+  KMA_HIP(hipMemcpy(d_off, rel.data(), (n_seq + 1) * 8ull, hipMemcpyHostToDevice));
+  if (n_pairs) {
+    KMA_HIP(hipMemcpy(d_pa, pair_a, n_pairs * 4, hipMemcpyHostToDevice));
+    KMA_HIP(hipMemcpy(d_pb, pair_b, n_pairs * 4, hipMemcpyHostToDevice));
+  }
+  KMA_HIP(hipMemset(d_alpha, 0, 4));
+  KMA_HIP(kma::launch_window_keys(d_res, d_off, n_seq, k, (flags & KMA_F_END_EXCLUSIVE) ? 1 : 0,
+                                  d_keys, d_alpha, nullptr));
+  size_t tb = 0;
+  KMA_HIP(kma::launch_segmented_sort(nullptr, &tb, d_keys, d_sorted, total, n_seq, d_off,
+                                     d_off + 1, 5 * k, nullptr));
+  void* d_temp;
+  KMA_HIP(b.alloc(&d_temp, tb));
+  KMA_HIP(kma::launch_segmented_sort(d_temp, &tb, d_keys, d_sorted, total, n_seq, d_off,
+                                     d_off + 1, 5 * k, nullptr));
+  KMA_HIP(kma::launch_distinct(d_sorted, d_off, n_seq, d_size, nullptr));
+  if (n_pairs)
+    KMA_HIP(kma::launch_pairs(d_sorted, d_off, d_size, d_sorted, d_off, d_size, d_pa, d_pb,
+                              n_pairs, d_sim, nullptr));
+  uint32_t alpha = 0;
+  KMA_HIP(hipMemcpy(&alpha, d_alpha, 4, hipMemcpyDeviceToHost));
+  if (alpha) return fail(KMA_E_ALPHABET, "a protein window holds a byte outside A-Z and '*'");
+  std::vector<uint32_t> size(n_seq);
+  KMA_HIP(hipMemcpy(size.data(), d_size, n_seq * 4ull, hipMemcpyDeviceToHost));
+  if (out_size) std::memcpy(out_size, size.data(), n_seq * 4ull);
+  if (n_pairs) KMA_HIP(hipMemcpy(out_sim, d_sim, n_pairs * 4, hipMemcpyDeviceToHost));
+  if (out_dist)
+    for (uint64_t i = 0; i < n_pairs; ++i) {
+      // SequenceKmers.distance restated: 1 - similarity / union, 1.0 when nothing is shared
+      const uint32_t sim = out_sim[i];
+      const double uni = (double)size[pair_a[i]] + (double)size[pair_b[i]] - (double)sim;
+      out_dist[i] = sim > 0 ? 1.0 - (double)sim / uni : 1.0;
+    }
+  return KMA_OK;
+}
+
+int kma_protein_best_match(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq, int k,
+                           uint32_t flags, const uint32_t* query, const uint64_t* cand_off,
+                           const uint32_t* cand, uint32_t n_query, double max_dist, int device,
+                           int32_t* out_best, double* out_best_dist) {
+  if (n_query && (!query || !cand_off || !out_best)) return fail(KMA_E_INVALID, "null argument");
+  const uint64_t n_pairs = n_query ? cand_off[n_query] - cand_off[0] : 0;
+  if (n_pairs && !cand) return fail(KMA_E_INVALID, "null argument");
+  for (uint32_t q = 0; q < n_query; ++q)
+    if (cand_off[q + 1] < cand_off[q]) return fail(KMA_E_INVALID, "cand_off decreases at %u", q);
+  std::vector<uint32_t> pa(n_pairs), pb(n_pairs), sim(n_pairs);
+  std::vector<double> dist(n_pairs);
+  for (uint32_t q = 0; q < n_query; ++q)
+    for (uint64_t i = cand_off[q]; i < cand_off[q + 1]; ++i) {
+      pa[i - cand_off[0]] = query[q];
+      pb[i - cand_off[0]] = cand[i];
+    }
+  if (int rc = kma_protein_distances(residues, offsets, n_seq, k, flags, pa.data(), pb.data(),
+                                     n_pairs, device, sim.data(), nullptr, dist.data()))
+    return rc;
+  // GeneCopyProcessor.java:135-146: fDist = maxDist; for each candidate in order,
+  // if (f2Dist <= fDist) { fDist = f2Dist; found = f2; }
+  for (uint32_t q = 0; q < n_query; ++q) {
+    double best = max_dist;
+    int32_t found = -1;
+    for (uint64_t i = cand_off[q]; i < cand_off[q + 1]; ++i) {
+      const double d = dist[i - cand_off[0]];
+      if (d <= best) {
+        best = d;
+        found = (int32_t)cand[i];
+      }
+    }
+    out_best[q] = found;
+    if (out_best_dist) out_best_dist[q] = best;
   }
   return KMA_OK;
 }

@@ -10,29 +10,47 @@
 namespace kma {
 
 // ---- signature-table layout in HBM ------------------------------------------------------------
-// n_buckets x 64-byte buckets (n_buckets < 2^29); each bucket = 8 slots of one u64:
+// n_buckets buckets of kSlotsPerBucket slots of one u64 (8 slots = 64 bytes, the default; 16 =
+// 128 bytes, the KMA_BUCKET_SLOTS=16 build):
 //   low dword  = key bits 0..31            (never 0 for a valid key: codes are 1..31)
 //   high dword = key bits 32..39 << 24 | overflow bit << 23 | fid (23 bits)
 // A slot whose low dword is 0 is empty. A key lives in its home bucket or, if that was full,
-// in the next buckets (linear bucket probing, wrapping). The 8 overflow bits of a bucket (one
+// in the next buckets (linear bucket probing, wrapping). The overflow bits of a bucket (one
 // per slot, independent of the slot's key) form a filter of the keys homed there that live
 // further down the chain: overflow bit ovf_index(key) of the home bucket is set for each. A
 // lookup that misses its home bucket walks the chain only if its bit is set (then it stops at
-// the key or at a bucket with an empty slot), so a miss costs one 64-byte request except for
-// ~1% of keys. Every compare is a 32-bit operation.
-constexpr int kSlotsPerBucket = 8;
+// the key or at a bucket with an empty slot). Every compare is a 32-bit operation.
+// Bucket width: the chip serves random 128-byte lines at the same request rate as 64-byte ones
+// (kma_gather_bench quad2 vs quad: 5.43e10 lines/s both, profiles/r02_gather_shapes_b.jsonl),
+// but a 128-byte probe doubles the load instructions and the registers per window in flight:
+// measured slower at load factor 0.5 (c5 4.89 vs 4.48-4.63 ms, c2 70 vs 64 us), so 64-byte
+// buckets are the default and 128-byte ones a build variant for crowded tables.
+#ifndef KMA_BUCKET_SLOTS
+#define KMA_BUCKET_SLOTS 8
+#endif
+constexpr int kSlotsPerBucket = KMA_BUCKET_SLOTS;
+static_assert(kSlotsPerBucket == 8 || kSlotsPerBucket == 16, "64- or 128-byte buckets");
+constexpr int kBucketBytes = kSlotsPerBucket * 8;
+constexpr int kBucketHalves = kBucketBytes / 64;  // 64-byte pieces a quad loads per bucket
+constexpr int kSlotBits = kSlotsPerBucket == 16 ? 4 : 3;
 constexpr uint32_t kFidMask = (1u << 23) - 1;
 constexpr uint32_t kOvfBit = 1u << 23;         // in the high dword
 constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
-// K1's per-window verdict while probing: fid + 1 in bits 0..23, slot in bucket at kSlotShift.
+// The probe's per-window verdict: fid + 1 in bits 0..23, slot in bucket at kSlotShift,
+// bit 31 = the key's overflow bit in its home bucket.
 constexpr uint32_t kWordFid = (1u << 24) - 1;
 constexpr uint32_t kSlotShift = 24;
+constexpr uint32_t kSlotMask = kSlotsPerBucket - 1;
+// Buckets per table: slot ids (bucket * slots + slot) stay 32-bit.
+constexpr uint64_t kMaxBuckets = 1ull << (32 - kSlotBits);
 
 __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
   return ((uint64_t)((uint32_t)(key >> 32) << 24 | (fid & kFidMask)) << 32) | (uint32_t)key;
 }
 // Which slot of the home bucket carries the key's overflow bit (from the key's low dword).
-__host__ __device__ inline uint32_t ovf_index(uint32_t klo) { return (klo * 0x9E3779B1u) >> 29; }
+__host__ __device__ inline uint32_t ovf_index(uint32_t klo) {
+  return (klo * 0x9E3779B1u) >> (32 - kSlotBits);
+}
 __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
   return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
 }
@@ -61,34 +79,59 @@ __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
 
 // Home bucket = the key's MINIMIZER hashed onto [0, n_buckets) (Lemire fast range). Two
 // consecutive windows of a protein share their minimizer with probability 2/(K - m + 2)
-// (1/2 for K = 8, m = 6; 1/3 for m = 7), so they share their home bucket and one 64-byte
-// request serves both: the probe kernel walks runs of consecutive windows and requests a bucket
-// only when it changes. Exactness is kept by the full-key compare.
+// (1/2 for K = 8, m = 6; 1/3 for m = 7), so they share their home bucket and the second
+// request is served by a line the CU just fetched. Exactness is kept by the full-key compare.
+// m = 0 is the flat layout (a hash of the whole key): the fallback for tables whose keys pile
+// onto few minimizers (low-complexity or adversarial kmer sets).
 __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
-#ifdef KMA_HOME_FLAT  // A/B build only: hash of the whole key
-  const uint32_t h = mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u));
-  (void)k, (void)m;
-#else
-  const uint32_t h = mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
-#endif
+  const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
+                            : mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
   return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
 }
 
-// Minimizer length of a table of n_buckets buckets for K-mers. Keys sharing a minimizer share
-// a bucket, so the m-mer space must stay large against the table: with 20 amino acids, m = 6
-// gives 6.4e7 m-mers and overflows ~12% of keys past their home bucket at 1e8 keys, m = 7
-// keeps that at ~2.6% (and still shares a bucket between consecutive windows 1/3 of the time).
-// So m = 6 up to 2^22 buckets (16.8M keys at load factor 0.5), else 7 (m <= K). The table
-// layout depends on it; build and lookup both derive it from (K, n_buckets). Defined in
-// kma_abi.cpp (KMA_MINIMIZER=6|7 overrides it, for layout experiments only).
+// Layout (minimizer length m, 0 = flat) of a table of n_buckets buckets for K-mers. Keys
+// sharing a minimizer share a bucket, so the m-mer space must stay large against the table,
+// while consecutive windows share their minimizer (and a request) with probability
+// 1 - 2/(K - m + 2): 1/2 for m = 6, 1/3 for m = 7. Simulated home-bucket loads of uniform
+// keys at load factor 0.5: 8-slot buckets leave 1.8% of 1e7 keys and 12% of
+// 1e8 keys past their home bucket at m = 6, 1.0% / 2.5% at m = 7; 16-slot buckets 0.25% / 4.2%
+// at m = 6. So m = 6 up to kMinimizer6Buckets buckets (16.8M keys at load factor 0.5 either
+// way), else 7 (m <= K). KMA_MINIMIZER=0|6|7 in the environment forces a layout (read per
+// call: tests run every layout in one process). Defined in kma_abi.cpp.
+constexpr uint64_t kMinimizer6Buckets = kSlotsPerBucket == 16 ? (1ull << 21) : (1ull << 22);
 int minimizer_len(int k, uint64_t n_buckets);
+// The table creators also build a minimizer-layout table flat when more than this fraction of
+// its keys were displaced past their home bucket, or a chain is longer than kMaxChain buckets,
+// and keep the flat one if it halves either (kma_abi.cpp; uniform keys at load factor 0.5
+// displace 2-4% under m = 6/7 and ~1% flat; keys sharing minimizers, nearly all).
+constexpr double kMaxDisplaced = 0.15;
+constexpr uint32_t kMaxChain = 32;
 
-// ---- kernel parameter blocks ------------------------------------------------------------------
-// A protein K2 leaves to vote_long_kernel: one role (fid), hits H >= 2, its window range.
-struct PendingRec {
-  uint32_t s, fid, hits, n_win;
-  uint64_t base;  // word index of window 0 (residue offsets[0] + base)
-};
+// ---- protein path (annotate_kernel) ------------------------------------------------------------
+// One kernel: a block owns kBlockProteins consecutive proteins, probes every window of them
+// (quad-cooperative bucket gathers, kProbeWin windows per lane per step) and keeps, per
+// protein, the smallest and largest fid hit and the SET of distinct keys hit (a key's slot id
+// is its unique identity in the table) in LDS; the vote is read off those at the end. A
+// protein's set takes ceil(1.5 x windows) u32 entries of the block's kSetPool-entry LDS pool;
+// a protein that does not fit keeps its set in workspace memory instead (2 u32 per residue,
+// at its own residues' offset: disjoint per protein). No words or slot ids go to HBM.
+#ifndef KMA_BLOCK_PROTEINS
+#define KMA_BLOCK_PROTEINS 4
+#endif
+#ifndef KMA_SET_POOL
+#define KMA_SET_POOL 4096
+#endif
+#ifndef KMA_PROBE_WIN
+#define KMA_PROBE_WIN (KMA_BUCKET_SLOTS == 16 ? 1 : 3)
+#endif
+// Windows per lane per step: each costs 4 dwordx4 per bucket half (16 VGPRs per 64 bytes) in
+// flight (3 with 64-byte buckets: 70 VGPRs, 7 waves/SIMD; 4 measured 9% slower in round 1).
+constexpr int kProbeWin = KMA_PROBE_WIN;
+constexpr int kBlockProteins = KMA_BLOCK_PROTEINS;
+constexpr int kSetPool = KMA_SET_POOL;
+constexpr int kChainQ = 384;   // deferred overflow-chain walks per wave (u32 positions)
+constexpr uint32_t kGlobalSet = 0xFFFFFFFFu;  // pset[] marker: the set lives in workspace memory
+constexpr int kWavesPerBlock = 4;
 
 struct ProteinArgs {
   const uint64_t* slots;
@@ -97,9 +140,9 @@ struct ProteinArgs {
   const uint8_t* residues;
   const uint64_t* offsets;
   uint32_t n_seq;
-  uint64_t n_residues;  // offsets[n_seq] - offsets[0]
+  uint32_t n_residues;  // offsets[n_seq] - offsets[0] (< 2^32: positions are u32)
   int32_t k;
-  int32_t mlen;  // minimizer length of the table
+  int32_t mlen;  // table layout (minimizer length, 0 = flat)
   int32_t min_hits;
   uint32_t flags;
   int32_t* out_fid;
@@ -107,73 +150,8 @@ struct ProteinArgs {
   uint8_t* out_status;
   uint32_t* tally;  // may be null
   uint32_t n_fid;
-  uint32_t* hits;           // workspace: fid + 1 (0 = miss) per residue position
-  uint32_t* sids;           // workspace: slot id of the hit (the key's identity in the table)
-  uint32_t* overflow_flag;  // workspace: lengths of the two `pending` lists (K1 zeroes them)
-  struct PendingRec* pending;  // workspace: proteins left to vote_long_kernel (two lists)
-  uint32_t pending_half;       // start of the second list
-  uint64_t* scratch;        // workspace: kFallbackBlocks x kFallbackCap u64
-  uint32_t seq_lo, seq_hi;  // the segment [seq_lo, seq_hi) of proteins this launch covers
-  uint32_t reset_flag;      // K1 of the first segment clears overflow_flag
+  uint32_t* gset;   // workspace: 2 u32 per residue, sets of proteins that do not fit in LDS
 };
-
-// K1 probe kernel: kProbeWin windows per lane per step, all first-bucket loads in flight
-// (3: 70 VGPRs, 7 waves/SIMD; 4 needs 125 VGPRs and measured 9% slower at c5). The grid is
-// the resident population (hipOccupancy...); kProbeBlocksPerCU is only the fallback.
-#ifndef KMA_PROBE_WIN
-#define KMA_PROBE_WIN 3
-#endif
-#ifndef KMA_PROBE_BPC
-#define KMA_PROBE_BPC 8
-#endif
-constexpr int kProbeWin = KMA_PROBE_WIN;
-constexpr int kProbeBlocksPerCU = KMA_PROBE_BPC;
-// K1 defers overflow-chain walks to a per-wave LDS queue of kChainQ positions, resolved a
-// wave's 64 lanes at a time.
-constexpr int kChainQ = 384;
-// K2 vote kernel: kVoteWaves waves per block share the kChunk-window chunks of kVoteProteins
-// proteins (kVoteWin consecutive windows per lane per chunk; a wave's first kVoteHold chunks
-// stay in registers between the passes) and an LDS pool of kVotePool u32 set entries.
-// Proteins whose set does not fit are finished by vote_long_kernel: one block each, an LDS set
-// of kLongSet keys, else kFallbackCap keys of workspace scratch per block.
-// (The KMA_VOTE_* macros exist for tuning builds: `make variant`.)
-#ifndef KMA_VOTE_WAVES
-#define KMA_VOTE_WAVES 4
-#endif
-#ifndef KMA_VOTE_PROTEINS
-#define KMA_VOTE_PROTEINS 8
-#endif
-#ifndef KMA_VOTE_POOL
-#define KMA_VOTE_POOL 4096
-#endif
-#ifndef KMA_VOTE_HOLD
-#define KMA_VOTE_HOLD 2
-#endif
-constexpr int kWavesPerBlock = 4;
-constexpr int kVoteWin = 4;
-constexpr int kChunk = 64 * kVoteWin;
-constexpr int kVoteWaves = KMA_VOTE_WAVES;
-constexpr int kVoteProteins = KMA_VOTE_PROTEINS;
-constexpr int kVotePool = KMA_VOTE_POOL;
-constexpr int kVoteHold = KMA_VOTE_HOLD;
-constexpr int kLongSet = 8192;
-constexpr int kLongHold = 4;  // vote_long_kernel: chunks of a protein in flight per wave
-constexpr int kLongWaveSet = kLongSet * 2 / 4;  // u32 slot ids per wave in vote_long_kernel
-// K2 wave form: one protein per wave, kWaveHold chunks in flight, an LDS set slice of kWaveSet
-// u32 slot ids per wave (4 waves per block), filled to at most 3/4.
-#ifndef KMA_WAVE_HOLD
-#define KMA_WAVE_HOLD 4
-#endif
-#ifndef KMA_WAVE_SET
-#define KMA_WAVE_SET 1024
-#endif
-constexpr int kWaveHold = KMA_WAVE_HOLD;
-constexpr int kWaveSet = KMA_WAVE_SET;
-constexpr uint32_t kDeferred = 1u << 31;  // K2: set taken from the whole pool in phase 3
-constexpr uint32_t kLongCap = 0xFFFFFFFFu;  // K2: set too large for the pool (vote_long_kernel)
-constexpr int kLongBlocksPerCU = 4;
-constexpr int kFallbackBlocks = 64;
-constexpr uint32_t kFallbackCap = 1u << 17;  // u64 entries per block (1 MiB)
 
 struct ContigArgs {
   const uint64_t* slots;
@@ -195,24 +173,21 @@ struct ContigArgs {
   // KmerFactory.Strict (peg join): pass 1 counts the locations of every table key
   // (strict_pass = 1: atomicAdd per hit into slot_count[slot id], nothing else is meaningful),
   // pass 2 keeps only hits whose key has exactly one location (strict_pass = 2).
-  uint32_t* slot_count;        // n_buckets * 8, zeroed before pass 1
+  uint32_t* slot_count;        // n_buckets * kSlotsPerBucket, zeroed before pass 1
   int32_t strict_pass;         // 0 = off
   uint8_t codon_codes[64];     // by value (TCAG order): 5-bit aa code, 0 = stop
 };
 constexpr int kContigTile = 256;  // forward positions per block
 
 // ---- launchers (kma_kernels.hip) --------------------------------------------------------------
+// status[0] = table full; stats (finalize) = {entries, max chain, displaced keys}.
 hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets, int k,
                                int m, const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream);
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
-hipError_t launch_probe(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K1
-hipError_t launch_vote(const ProteinArgs& a, int n_cu, hipStream_t stream);   // K2 (segment)
-hipError_t launch_long(const ProteinArgs& a, int n_cu, hipStream_t stream);   // long proteins
-hipError_t launch_fused(const ProteinArgs& a, int n_cu, hipStream_t stream);  // K12 = K1 + K2
-uint32_t fused_min_proteins(int n_cu);  // K12 is used for batches of at least this many proteins
+hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
                               void* temp, size_t* temp_bytes, hipStream_t stream);

@@ -220,8 +220,6 @@ class ApplyKmerProcessor {
                                     status.data(), nullptr, 0),
               "kma_annotate_proteins");
       for (uint32_t i = 0; i < n; ++i) {
-        if (status[i] == KMA_STATUS_TOO_LONG)
-          throw NativeError("protein " + pegs[i]->id + " exceeds the native dedupe capacity");
         if (status[i] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
           reporter_->recordFeature(*pegs[i], db_.roles[fid[i]], count[i]);
       }

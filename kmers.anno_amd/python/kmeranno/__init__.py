@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("KMERANNO_LIB") or os.path.join(PKG_ROOT, "build", "li
 
 OK = 0
 E_INVALID, E_DEVICE, E_NOMEM, E_CAPACITY, E_ALPHABET, E_TABLE_FULL = -1, -2, -3, -4, -5, -6
-STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN, STATUS_TOO_LONG = 0, 1, 2, 3, 4
+STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN = 0, 1, 2, 3
 F_END_EXCLUSIVE, F_MULTISET = 0x1, 0x2
 MAX_K = 8
 
@@ -31,7 +31,9 @@ EXPORTS = (
     "kma_workspace_destroy", "kma_workspace_timing", "kma_workspace_timing_read",
     "kma_annotate_proteins", "kma_annotate_proteins_device", "kma_annotate_contigs",
     "kma_workspace_reserve_contigs", "kma_annotate_contigs_device", "kma_contig_window_count",
-    "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures", "kma_protein_form",
+    "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures", "kma_table_layout_for",
+    "kma_table_create_replicated", "kma_table_replicate", "kma_table_replicas",
+    "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
 )
 
 
@@ -45,7 +47,8 @@ class TableInfo(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_skipped", C.c_uint64), ("n_entries", C.c_uint64),
                 ("n_buckets", C.c_uint64), ("bytes", C.c_uint64), ("k", C.c_int32),
                 ("device", C.c_int32), ("max_probe", C.c_uint32), ("n_extra_syms", C.c_uint32),
-                ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32)]
+                ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32),
+                ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32), ("reserved", C.c_int32)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
@@ -78,8 +81,18 @@ def load(path: str | None = None):
         L.kma_table_destroy.argtypes = [_vp]
         L.kma_table_buckets_for.restype = _u64
         L.kma_table_buckets_for.argtypes = [_u64, C.c_double]
-        L.kma_table_build_device.argtypes = [_vp, _u64, _int, _vp, _vp, _vp, _u64, _vp, _vp]
-        L.kma_table_wrap_device.argtypes = [_vp, _u64, _int, _int, C.POINTER(_vp)]
+        L.kma_table_build_device.argtypes = [_vp, _u64, _int, _int, _vp, _vp, _vp, _u64, _vp,
+                                             _vp]
+        L.kma_table_wrap_device.argtypes = [_vp, _u64, _int, _int, _int, C.POINTER(_vp)]
+        L.kma_table_layout_for.argtypes = [_int, _u64]
+        L.kma_protein_distances.argtypes = [_u8p, _u64p, _u32, _int, _u32, _u32p, _u32p, _u64,
+                                            _int, _u32p, _vp, _vp]
+        L.kma_protein_best_match.argtypes = [_u8p, _u64p, _u32, _int, _u32, _u32p, _u64p, _u32p,
+                                             _u32, C.c_double, _int, _i32p, _vp]
+        L.kma_table_create_replicated.argtypes = [C.c_char_p, _u64p, _u32p, _u64, _int, _int,
+                                                  _i32p, C.c_double, C.POINTER(_vp)]
+        L.kma_table_replicate.argtypes = [_vp, _int, _i32p]
+        L.kma_table_replicas.argtypes = [_vp, C.POINTER(_int), _vp, _int]
         L.kma_table_device_ptr.argtypes = [_vp, C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
         L.kma_workspace_destroy.argtypes = [_vp]
@@ -94,7 +107,6 @@ def load(path: str | None = None):
         L.kma_annotate_contigs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _vp, _u64,
                                            C.POINTER(_u64), _vp, _u32]
         L.kma_workspace_reserve_contigs.argtypes = [_vp, _u64]
-        L.kma_protein_form.argtypes = [_vp, _u32]
         L.kma_annotate_contigs_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _vp,
                                                   _u64, _vp, _vp, _u32, _vp]
         L.kma_build_signatures.argtypes = [_u8p, _u64p, _i32p, _u32, _int, _u32, _int, _vp, _vp,
@@ -183,10 +195,36 @@ class SignatureTable:
         return cls(h), nw.value
 
     @classmethod
-    def wrap_device(cls, d_slots: int, n_buckets: int, k: int = 8, device: int = 0):
+    def from_rows_replicated(cls, kmers, fids, devices, k: int = 8, load_factor: float = 0.5):
+        """One table with a replica on each listed device (a device may repeat); host calls
+        shard their batch over the replicas."""
+        buf, off = pack_strings(kmers)
+        dv = np.ascontiguousarray(devices, np.int32)
         h = _vp()
-        _check(load().kma_table_wrap_device(d_slots, n_buckets, k, device, C.byref(h)))
+        _check(load().kma_table_create_replicated(buf.tobytes(), off,
+                                                  np.ascontiguousarray(fids, np.uint32),
+                                                  len(off) - 1, k, len(dv), dv, load_factor,
+                                                  C.byref(h)))
         return cls(h)
+
+    @classmethod
+    def wrap_device(cls, d_slots: int, n_buckets: int, k: int = 8, device: int = 0,
+                    layout: int = -1):
+        h = _vp()
+        _check(load().kma_table_wrap_device(d_slots, n_buckets, k, layout, device, C.byref(h)))
+        return cls(h)
+
+    def replicate(self, devices):
+        dv = np.ascontiguousarray(devices, np.int32)
+        _check(load().kma_table_replicate(self._h, len(dv), dv))
+
+    @property
+    def replicas(self):
+        n = _int(0)
+        _check(load().kma_table_replicas(self._h, C.byref(n), None, 0))
+        out = (C.c_int * max(n.value, 1))()
+        _check(load().kma_table_replicas(self._h, C.byref(n), out, n.value))
+        return list(out)[:n.value]
 
     @property
     def info(self) -> TableInfo:
@@ -233,13 +271,6 @@ class Workspace:
     def reserve(self, n_residues: int):
         _check(load().kma_workspace_reserve(self._h, n_residues))
 
-    def protein_form(self, n_seq: int) -> int:
-        """1 if a batch of n_seq proteins runs the fused probe + vote kernel, 0 if K1 + K2."""
-        rc = load().kma_protein_form(self._h, n_seq)
-        if rc < 0:
-            _check(rc)
-        return rc
-
     def reserve_contigs(self, n_bases: int):
         _check(load().kma_workspace_reserve_contigs(self._h, n_bases))
 
@@ -248,7 +279,7 @@ class Workspace:
         _check(load().kma_workspace_timing(self._h, int(enable)))
 
     def timing_read(self):
-        """(n_calls, probe_ms_total, vote_ms_total) since the last read; clears them."""
+        """(n_calls, kernel_ms_total, rest_ms_total) since the last read; clears them."""
         n, p, v = _u32(), C.c_double(), C.c_double()
         _check(load().kma_workspace_timing_read(self._h, C.byref(n), C.byref(p), C.byref(v)))
         return n.value, p.value, v.value
@@ -269,10 +300,22 @@ def buckets_for(n_keys: int, load_factor: float = 0.5) -> int:
     return int(load().kma_table_buckets_for(n_keys, load_factor))
 
 
+def bucket_slots() -> int:
+    """u64 slots per bucket of this build (8: 64-byte buckets; 16: the 128-byte variant)."""
+    return int(load().kma_bucket_slots())
+
+
+def layout_for(k: int, n_buckets: int) -> int:
+    """The size-derived table layout (minimizer length; 0 = flat)."""
+    return int(load().kma_table_layout_for(k, n_buckets))
+
+
 def build_device(d_slots: int, n_buckets: int, d_winner: int, d_keys: int, d_fids: int, n: int,
-                 d_status: int, stream: int = 0, k: int = 8):
-    _check(load().kma_table_build_device(d_slots, n_buckets, k, d_winner, d_keys, d_fids, n,
-                                         d_status, stream or None))
+                 d_status: int, stream: int = 0, k: int = 8, layout: int = -1):
+    """Device-resident table build; d_status (4 x u32) <- {full, entries, longest chain,
+    displaced keys}."""
+    _check(load().kma_table_build_device(d_slots, n_buckets, k, layout, d_winner, d_keys, d_fids,
+                                         n, d_status, stream or None))
 
 
 def annotate_proteins(table: SignatureTable, residues: np.ndarray, offsets: np.ndarray,
@@ -368,3 +411,37 @@ def build_signatures(residues: np.ndarray, offsets: np.ndarray, roles, k: int = 
 def contig_window_count(offsets: np.ndarray, k: int = 8) -> int:
     offsets = np.ascontiguousarray(offsets, np.uint64)
     return int(load().kma_contig_window_count(offsets, len(offsets) - 1, k))
+
+
+def protein_distances(residues, offsets, pair_a, pair_b, k: int = 8, flags: int = 0,
+                      device: int = 0):
+    """ProteinKmers.distance per pair (GeneCopyProcessor.java:137-142) on the GPU:
+    (similarity, per-protein set sizes, distances)."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    pa = np.ascontiguousarray(pair_a, np.uint32)
+    pb = np.ascontiguousarray(pair_b, np.uint32)
+    n = len(offsets) - 1
+    sim = np.empty(len(pa), np.uint32)
+    size = np.empty(n, np.uint32)
+    dist = np.empty(len(pa), np.float64)
+    _check(load().kma_protein_distances(residues, offsets, n, k, flags, pa, pb, len(pa), device,
+                                        sim, size.ctypes.data, dist.ctypes.data))
+    return sim, size, dist
+
+
+def protein_best_match(residues, offsets, query, cand_off, cand, max_dist: float, k: int = 8,
+                       flags: int = 0, device: int = 0):
+    """GeneCopyProcessor's closest-source choice (:135-146): (best index or -1, distance)."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    query = np.ascontiguousarray(query, np.uint32)
+    cand_off = np.ascontiguousarray(cand_off, np.uint64)
+    cand = np.ascontiguousarray(cand, np.uint32)
+    best = np.empty(len(query), np.int32)
+    bd = np.empty(len(query), np.float64)
+    _check(load().kma_protein_best_match(residues, offsets, len(offsets) - 1, k, flags, query,
+                                         cand_off, cand if len(cand) else np.zeros(1, np.uint32),
+                                         len(query), max_dist, device, best, bd.ctypes.data))
+    return best, bd
+

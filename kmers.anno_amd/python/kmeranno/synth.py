@@ -80,11 +80,16 @@ class SignatureSet:
     n_fid: int
 
 
-def make_table(table_size: int, n_fid: int, seed: int, k: int = 8) -> SignatureSet:
+def make_table(table_size: int, n_fid: int, seed: int, k: int = 8,
+               protos_only: bool = False) -> SignatureSet:
+    """protos_only: the prototypes alone (what a rank that receives the table by broadcast
+    needs to generate its queries); keys and fids are then empty."""
     rng = np.random.default_rng(seed)
     lens = cds_lengths()
     plen = rng.choice(lens, n_fid)
     protos = [AA[rng.integers(0, 20, int(L))] for L in plen]
+    if protos_only:
+        return SignatureSet(protos, np.zeros(0, np.uint64), np.zeros(0, np.uint32), n_fid)
     pk = [np.unique(window_keys(p, k)) for p in protos]
     all_k = np.concatenate(pk)
     all_f = np.repeat(np.arange(n_fid, dtype=np.uint32), [len(x) for x in pk])

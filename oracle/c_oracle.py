@@ -40,6 +40,11 @@ def lib():
         L.orc_table_size.argtypes = [C.c_void_p]
         L.orc_apply.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint32, C.c_int, C.c_int,
                                 C.c_uint32, _i32p, _i32p, _u8p]
+        L.orc_apply_mt.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint32, C.c_int, C.c_int,
+                                   C.c_uint32, _i32p, _i32p, _u8p, C.c_int]
+        L.orc_protein_distances.argtypes = [_u8p, _u64p, C.c_int, C.c_uint32, _u32p, _u32p,
+                                            C.c_uint64, _u32p, _u32p, _u32p,
+                                            np.ctypeslib.ndpointer(np.float64, flags="C")]
         L.orc_translate.restype = C.c_int64
         L.orc_translate.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_int, C.c_char_p]
         L.orc_contig_kmers.restype = C.c_uint64
@@ -101,6 +106,17 @@ def apply(table: Table, residues: np.ndarray, offsets: np.ndarray, k: int = 8,
     cnt = np.empty(n, np.int32)
     st = np.empty(n, np.uint8)
     lib().orc_apply(table._h, residues, offsets, n, k, min_hits, flags, fid, cnt, st)
+    return fid, cnt, st
+
+
+def apply_mt(table: Table, residues: np.ndarray, offsets: np.ndarray, k: int = 8,
+             min_hits: int = 5, flags: int = 0, threads: int = 1):
+    """orc_apply over `threads` pthreads (contiguous protein ranges; same outputs)."""
+    n = len(offsets) - 1
+    fid = np.empty(n, np.int32)
+    cnt = np.empty(n, np.int32)
+    st = np.empty(n, np.uint8)
+    lib().orc_apply_mt(table._h, residues, offsets, n, k, min_hits, flags, fid, cnt, st, threads)
     return fid, cnt, st
 
 
@@ -171,3 +187,16 @@ def build_signatures(residues, offsets, roles, k: int = 8, flags: int = 0):
     rl = np.empty(n, np.int32)
     lib().orc_build(residues, offsets, roles, n_seq, k, flags, km.ctypes.data, rl.ctypes.data, n)
     return km, rl
+
+
+def protein_distances(residues, offsets, pair_a, pair_b, k: int = 8, flags: int = 0):
+    """SequenceKmers.distance per pair: (sim, |A|, |B|, distance) arrays."""
+    pa = np.ascontiguousarray(pair_a, np.uint32)
+    pb = np.ascontiguousarray(pair_b, np.uint32)
+    n = len(pa)
+    sim, sa, sb = np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty(n, np.uint32)
+    dist = np.empty(n, np.float64)
+    lib().orc_protein_distances(residues, np.ascontiguousarray(offsets, np.uint64), k, flags,
+                                pa, pb, n, sim, sa, sb, dist)
+    return sim, sa, sb, dist
+

@@ -18,6 +18,7 @@
  *     ApplyKmerProcessor or ProteinKmers. This restatement is cross-checked against an
  *     independent pure-Python restatement (oracle/oracle_py.py) and hand-built edge cases.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -128,9 +129,10 @@ void orc_table_free(orc_table* t) {
 /* ------------------------------------------------------------------------------------------ */
 typedef struct {
   int32_t* slots; /* open addressing over window starts, -1 empty */
-  uint32_t cap;
+  uint32_t cap;   /* allocated slots */
   int32_t* order; /* distinct window starts, insertion order */
   uint32_t n;
+  uint32_t mask;  /* hash mask of the last build (its capacity - 1) */
 } kmer_set;
 
 static void kmer_set_build(kmer_set* s, const char* p, int64_t L, int K, uint32_t flags) {
@@ -147,6 +149,7 @@ static void kmer_set_build(kmer_set* s, const char* p, int64_t L, int K, uint32_
     s->cap = cap;
   }
   for (uint32_t i = 0; i < cap; i++) s->slots[i] = -1;
+  s->mask = cap - 1;
   for (int64_t i = 0; i < nwin; i++) {
     if (flags & ORC_F_MULTISET) { /* every window counts: no set semantics */
       s->order[s->n++] = (int32_t)i;
@@ -210,6 +213,49 @@ void orc_apply(const orc_table* t, const uint8_t* residues, const uint64_t* offs
   free(set.order);
 }
 
+/* The same loop over all host cores (the CPU baseline's multi-core leg):
+ * proteins are independent and the table is read-only after the load, so contiguous ranges
+ * of proteins go to n_threads pthreads, each with its own kmer set. */
+typedef struct {
+  const orc_table* t;
+  const uint8_t* residues;
+  const uint64_t* offsets;
+  uint32_t lo, hi;
+  int K, min_hits;
+  uint32_t flags;
+  int32_t *fid, *count;
+  uint8_t* status;
+} orc_apply_job;
+
+static void* orc_apply_worker(void* arg) {
+  orc_apply_job* j = (orc_apply_job*)arg;
+  orc_apply(j->t, j->residues, j->offsets + j->lo, j->hi - j->lo, j->K, j->min_hits, j->flags,
+            j->fid + j->lo, j->count + j->lo, j->status + j->lo);
+  return 0;
+}
+
+void orc_apply_mt(const orc_table* t, const uint8_t* residues, const uint64_t* offsets,
+                  uint32_t n_seq, int K, int min_hits, uint32_t flags, int32_t* out_fid,
+                  int32_t* out_count, uint8_t* out_status, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  pthread_t th[256];
+  orc_apply_job job[256];
+  for (int i = 0; i < n_threads; i++) {
+    /* interleaved chunks of 64 proteins would balance better; contiguous ranges keep each
+     * thread's residues contiguous, and protein lengths are iid in the sample */
+    job[i] = (orc_apply_job){t, residues, offsets, (uint32_t)((uint64_t)n_seq * i / n_threads),
+                             (uint32_t)((uint64_t)n_seq * (i + 1) / n_threads), K, min_hits,
+                             flags, out_fid, out_count, out_status};
+    if (pthread_create(&th[i], 0, orc_apply_worker, &job[i]) != 0) { /* run it here */
+      orc_apply_worker(&job[i]);
+      th[i] = 0;
+    }
+  }
+  for (int i = 0; i < n_threads; i++)
+    if (th[i]) pthread_join(th[i], 0);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* DnaTranslator restated (external org.theseed.proteins): codon -> amino acid by NCBI table,  */
 /* case-insensitive ACGT, any other base makes the codon 'X'.                                 */
@@ -259,15 +305,17 @@ int64_t orc_translate(const char* dna, int64_t len, int frame, int gcode, char* 
   return n;
 }
 
-/* Contig.getRSequence restated: reverse complement (case kept, other bytes -> 'n'). */
+/* Contig.getRSequence restated: reverse complement (case kept, other bytes -> 'n'). The RNA
+ * base U pairs like T (U -> A), as DnaTranslator reads U as T on the forward strand: a
+ * documented choice (both are external, parity unpinned for U); the kernel does the same. */
 void orc_reverse_complement(const char* dna, int64_t len, char* out) {
   for (int64_t i = 0; i < len; i++) {
     char c = dna[len - 1 - i], r;
     switch (c) {
       case 'a': r = 't'; break; case 'c': r = 'g'; break;
-      case 'g': r = 'c'; break; case 't': r = 'a'; break;
+      case 'g': r = 'c'; break; case 't': case 'u': r = 'a'; break;
       case 'A': r = 'T'; break; case 'C': r = 'G'; break;
-      case 'G': r = 'C'; break; case 'T': r = 'A'; break;
+      case 'G': r = 'C'; break; case 'T': case 'U': r = 'A'; break;
       default: r = 'n';
     }
     out[i] = r;
@@ -513,3 +561,43 @@ uint64_t orc_build(const uint8_t* residues, const uint64_t* offsets, const int32
   orc_table_free(m);
   return n;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* SequenceKmers.distance restated (external org.theseed.sequence, UNVERIFIED semantics), as   */
+/* GeneCopyProcessor.runCommand calls it (genome/compare/GeneCopyProcessor.java:137-142):      */
+/* similarity = |{distinct kmers of B} n {kmers of A}|, union = |A| + |B| - similarity,        */
+/* distance = 1 - similarity / union, or 1.0 when nothing is shared. Kmers are ProteinKmers    */
+/* sets of size K (i = 0..L-K; ORC_F_END_EXCLUSIVE: i < L-K).                                  */
+/* ------------------------------------------------------------------------------------------ */
+static int kmer_set_contains(const kmer_set* s, const char* p, const char* km, int K) {
+  if (s->n == 0) return 0;
+  uint32_t h = java_string_hash(km, K) & s->mask;
+  for (;;) {
+    int32_t j = s->slots[h];
+    if (j < 0) return 0;
+    if (memcmp(p + j, km, (size_t)K) == 0) return 1;
+    h = (h + 1) & s->mask;
+  }
+}
+
+void orc_protein_distances(const uint8_t* residues, const uint64_t* offsets, int K,
+                           uint32_t flags, const uint32_t* pair_a, const uint32_t* pair_b,
+                           uint64_t n_pairs, uint32_t* out_sim, uint32_t* out_size_a,
+                           uint32_t* out_size_b, double* out_dist) {
+  kmer_set sa = {0}, sb = {0};
+  flags &= ~ORC_F_MULTISET;
+  for (uint64_t i = 0; i < n_pairs; i++) {
+    const char* pa = (const char*)residues + offsets[pair_a[i]];
+    const char* pb = (const char*)residues + offsets[pair_b[i]];
+    kmer_set_build(&sa, pa, (int64_t)(offsets[pair_a[i] + 1] - offsets[pair_a[i]]), K, flags);
+    kmer_set_build(&sb, pb, (int64_t)(offsets[pair_b[i] + 1] - offsets[pair_b[i]]), K, flags);
+    uint32_t sim = 0;
+    for (uint32_t j = 0; j < sb.n; j++) sim += (uint32_t)kmer_set_contains(&sa, pa, pb + sb.order[j], K);
+    out_sim[i] = sim;
+    out_size_a[i] = sa.n;
+    out_size_b[i] = sb.n;
+    out_dist[i] = sim > 0 ? 1.0 - (double)sim / ((double)sa.n + (double)sb.n - (double)sim) : 1.0;
+  }
+  free(sa.slots), free(sa.order), free(sb.slots), free(sb.order);
+}
+

@@ -43,8 +43,10 @@ def translate(dna: str, frame: int, gcode: int) -> str:
 
 
 def reverse_complement(dna: str) -> str:
-    """Contig.getRSequence (external; KmerReference.java:166)."""
-    comp = {"a": "t", "c": "g", "g": "c", "t": "a", "A": "T", "C": "G", "G": "C", "T": "A"}
+    """Contig.getRSequence (external; KmerReference.java:166). U pairs like T (U -> A), as
+    translate reads U as T: a documented choice, parity unpinned for U."""
+    comp = {"a": "t", "c": "g", "g": "c", "t": "a", "A": "T", "C": "G", "G": "C", "T": "A",
+            "u": "a", "U": "A"}
     return "".join(comp.get(c, "n") for c in reversed(dna))
 
 
@@ -160,3 +162,24 @@ def build_signatures(prots, roles, k: int = 8, end_exclusive: bool = False):
             for km in protein_kmers(p, k, end_exclusive, False):
                 keep.pop(km, None)
     return keep
+
+
+def distance(a: str, b: str, k: int = 8, end_exclusive: bool = False) -> float:
+    """ProteinKmers(a).distance(ProteinKmers(b)) (external SequenceKmers.distance, restated;
+    GeneCopyProcessor.java:137-142): Jaccard distance of the kmer sets, 1.0 if disjoint."""
+    sa = set(protein_kmers(a, k, end_exclusive))
+    sb = set(protein_kmers(b, k, end_exclusive))
+    sim = len(sa & sb)
+    return 1.0 - sim / (len(sa) + len(sb) - sim) if sim else 1.0
+
+
+def best_match(query: str, cands, max_dist: float, k: int = 8):
+    """GeneCopyProcessor.java:135-146: (index of the last candidate with distance <= the
+    running best starting at max_dist, or -1; that distance)."""
+    best, found = max_dist, -1
+    for i, c in enumerate(cands):
+        d = distance(query, c, k)
+        if d <= best:
+            best, found = d, i
+    return found, best
+

@@ -20,8 +20,7 @@ def load(d):
         return {}
     per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in csv.DictReader(open(files[0])):
-        m = re.search(r"(probe_\w+_kernel<[^>]*>|vote_\w+kernel<[^>]*>|vote_kernel<[^>]*>|"
-                      r"annotate_kernel<[^>]*>|contigs_\w+_kernel(?:<[^>]*>)?|gather_\w+)",
+        m = re.search(r"(annotate_kernel<[^>]*>|contigs_\w+_kernel(?:<[^>]*>)?|gather_\w+)",
                       r["Kernel_Name"])
         if not m:
             continue
@@ -36,7 +35,7 @@ corr = lines * 64 / (g[gk]["FETCH_SIZE"] * 1024)
 out = {"calibration": {"kernel": gk, "lines_per_launch": lines,
                        "fetch_bytes": g[gk]["FETCH_SIZE"] * 1024, "factor": corr},
        "workloads": {}}
-for wl in ("c2", "c3", "c5"):
+for wl in ("c2", "c3", "c4", "c5"):
     f, w, t = (load(f"{root}/pmc_{wl}_{c}") for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum"))
     if not f:
         continue
@@ -49,6 +48,7 @@ for wl in ("c2", "c3", "c5"):
         miss = tc.get("TCC_MISS_sum", 0.0)
         ks[k] = {"read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
                  "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
-                 "ea_rdreq": tc.get("TCC_EA0_RDREQ_sum")}
+                 "read_requests": tc.get("TCC_EA0_RDREQ_sum"),
+                 "read_requests_32B": tc.get("TCC_EA0_RDREQ_32B_sum")}
     out["workloads"][wl] = ks
 print(json.dumps(out, indent=1))

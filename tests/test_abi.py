@@ -25,14 +25,16 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 1
+    assert native_lib.kma_abi_version() == 2
     assert isinstance(native_lib.kma_last_error(), bytes)
 
 
 def test_bucket_sizing_host_helper(native_lib):
     import kmeranno
-    assert kmeranno.buckets_for(1000, 0.5) == 250        # 2000 slots / 8
-    assert kmeranno.buckets_for(10**8, 0.75) * 8 >= 10**8 / 0.75
+    s = kmeranno.bucket_slots()
+    assert s in (8, 16)
+    assert kmeranno.buckets_for(1000, 0.5) == 2000 // s
+    assert kmeranno.buckets_for(10**8, 0.75) * s >= 10**8 / 0.75
     assert kmeranno.buckets_for(0, 0.5) == 1
 
 
@@ -46,3 +48,18 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
         o = np.array([0, L], np.uint64)
         expect = sum(2 * max(0, (L - f + 1) // 3 - 8) for f in (1, 2, 3))
         assert kmeranno.contig_window_count(o, 8) == expect, L
+
+
+def test_table_layout_host_helper(native_lib, monkeypatch):
+    """Layout choice: minimizer m = 6 up to 16.8M keys at load factor 0.5 (2^25 slots), m = 7
+    beyond; KMA_MINIMIZER forces 0 (flat), 6 or 7, read per call."""
+    import kmeranno
+    monkeypatch.delenv("KMA_MINIMIZER", raising=False)
+    nb6 = (1 << 25) // kmeranno.bucket_slots()
+    assert kmeranno.layout_for(8, nb6) == 6
+    assert kmeranno.layout_for(8, nb6 + 1) == 7
+    assert kmeranno.layout_for(5, 1 << 30) == 5  # m <= K
+    monkeypatch.setenv("KMA_MINIMIZER", "0")
+    assert kmeranno.layout_for(8, 1000) == 0
+    monkeypatch.setenv("KMA_MINIMIZER", "7")
+    assert kmeranno.layout_for(8, 1000) == 7

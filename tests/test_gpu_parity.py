@@ -2,8 +2,10 @@
 
 Apply outputs (fid, count, status) per protein and 6-frame hits (contig, left, strand,
 frame, fid) must equal the CPU restatement's on the same inputs: the committed golden
-vectors, hand-built edge cases, seeded synthetic workloads (BASELINE configs 1-2 shapes)
-and size-independent properties at larger sizes.
+vectors, hand-built edge cases, seeded synthetic workloads at the BASELINE config sizes
+(c2: 10k proteins vs a 10^7 table; c5: 10^8 table, with a 20k-protein sample checked against
+the oracle and the whole 1M batch by properties), under every table layout the library
+builds (minimizer m = 6, m = 7, flat), and size-independent properties.
 """
 import json
 import os
@@ -12,17 +14,22 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
+from helpers import restricted_oracle_table, take_proteins
 from oracle import oracle_py
 
 pytestmark = pytest.mark.gpu
 K = 8
 
 
-@pytest.fixture(autouse=True, params=["0", "1"], ids=["K1+K2", "K12"])
-def protein_form(request, monkeypatch):
-    """Every test under both protein-path forms: the two-kernel K1 + K2 pipeline and the fused
-    K12 kernel (the library picks by batch size; KMA_FUSED forces one, read per call)."""
-    monkeypatch.setenv("KMA_FUSED", request.param)
+@pytest.fixture(params=["auto", "7", "0"], ids=["m-auto", "m7", "flat"])
+def layout(request, monkeypatch):
+    """Table layouts: the size-derived minimizer layout (m = 6 up to 16.8M keys at load factor
+    0.5), the m = 7 layout of larger tables (c5), and the flat fallback (KMA_MINIMIZER is read
+    per table creation)."""
+    if request.param == "auto":
+        monkeypatch.delenv("KMA_MINIMIZER", raising=False)
+    else:
+        monkeypatch.setenv("KMA_MINIMIZER", request.param)
     return request.param
 
 
@@ -50,7 +57,16 @@ def _gpu_apply(kma, rows, prots, min_hits=5, flags=0, lf=0.5):
     return [[int(s), inv.get(int(f)), int(n)] for f, n, s in zip(fid, cnt, st)]
 
 
-def test_edge_cases_golden(kma):
+def _oracle_apply(oracle_c, rows, prots, min_hits=5, flags=0):
+    ids = _roles(rows)
+    ot = oracle_c.Table([r[0] for r in rows], [ids[r[1]] for r in rows])
+    res, off = oracle_c.pack_strings(prots)
+    efid, ecnt, est = oracle_c.apply(ot, res, off, K, min_hits, flags)
+    inv = {v: k for k, v in ids.items()}
+    return [[int(s), inv.get(int(f)), int(n)] for f, n, s in zip(efid, ecnt, est)]
+
+
+def test_edge_cases_golden(kma, layout):
     for c in json.load(open(os.path.join(GOLDEN, "apply_edge.json"))):
         got = _gpu_apply(kma, [tuple(r) for r in c["rows"]], c["proteins"], c["min_hits"],
                          c["flags"])
@@ -63,6 +79,7 @@ def test_table_info_and_alphabet(kma):
     i = t.info
     assert (i.n_rows, i.n_skipped, i.n_entries, i.k) == (4, 1, 2, 8)
     assert i.n_extra_syms == 1 and i.extra_syms[0] == ord("-")
+    assert i.n_replicas == 1 and t.replicas == [0]
     keys = t.pack(["ACDEFGHI", "ACDE-GHI", "ACDEFGH", "ACDE#GHI"])
     assert keys[0] != 0 and keys[1] != 0 and keys[2] == 0 and keys[3] == 0
     t.close()
@@ -81,7 +98,7 @@ def test_min_hits_must_be_positive(kma):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2])
-def test_config1_golden(kma, flags):
+def test_config1_golden(kma, layout, flags):
     z = np.load(os.path.join(GOLDEN, "apply_c1.npz"))
     with kma.SignatureTable.from_rows([bytes(r).decode() for r in z["table_kmers"]],
                                       z["table_fids"], K) as t:
@@ -95,9 +112,9 @@ def test_config1_golden(kma, flags):
 
 
 @pytest.mark.parametrize("lf", [0.5, 0.9, 0.95])
-def test_synthetic_vs_oracle(kma, oracle_c, lf):
-    """2,000 proteins vs a 200k-entry table (seeded), packed-key table path, two load factors
-    (0.9 forces multi-bucket probe chains)."""
+def test_synthetic_vs_oracle(kma, oracle_c, layout, lf):
+    """2,000 proteins vs a 200k-entry table (seeded), packed-key table path, load factors up
+    to 0.95 (overflow chains and filter bits)."""
     from kmeranno import synth
     wl = synth.make_workload(2000, 200_000, 2000, seed=11)
     kmers = [synth.unpack_key(x) for x in wl.keys]
@@ -105,34 +122,48 @@ def test_synthetic_vs_oracle(kma, oracle_c, lf):
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
         assert t.info.n_entries == ot.size
+        assert t.info.minimizer_len == {"auto": 6, "7": 7, "0": 0}[layout]
         if lf == 0.9:
-            assert t.info.max_probe >= 2
+            assert t.info.max_probe >= 2 and t.info.n_displaced > 0
         fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0)
     assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
     assert (st == 1).sum() > 500 and (st == 2).sum() > 50
 
 
-def test_long_proteins_global_dedupe(kma, oracle_c):
-    """Proteins with more distinct hits than the per-wave LDS set (1,536) go through the
-    global-memory dedupe pass; duplicates inside them still count once."""
+def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout):
+    """Proteins whose distinct-kmer sets do not fit the block's LDS pool keep them in workspace
+    memory: long ones, and short ones behind a long one in the same block; duplicates inside
+    them still count once."""
     rng = np.random.default_rng(3)
     aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
     prots, rows = [], []
-    for L, role in ((3000, "R1"), (6000, "R2"), (1700, "R3"), (2500, "R4")):
+    for L, role in ((3000, "R1"), (6000, "R2"), (1700, "R3"), (2500, "R4"), (90, "R5"),
+                    (2800, "R6"), (40, "R7"), (2900, "R8")):
         p = aa[rng.integers(0, 20, L)].tobytes().decode()
-        p = p + p[:900]  # repeated block: 893 duplicate windows
+        p = p + p[:min(900, L)]  # repeated block: duplicate windows
         prots.append(p)
-        rows += [(p[i:i + K], role) for i in range(0, len(p) - K + 1)]
+        rows += [(p[i:i + K], role) for i in range(0, len(p) - K + 1, 1 + (L % 3))]
     prots.append(prots[0][:1000] + prots[1][:1000])  # ambiguous long protein
+    prots += [prots[4], prots[6], prots[2]]           # small ones after a long one
     rows.reverse()
-    ids = _roles(rows)
-    ot = oracle_c.Table([r[0] for r in rows], [ids[r[1]] for r in rows])
-    res, off = oracle_c.pack_strings(prots)
-    efid, ecnt, est = oracle_c.apply(ot, res, off, K, 5, 0)
-    assert max(ecnt) > 1536
-    inv = {v: k for k, v in ids.items()}
-    got = _gpu_apply(kma, rows, prots)
-    assert got == [[int(s), inv.get(int(f)), int(n)] for f, n, s in zip(efid, ecnt, est)]
+    exp = _oracle_apply(oracle_c, rows, prots)
+    assert max(e[2] for e in exp) > 1536
+    assert _gpu_apply(kma, rows, prots) == exp
+
+
+def test_giant_proteins_any_length(kma, oracle_c):
+    """No length limit (ABI 1 returned TOO_LONG beyond 2^16 windows): proteins of 70k and
+    200k residues with repeated blocks, one role and two roles, voted exactly."""
+    rng = np.random.default_rng(17)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    a = aa[rng.integers(0, 20, 50_000)].tobytes().decode()
+    b = aa[rng.integers(0, 20, 150_000)].tobytes().decode()
+    prots = [a + a[:20_000], b + b[:50_000], a[:30_000] + b[:40_000], "ACDEFGHIKLMN"]
+    rows = [(a[i:i + K], "RA") for i in range(0, len(a) - K + 1, 2)]
+    rows += [(b[i:i + K], "RB") for i in range(1, len(b) - K + 1, 3)]
+    exp = _oracle_apply(oracle_c, rows, prots)
+    assert exp[0][0] == 1 and exp[0][2] > 20_000 and exp[2][0] == 2
+    assert _gpu_apply(kma, rows, prots) == exp
 
 
 def test_empty_and_ragged_batches(kma, oracle_c):
@@ -146,7 +177,163 @@ def test_empty_and_ragged_batches(kma, oracle_c):
     assert len(st) == 0
 
 
-def test_contigs_golden(kma):
+def test_adversarial_minimizer_keys_fall_back_flat(kma, oracle_c):
+    """Keys built to share a minimizer (every 8-mer holding one of 40 fixed 6-mers) pile onto
+    a few home buckets under the minimizer layout; the creator rebuilds the table flat, and
+    the answers stay exact."""
+    rng = np.random.default_rng(23)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+
+    def mix32(h):
+        h = h ^ (h >> np.uint64(16))
+        h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+        h = h ^ (h >> np.uint64(13))
+        h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+        return h ^ (h >> np.uint64(16))
+
+    # the 40 lowest-hash 6-mers of 200k candidates: the minimizer of any 8-mer holding one
+    cand = aa[rng.integers(0, 20, (200_000, 6))]
+    packed = np.zeros(len(cand), np.uint64)
+    for j in range(6):
+        packed = (packed << np.uint64(5)) | (cand[:, j].astype(np.uint64) - np.uint64(64))
+    h = mix32((packed * np.uint64(0x9E3779B1) + np.uint64(0x7F4A7C15)) & np.uint64(0xFFFFFFFF))
+    cores = [cand[i].tobytes().decode() for i in np.argsort(h)[:40]]
+    keys = set()
+    for c in cores:
+        for pos in range(3):
+            for x in range(400):
+                pre = "".join(chr(aa[(x // 20 ** i) % 20]) for i in range(pos))
+                suf = "".join(chr(aa[(x // 20 ** (i + pos)) % 20]) for i in range(2 - pos))
+                keys.add(pre + c + suf)
+    keys = sorted(keys)
+    rows = [(km, f"R{i % 50}") for i, km in enumerate(keys)]
+    prots = ["".join(keys[j] for j in rng.integers(0, len(keys), 30)) for _ in range(200)]
+    ids = _roles(rows)
+    with kma.SignatureTable.from_rows([r[0] for r in rows], [ids[r[1]] for r in rows], K) as t:
+        assert t.info.minimizer_len == 0, "crowded minimizer table must be rebuilt flat"
+    assert _gpu_apply(kma, rows, prots) == _oracle_apply(oracle_c, rows, prots)
+
+
+def test_replicated_table_host_fan_out(kma, oracle_c):
+    """A table with two replicas (both on device 0 here: two host threads and streams, the
+    same code path as two GPUs) shards a host call by residues; outputs and the summed tally
+    equal the single-replica call. On a multi-GPU box, replicas on devices 0 and 1 too."""
+    from kmeranno import synth
+    wl = synth.make_workload(3000, 100_000, 500, seed=29)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    with kma.SignatureTable.from_rows(kmers, wl.fids, K) as t1:
+        ref = kma.annotate_proteins(t1, wl.residues, wl.offsets, 5, 0, n_fid=500)
+    devsets = [[0, 0]] + ([[0, 1], [1, 0, 1]] if kma.device_count() > 1 else [])
+    for devs in devsets:
+        with kma.SignatureTable.from_rows_replicated(kmers, wl.fids, devs, K) as t:
+            assert t.replicas == devs and t.info.n_replicas == len(devs)
+            for _ in range(2):  # second call reuses the pooled host contexts
+                got = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0, n_fid=500)
+                for a, b in zip(got, ref):
+                    assert (a == b).all()
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
+    assert (ref[2] == est).all() and (ref[0] == efid).all() and (ref[1] == ecnt).all()
+
+
+def test_concurrent_host_callers(kma):
+    """Concurrent host calls on one table (each takes its own pooled context and stream)."""
+    import threading
+    from kmeranno import synth
+    wl = synth.make_workload(1500, 50_000, 300, seed=31)
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        ref = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0, n_fid=300)
+        errs = []
+
+        def run():
+            try:
+                for _ in range(3):
+                    got = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0, n_fid=300)
+                    assert all((a == b).all() for a, b in zip(got, ref))
+            except Exception as e:  # noqa: BLE001 - collected for the main thread
+                errs.append(e)
+
+        th = [threading.Thread(target=run) for _ in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs
+
+
+def _config_table(kma, sig, lf=0.5):
+    return kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=lf)
+
+
+def test_config2_size_vs_oracle(kma, oracle_c):
+    """BASELINE configs[1] at full size: 10k proteins vs the 10^7-entry table, bit-exact
+    against the oracle on the rows the batch can look up (tests/helpers.py)."""
+    from kmeranno import synth
+    n_seq, t_size, n_fid, seed = synth.CONFIGS["c2"]
+    sig = synth.make_table(t_size, n_fid, seed, K)
+    res, off, kinds, true_fid = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
+    with _config_table(kma, sig) as t:
+        assert t.info.n_buckets == 20_000_000 // kma.bucket_slots()
+        assert t.info.minimizer_len == 6
+        fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+    ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, res)
+    efid, ecnt, est = oracle_c.apply(ot, res, off, K, 5, 0)
+    assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    assert (tally == np.bincount(efid[est == 1], minlength=n_fid)).all()
+    assert (st == 1).sum() > 0.4 * n_seq
+
+
+@pytest.mark.timeout(600)
+def test_config5_size_sample_and_properties(kma, oracle_c):
+    """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 7 layout) and
+    the 1M-protein batch. A random 20k-protein sample of the batch is bit-exact against the
+    oracle; the whole batch is checked by properties: a second call on shuffled-size shards
+    (device entry point on pointer offsets) gives identical outputs, the tally equals the
+    called-fid histogram, and copies called are called for their own function."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    n_seq, t_size, n_fid, seed = synth.CONFIGS["c5"]
+    sig = synth.make_table(t_size, n_fid, seed, K)
+    res, off, kinds, true_fid = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
+    print(f"c5 workload generated: {len(res)} residues", flush=True)
+    dev = torch.device("cuda", 0)
+    with _config_table(kma, sig) as t:
+        assert t.info.minimizer_len == 7 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
+        assert t.info.n_entries > 0.99 * t_size
+        fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+        # property 1: the same batch cut into uneven shards through the device entry point
+        d_res = torch.from_numpy(res).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_fid = torch.empty(n_seq, dtype=torch.int32, device=dev)
+        d_cnt = torch.empty(n_seq, dtype=torch.int32, device=dev)
+        d_st = torch.empty(n_seq, dtype=torch.uint8, device=dev)
+        ws = kma.Workspace(0, int(off[-1]))
+        stream = torch.cuda.current_stream().cuda_stream
+        cuts = [0, 1, 7, 4096, 333_333, 500_001, 999_999, n_seq]
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            kma.annotate_proteins_device(t, ws, d_res.data_ptr(), d_off.data_ptr() + 8 * lo,
+                                         hi - lo, int(off[hi] - off[lo]), 5, 0,
+                                         d_fid.data_ptr() + 4 * lo, d_cnt.data_ptr() + 4 * lo,
+                                         d_st.data_ptr() + lo, 0, 0, stream)
+        torch.cuda.synchronize()
+        assert (d_fid.cpu().numpy() == fid).all() and (d_cnt.cpu().numpy() == cnt).all()
+        assert (d_st.cpu().numpy() == st).all()
+        ws.close()
+    # property 2: tally = histogram of called fids; copies called carry their own function
+    assert (tally == np.bincount(fid[st == 1], minlength=n_fid)).all()
+    copies = (kinds == 0) & (st == 1)
+    assert copies.sum() > 0.2 * n_seq  # decoy hits make many copies AMBIGUOUS at 10^8
+    assert (fid[copies] == true_fid[copies]).mean() > 0.999
+    # sample vs the oracle
+    rng = np.random.default_rng(55)
+    idx = np.sort(rng.choice(n_seq, 20_000, replace=False))
+    sres, soff = take_proteins(res, off, idx)
+    ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, sres)
+    efid, ecnt, est = oracle_c.apply(ot, sres, soff, K, 5, 0)
+    assert (st[idx] == est).all() and (fid[idx] == efid).all() and (cnt[idx] == ecnt).all()
+
+
+def test_contigs_golden(kma, layout):
     z = np.load(os.path.join(GOLDEN, "contigs_gto.npz"))
     with kma.SignatureTable.from_rows([bytes(r).decode() for r in z["table_kmers"]],
                                       z["table_fids"], K) as t:
@@ -164,13 +351,16 @@ def test_contigs_golden(kma):
 
 
 @pytest.mark.parametrize("gcode", [11, 4])
-def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, gcode):
-    """All five small.gto contigs plus boundary-length contigs and ambiguous bases: every
-    6-frame window hit equals the oracle's, and (AppTest.java:131-138) each hit's kmer is the
-    translation of the DNA at its location."""
+def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, gcode):
+    """All five small.gto contigs plus boundary-length contigs, ambiguous bases and RNA 'u'/'U'
+    bases: every 6-frame window hit equals the oracle's, and (AppTest.java:131-138) each hit's
+    kmer is the translation of the DNA at its location."""
     contigs = [c["dna"] for c in small_gto["contigs"]]
     contigs[2] = contigs[2][:50000] + "nnnNacgtRYk" + contigs[2][50000:]
     contigs += [contigs[0][100:100 + n] for n in range(20, 36)]  # 3K-4 .. 3K+11 bases
+    # RNA bases: a stretch of contig 1 as is, with t -> u, and upper case with T -> U
+    s = contigs[1][20000:26000]
+    contigs += [s, s.replace("t", "u"), s.upper().replace("T", "U")]
     dna, off = oracle_c.pack_strings(contigs)
     km, ct, lf, sd, fr = oracle_c.contig_kmers(dna, off, gcode, K)
     rng = np.random.default_rng(5)
@@ -184,8 +374,16 @@ def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, gcode):
         tab = dict(zip(t.pack(kmers).tolist(), kmers))
     for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"], hits["fid"]), e):
         assert (a == b).all()
+    # the u/U contigs hit exactly like their t/T source, on both strands
+    n = len(contigs)
+    src = hits[hits["contig"] == n - 3]
+    assert (src["strand"] == ord("-")).any() and (src["strand"] == ord("+")).any()
+    for c in (n - 2, n - 1):
+        got = hits[hits["contig"] == c]
+        assert len(got) == len(src)
+        for f in ("left", "strand", "frame", "fid"):
+            assert (got[f] == src[f]).all()
     # property: translate(getDna(loc)) == kmer, for a sample of hits
-    from kmeranno import synth
     for h in hits[rng.choice(len(hits), 500, replace=False)]:
         seq = contigs[h["contig"]][h["left"] - 1:h["left"] - 1 + 3 * K]
         if h["strand"] == ord("-"):
@@ -201,8 +399,8 @@ def test_device_api_with_torch_buffers(kma):
     wl = synth.make_workload(3000, 100_000, 1000, seed=21)
     dev = torch.device("cuda", 0)
     nb = kma.buckets_for(len(wl.keys), 0.5)
-    slots = torch.empty(nb * 8, dtype=torch.int64, device=dev)
-    winner = torch.empty(nb * 8, dtype=torch.int32, device=dev)
+    slots = torch.empty(nb * kma.bucket_slots(), dtype=torch.int64, device=dev)
+    winner = torch.empty(nb * kma.bucket_slots(), dtype=torch.int32, device=dev)
     status = torch.zeros(4, dtype=torch.int32, device=dev)
     keys = torch.from_numpy(wl.keys.view(np.int64)).to(dev)
     fids = torch.from_numpy(wl.fids.view(np.int32)).to(dev)
@@ -210,8 +408,10 @@ def test_device_api_with_torch_buffers(kma):
     kma.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(), fids.data_ptr(),
                      len(wl.keys), status.data_ptr(), stream)
     torch.cuda.synchronize()
-    assert status[0].item() == 0
+    st4 = status.cpu().numpy()
+    assert st4[0] == 0 and st4[1] == len(np.unique(wl.keys)) and st4[2] >= 1
     t = kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0)
+    assert t.info.minimizer_len == kma.layout_for(K, nb)
     n_res = int(wl.offsets[-1])
     ws = kma.Workspace(0, n_res)
     res = torch.from_numpy(wl.residues).to(dev)
@@ -230,12 +430,20 @@ def test_device_api_with_torch_buffers(kma):
     assert (fid.cpu().numpy() == hf).all() and (cnt.cpu().numpy() == hc).all()
     assert (st.cpu().numpy() == hs).all()
     assert (tally.cpu().numpy().astype(np.uint32) == ht).all()
+    # a batch whose residues start at an odd offset (blocks' spans are unaligned anyway)
+    k0 = 5
+    kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr() + 8 * k0, n - k0,
+                                 int(wl.offsets[-1] - wl.offsets[k0]), 5, 0, fid.data_ptr(),
+                                 cnt.data_ptr(), st.data_ptr(), 0, 0, stream)
+    torch.cuda.synchronize()
+    assert (fid.cpu().numpy()[:n - k0] == hf[k0:]).all()
+    assert (st.cpu().numpy()[:n - k0] == hs[k0:]).all()
     ws.close()
     t.close()
 
 
-def test_workspace_phase_timing(kma):
-    """kma_workspace_timing: per-phase hipEvent durations of device calls (probe, vote)."""
+def test_workspace_timing(kma):
+    """kma_workspace_timing: hipEvent durations of device calls (the protein kernel)."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_workload(500, 20_000, 200, seed=31)
@@ -252,8 +460,8 @@ def test_workspace_phase_timing(kma):
         for _ in range(3):
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
                                          *[o.data_ptr() for o in outs], 0, 0, stream)
-        calls, probe_ms, vote_ms = ws.timing_read()
-        assert calls == 3 and probe_ms > 0 and vote_ms > 0
+        calls, kernel_ms, rest_ms = ws.timing_read()
+        assert calls == 3 and kernel_ms > 0 and rest_ms >= 0
         assert ws.timing_read()[0] == 0
         with pytest.raises(kma.KmerAnnoError) as e:  # reservation too small
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res + 1, 5,
@@ -310,8 +518,21 @@ def test_contigs_device_api_planted_genome(kma, oracle_c):
         ws.close()
 
 
+def test_contigs_replicated_host_fan_out(kma, oracle_c):
+    """6-frame host calls on a two-replica table: contig shards, hits re-based and merged in
+    canonical order, tally rows per shard; equal to the single-replica answer."""
+    from kmeranno import synth
+    wl = synth.make_contig_workload(400_000, 9, 41, table_size=200_000, n_fid=300)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    with kma.SignatureTable.from_rows(kmers, wl.fids, K) as t1:
+        h1, t1y = kma.annotate_contigs(t1, wl.dna, wl.offsets, 11, n_fid=300)
+    with kma.SignatureTable.from_rows_replicated(kmers, wl.fids, [0, 0], K) as t2:
+        h2, t2y = kma.annotate_contigs(t2, wl.dna, wl.offsets, 11, n_fid=300)
+    assert (h1 == h2).all() and (t1y == t2y).all() and len(h1) > 1000
+
+
 @pytest.mark.parametrize("strict", [False, True])
-def test_peg_connect_small_gto_vs_oracle(kma, oracle_c, small_gto, strict):
+def test_peg_connect_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, strict):
     """A9, KmerProcessor.java:195-207: singleton peg kmers of a close genome (small.gto's pegs,
     mutated 5%, plus exact copies of five pegs so that their kmers are no longer singletons,
     and an 'X' run) joined with the 6-frame kmer map of small.gto's contigs, AGGRESSIVE and
