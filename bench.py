@@ -278,13 +278,15 @@ def timed(step, ws, args, world, stream, dev, before=None, after=None):
     ws.timing(True)
     for _ in range(args.steps):
         step()
-    n_t, kern_ms, rest_ms = ws.timing_read()
+    n_t, phases = ws.phases_read()
     ws.timing(False)
-    stats = torch.tensor([elapsed, gpu_ms, kern_ms / max(n_t, 1), rest_ms / max(n_t, 1)],
+    names = list(phases)
+    stats = torch.tensor([elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names],
                          dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    return stats.tolist()
+    v = stats.tolist()
+    return v[0], v[1], dict(zip(names, v[2:]))
 
 
 def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
@@ -315,6 +317,46 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
     return out
 
 
+def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
+    """Roofline of the protein path's dominant kernel (rank 0's shard; times are max over ranks).
+    Direct path (one kernel): one 64-B bucket line per window + 1 B per residue,
+    against the live random-64-B-request ceiling. Partitioned path: each phase's streamed bytes
+    per launch (algorithmic, from the record / result formats: 8-B records and 4-B results per
+    window; the table read once by the region sweep) against the 8 TB/s HBM spec; every phase's
+    rate is listed, the dominant one is the headline."""
+    if "annotate_kernel" in ph and len(ph) == 1:
+        return roofline("windows x 64 B + residues", workload,
+                        f"annotate_kernel<{K}, {m}, 4> (direct path: probe + sets + vote)",
+                        ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP + n_res, table_bytes,
+                        n_win, live=live)
+    alg = {"partition_kernel": (n_res + 8 * n_win, "residues + 8-B record per window"),
+           "probe_regions_kernel": (12 * n_win + table_bytes,
+                                    "8-B record + 4-B result per window + the table once"),
+           "vote_chunks_kernel": (4 * n_win, "4-B result per window")}
+    per = {k: {"ms": ph[k], "alg_bytes": b, "rule": r, "GBps": b / (ph[k] * 1e-3) / 1e9}
+           for k, (b, r) in alg.items() if ph.get(k)}
+    dom = max(per, key=lambda k: per[k]["ms"])
+    name = {"partition_kernel": f"partition_kernel<{K}, {m}>",
+            "probe_regions_kernel": f"probe_regions_kernel<{K}, {m}>",
+            "vote_chunks_kernel": "vote_chunks_kernel"}[dom]
+    traffic, reqs, src = pmc_traffic(workload, dom)
+    out = {"bound": "hbm", "achieved": per[dom]["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": per[dom]["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "
+                              "(MI355X_MICROARCH.md HBM section)") if src else None,
+           "kernel": name + " (partitioned path)", "kernel_ms": per[dom]["ms"],
+           "alg_bytes_per_launch": per[dom]["alg_bytes"], "alg_bytes_rule": per[dom]["rule"],
+           "windows_per_launch": n_win, "table_bytes": table_bytes, "phases": per}
+    if live:
+        ceil = gather_ceiling(table_bytes)
+        if ceil:
+            total = sum(ph.values())
+            out["measured_random_64B_ceiling"] = {k: ceil[k] for k in
+                                                  ("lines_per_s", "GBps", "buffer_MiB", "inflight")}
+            out["windows_per_s_vs_random_ceiling"] = n_win / (total * 1e-3) / ceil["lines_per_s"]
+    return out
+
+
 def bench_contigs(args, rank, world, dev, stream, sp):
     total_bp, n_contig, seed, t_size, n_fid = 5_000_000, 20, 3, 10_000_000, 10_000
     t0 = time.perf_counter()
@@ -339,7 +381,8 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                          n_bases, 11, d_hits.data_ptr(), cap, d_nh.data_ptr(),
                                          0, 0, sp)
 
-    elapsed, gpu_ms, k_ms, rest_ms = timed(step, ws, args, world, stream, dev)
+    elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev)
+    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["scan_emit"]
     n_hits = int(d_nh.item())
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
@@ -452,15 +495,15 @@ def main():
 
     # per-function tallies of the whole job -> rank 0, inside the timed region
     reduce = (lambda: kdist.reduce_tallies(d_tally, dst=0)) if world > 1 else None
-    elapsed, gpu_ms, k_ms, _ = timed(step, ws, args, world, stream, dev, before=d_tally.zero_,
-                                     after=reduce)
+    elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev, before=d_tally.zero_,
+                                after=reduce)
     st = d_st.cpu().numpy()
     called = int((st == kmeranno.STATUS_CALLED).sum())
     if rank == 0:
         total_lookups = (batch_windows if strong else n_win * world) * args.steps
         value = total_lookups / elapsed
         seqs = batch_seqs if strong else n_seq * world
-        kname = f"annotate_kernel<{K}, {table.info.minimizer_len}, 4>"
+        m = table.info.minimizer_len
         out = {
             "metric": METRIC, "value": value, "unit": "kmer lookups/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -479,14 +522,11 @@ def main():
             "seqs_per_s": seqs * args.steps / elapsed,
             "called_per_batch": called,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"annotate_kernel": k_ms},
+            "protein_path": "partitioned" if "probe_regions_kernel" in ph else "direct",
+            "phases_ms": ph,
         }
-        # one 64-B bucket line per probed window + 1 B per residue streamed in;
-        # rank 0's shard (the kernel time is the max over ranks)
-        out["roofline"] = roofline("windows x 64 B + residues", args.workload,
-                                   kname + " (the whole protein path: probe + sets + vote)",
-                                   k_ms, n_win * BYTES_PER_LOOKUP + n_res, table.info.bytes,
-                                   n_win, live=not args.no_extras)
+        out["roofline"] = protein_roofline(ph, args.workload, m, n_win, n_res, table.info.bytes,
+                                           live=not args.no_extras)
         if world == 1:
             if not args.no_extras:
                 ms = e2e_host(table, residues, offsets, n_fid)

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 2
+#define KMA_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -194,20 +194,32 @@ int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, 
 int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes);
 
 /* ---- workspaces -----------------------------------------------------------------------------
- * Per-stream scratch of the _device entry points. kma_workspace_reserve sizes it for calls of
- * up to n_residues residues (< 2^32 - 128; 8 bytes per residue of HBM: the distinct-kmer sets
- * of proteins too long for the kernel's LDS); it is the only call that allocates.            */
+ * Per-stream scratch of the _device entry points. kma_workspace_reserve_batch sizes it for
+ * calls of up to n_residues residues (< 2^32 - 128) and n_seq proteins: 12 bytes per residue
+ * of HBM (the distinct-kmer sets of proteins too long for LDS; the partitioned path's 8-byte
+ * records and 4-byte results), 20 bytes per protein and the partitioned path's chunk tables.
+ * kma_workspace_reserve(ws, n) = _reserve_batch(ws, n, n / 16 + 256). A call with more proteins
+ * than reserved takes the direct path. These are the only calls that allocate.              */
 int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
+int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t n_seq);
 int kma_workspace_destroy(kma_workspace* ws);
 /* Device timing of the _device calls made with this workspace: with enable = 1 each call
- * records hipEvents on its stream around its main kernel (proteins: the whole path in one
- * kernel; contigs: the 6-frame probe) and the rest (contigs: scan + emit; proteins: nothing).
- * Not for graph capture. _read synchronises on the recorded events (the last 256 calls),
- * returns their count and summed milliseconds, and clears the accumulators.                  */
+ * records hipEvents on its stream at its phase boundaries. Not for graph capture. Both reads
+ * synchronise on the recorded events (the last 256 calls) and clear the accumulators.
+ *   _phases_read : the calls laid out like the last one (same path): their count, the number
+ *                  of phases and each phase's summed milliseconds and name (static strings):
+ *                  direct protein path {annotate_kernel}; partitioned {chunking,
+ *                  partition_kernel, probe_regions_kernel, vote_chunks_kernel,
+ *                  annotate_list_kernel}; contigs {contigs_probe_kernel, scan_emit}.
+ *   _timing_read : kernel_ms = proteins: every phase / contigs: the probe; rest_ms = contigs:
+ *                  scan + emit.                                                              */
+#define KMA_MAX_PHASES 8
 int kma_workspace_timing(kma_workspace* ws, int enable);
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
                               double* rest_ms);
+int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phases,
+                              double* phase_ms, const char** phase_names);
 
 /* ---- protein annotation (ApplyKmerProcessor.java:118-148) ----------------------------------
  * residues: raw ASCII proteins concatenated; sequence s is residues[offsets[s]..offsets[s+1]).
@@ -221,7 +233,11 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
 /* Device form: every pointer is device memory on the workspace's device (the table has a
  * replica there); `d_residues` is 8-byte aligned and readable for 32 bytes past offsets[n_seq]; n_residues =
  * offsets[n_seq] - offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is
- * accumulated into, not cleared. One kernel launch, asynchronous on `stream`.                */
+ * accumulated into, not cleared. Asynchronous on `stream`. Two forms, same results: the direct
+ * path (one kernel: each window probes the table where it stands) and, for batches with >= 4
+ * windows per table bucket, the region-partitioned path (windows sorted to table regions, each
+ * region probed from one XCD's L2). KMA_PATH=direct|partitioned in the environment forces one
+ * (read per call); KMA_REGION_BITS=4..16 sets the region size (default 15: 2 MiB).           */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
                                  uint32_t n_seq, uint64_t n_residues, int min_hits,

@@ -54,6 +54,7 @@ constexpr uint64_t kResPad = 64;            // workspace positions past the last
 constexpr uint64_t kMaxResidues = (1ull << 32) - 2 * kResPad;  // positions are u32 in kernels
 using kma::kMaxBuckets;
 constexpr uint32_t kTimingRing = 256;
+constexpr int kMaxEv = 8;  // events per timed call
 
 thread_local std::string g_err;
 
@@ -234,8 +235,24 @@ std::vector<uint32_t> shard_bounds(const uint64_t* off, uint32_t n, int parts) {
 struct kma_workspace {
   int device = 0;
   int n_cu = 256;
-  uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
+  uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue; the
+                               // partitioned path's records (u64 per residue) share it
   uint64_t res_cap = 0;        // residues per call
+  // Partitioned protein path (kma_internal.h): results (u32 per residue), per-protein chunk
+  // flags / scan / direct-path list (seq_cap proteins), chunk tables (chunk_cap chunks) and the
+  // region offsets (u16 per chunk and region, for up to kMaxRegions regions).
+  uint32_t* d_pres = nullptr;
+  uint64_t* d_pflags = nullptr;
+  uint64_t* d_pexcl = nullptr;
+  uint32_t* d_plist = nullptr;
+  uint32_t* d_cfirst = nullptr;
+  uint32_t* d_cend = nullptr;
+  uint8_t* d_cfb = nullptr;
+  uint32_t* d_pcounts = nullptr;
+  uint16_t* d_runoff = nullptr;
+  void* d_ptemp = nullptr;
+  size_t ptemp_bytes = 0;
+  uint64_t seq_cap = 0, chunk_cap = 0;
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
   uint64_t* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
@@ -243,9 +260,12 @@ struct kma_workspace {
   void* d_ctemp = nullptr;
   size_t ctemp_bytes = 0;
   uint64_t contig_cap = 0;  // bases
-  // Per-phase timing (kma_workspace_timing): a ring of (start, after the main kernel, end).
+  // Per-phase timing (kma_workspace_timing): a ring of calls, each kMaxEv events (phase i runs
+  // from event i to event i + 1) and its phase names.
   bool timing = false;
   std::vector<hipEvent_t> events;
+  std::vector<const char* const*> names;  // per ring slot
+  std::vector<int> n_phases;              // per ring slot
   uint32_t n_timed = 0;
 };
 
@@ -710,6 +730,22 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 }  // extern "C"
 
 namespace {
+void free_protein_scratch(kma_workspace* ws) {
+  for (void* p : {(void*)ws->d_gset, (void*)ws->d_pres, (void*)ws->d_pflags, (void*)ws->d_pexcl,
+                  (void*)ws->d_plist, (void*)ws->d_cfirst, (void*)ws->d_cend, (void*)ws->d_cfb,
+                  (void*)ws->d_pcounts, (void*)ws->d_runoff, ws->d_ptemp})
+    if (p) (void)hipFree(p);
+  ws->d_gset = nullptr;
+  ws->d_pres = nullptr;
+  ws->d_pflags = ws->d_pexcl = nullptr;
+  ws->d_plist = ws->d_cfirst = ws->d_cend = ws->d_pcounts = nullptr;
+  ws->d_cfb = nullptr;
+  ws->d_runoff = nullptr;
+  ws->d_ptemp = nullptr;
+  ws->ptemp_bytes = 0;
+  ws->res_cap = ws->seq_cap = ws->chunk_cap = 0;
+}
+
 void free_contig_scratch(kma_workspace* ws) {
   for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix, ws->d_ctemp})
     if (p) (void)hipFree(p);
@@ -761,6 +797,51 @@ int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64
   return KMA_OK;
 }
 
+// Records the phase boundaries of one timed device call (nothing when timing is off).
+struct PhaseClock {
+  hipEvent_t* ev = nullptr;
+  int n = 0;
+  hipStream_t s = nullptr;
+  PhaseClock(kma_workspace* ws, hipStream_t stream, const char* const* names, int n_phases)
+      : s(stream) {
+    if (!ws->timing) return;
+    const uint32_t slot = ws->n_timed++ % kTimingRing;
+    ev = &ws->events[kMaxEv * slot];
+    ws->names[slot] = names;
+    ws->n_phases[slot] = n_phases;
+  }
+  hipError_t mark() { return ev ? hipEventRecord(ev[n++], s) : hipSuccess; }
+};
+
+const char* const kDirectPhases[] = {"annotate_kernel"};
+const char* const kPartPhases[] = {"chunking", "partition_kernel", "probe_regions_kernel",
+                                   "vote_chunks_kernel", "annotate_list_kernel"};
+const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
+
+// Region bits of the partitioned path (KMA_REGION_BITS=4..16 overrides, read per call).
+int region_bits() {
+  const char* e = getenv("KMA_REGION_BITS");
+  const int v = (e && *e) ? atoi(e) : 0;
+  return (v >= 4 && v <= 16) ? v : kma::kRegionBits;
+}
+
+// Which protein path a device call takes: 1 = partitioned (kma_internal.h), 0 = direct.
+// KMA_PATH=direct|partitioned forces it (read per call, so that tests run both in one
+// process); automatic: partitioned when the batch has >= 4 windows per table bucket (each
+// bucket line is then reused from L2 several times) and the table cuts into kMinRegions ..
+// kMaxRegions regions.
+int protein_path(const kma_table* t, const kma_workspace* ws, uint32_t n_seq, uint64_t n_res,
+                 int rb) {
+  const uint64_t regions = (t->n_buckets + (1ull << rb) - 1) >> rb;
+  const bool fits = regions <= (uint64_t)kma::kMaxRegions && n_seq <= ws->seq_cap &&
+                    kma::chunk_bound(n_res, n_seq) <= ws->chunk_cap && ws->d_pres != nullptr &&
+                    t->k <= 8;
+  const char* e = getenv("KMA_PATH");
+  if (e && !strcmp(e, "direct")) return 0;
+  if (e && !strcmp(e, "partitioned")) return fits ? 1 : 0;
+  return fits && regions >= (uint64_t)kma::kMinRegions && n_res >= 4 * t->n_buckets ? 1 : 0;
+}
+
 // The protein path on one replica (device buffers, asynchronous on s).
 int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws,
                          const uint8_t* d_residues, const uint64_t* d_offsets, uint32_t n_seq,
@@ -785,16 +866,63 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
-  hipEvent_t* ev = nullptr;
-  if (ws->timing) {
-    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
-    KMA_HIP(hipEventRecord(ev[0], s));
+  const int rb = region_bits();
+  if (!protein_path(t, ws, n_seq, n_residues, rb)) {
+    PhaseClock clk(ws, s, kDirectPhases, 1);
+    KMA_HIP(clk.mark());
+    KMA_HIP(kma::launch_annotate(a, s));
+    KMA_HIP(clk.mark());
+    return KMA_OK;
   }
-  KMA_HIP(kma::launch_annotate(a, s));
-  if (ev) {
-    KMA_HIP(hipEventRecord(ev[1], s));
-    KMA_HIP(hipEventRecord(ev[2], s));
-  }
+  kma::PartArgs p{};
+  p.slots = r.d_slots;
+  p.n_buckets = (uint32_t)t->n_buckets;
+  p.lut = r.d_lut;
+  p.residues = d_residues;
+  p.offsets = d_offsets;
+  p.n_seq = n_seq;
+  p.k = t->k;
+  p.mlen = t->mlen;
+  p.region_bits = rb;
+  p.n_regions = (uint32_t)((t->n_buckets + (1ull << rb) - 1) >> rb);
+  p.min_hits = min_hits;
+  p.flags = flags;
+  p.chunk_flags = ws->d_pflags;
+  p.chunk_excl = ws->d_pexcl;
+  p.chunk_first = ws->d_cfirst;
+  p.chunk_end = ws->d_cend;
+  p.chunk_fb = ws->d_cfb;
+  p.counts = ws->d_pcounts;
+  p.list = ws->d_plist;
+  p.run_off = ws->d_runoff;
+  p.rec = reinterpret_cast<uint64_t*>(ws->d_gset);
+  p.res = ws->d_pres;
+  p.out_fid = d_fid;
+  p.out_count = d_count;
+  p.out_status = d_status;
+  p.tally = d_tally;
+  p.n_fid = d_tally ? n_fid : 0;
+  const int cu = ws->n_cu;
+  // P2: whole XCD groups, enough blocks that one holds <= kMaxRunsPerBlock chunks.
+  const uint64_t nb_min = (kma::chunk_bound(n_residues, n_seq) + kma::kMaxRunsPerBlock - 1) /
+                          kma::kMaxRunsPerBlock;
+  const uint64_t nb = std::max<uint64_t>(
+      nb_min, (uint64_t)std::max(1, cu / 8) * kma::partition_occupancy(t->k, t->mlen, 1));
+  PhaseClock clk(ws, s, kPartPhases, 5);
+  KMA_HIP(clk.mark());
+  size_t tb = ws->ptemp_bytes;
+  KMA_HIP(kma::launch_chunking(p, ws->d_ptemp, &tb, s));
+  KMA_HIP(clk.mark());
+  KMA_HIP(kma::launch_partition(p, (unsigned)(cu * kma::partition_occupancy(t->k, t->mlen, 0)), s));
+  KMA_HIP(clk.mark());
+  KMA_HIP(kma::launch_probe_regions(p, (unsigned)(8 * nb), s));
+  KMA_HIP(clk.mark());
+  KMA_HIP(kma::launch_vote_chunks(p, (unsigned)(cu * kma::partition_occupancy(t->k, t->mlen, 2)), s));
+  KMA_HIP(clk.mark());
+  a.list = ws->d_plist;
+  a.list_n = ws->d_pcounts + 1;
+  KMA_HIP(kma::launch_annotate_list(a, (unsigned)(2 * cu), s));
+  KMA_HIP(clk.mark());
   return KMA_OK;
 }
 
@@ -829,7 +957,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   KMA_HIP(c->d_out.reserve(out_bytes));
   KMA_HIP(c->h_in.reserve(in_bytes + off_bytes));
   KMA_HIP(c->h_out.reserve(out_bytes));
-  if (int rc = kma_workspace_reserve(c->ws, nres)) return rc;
+  if (int rc = kma_workspace_reserve_batch(c->ws, nres, n)) return rc;
   // Stage: residues (zero padded) then rebased offsets, in one pinned buffer.
   uint8_t* hin = c->h_in.p;
   std::memcpy(hin, residues + base, nres);
@@ -901,18 +1029,41 @@ int kma_workspace_create(int device, kma_workspace** out) {
 }
 
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues) {
+  return kma_workspace_reserve_batch(ws, n_residues, n_residues / 16 + 256);
+}
+
+int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t n_seq) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
   if (n_residues > kMaxResidues)
     return fail(KMA_E_INVALID, "%llu residues in one call (limit 2^32 - 128)",
                 (unsigned long long)n_residues);
-  if (ws->d_gset && n_residues <= ws->res_cap) return KMA_OK;
+  if (n_seq >= (1ull << 31)) return fail(KMA_E_INVALID, "more than 2^31 proteins in one call");
+  if (ws->d_gset && n_residues <= ws->res_cap && n_seq <= ws->seq_cap) return KMA_OK;
   DeviceScope ds(ws->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
-  if (ws->d_gset) (void)hipFree(ws->d_gset);
-  ws->d_gset = nullptr;
-  ws->res_cap = 0;
+  n_residues = std::max<uint64_t>(n_residues, ws->res_cap);
+  n_seq = std::max<uint64_t>(n_seq, ws->seq_cap);
+  free_protein_scratch(ws);
+  const uint64_t chunks = kma::chunk_bound(n_residues, n_seq);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
+  KMA_HIP(hipMalloc(&ws->d_pres, (n_residues + kResPad) * 4));
+  KMA_HIP(hipMalloc(&ws->d_pflags, (n_seq + 1) * 8));
+  KMA_HIP(hipMalloc(&ws->d_pexcl, (n_seq + 1) * 8));
+  KMA_HIP(hipMalloc(&ws->d_plist, (n_seq + 1) * 4));
+  KMA_HIP(hipMalloc(&ws->d_cfirst, chunks * 4));
+  KMA_HIP(hipMalloc(&ws->d_cend, chunks * 4));
+  KMA_HIP(hipMalloc(&ws->d_cfb, chunks));
+  KMA_HIP(hipMalloc(&ws->d_pcounts, 16));
+  KMA_HIP(hipMalloc(&ws->d_runoff, chunks * (kma::kMaxRegions + 1) * 2));
+  kma::PartArgs q{};
+  q.n_seq = (uint32_t)std::max<uint64_t>(n_seq, 1);
+  size_t tb = 0;
+  KMA_HIP(kma::launch_chunking(q, nullptr, &tb, nullptr));
+  KMA_HIP(hipMalloc(&ws->d_ptemp, tb ? tb : 1));
+  ws->ptemp_bytes = tb;
   ws->res_cap = n_residues;
+  ws->seq_cap = n_seq;
+  ws->chunk_cap = chunks;
   return KMA_OK;
 }
 
@@ -920,10 +1071,45 @@ int kma_workspace_timing(kma_workspace* ws, int enable) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
   DeviceScope ds(ws->device);
   if (enable && ws->events.empty()) {
-    ws->events.resize(3 * kTimingRing);
+    ws->events.resize(kMaxEv * kTimingRing);
     for (auto& e : ws->events) KMA_HIP(hipEventCreate(&e));
+    ws->names.assign(kTimingRing, nullptr);
+    ws->n_phases.assign(kTimingRing, 0);
   }
   ws->timing = enable != 0;
+  ws->n_timed = 0;
+  return KMA_OK;
+}
+
+int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phases,
+                              double* phase_ms, const char** phase_names) {
+  if (!ws || !n_calls || !n_phases || !phase_ms) return fail(KMA_E_INVALID, "null argument");
+  DeviceScope ds(ws->device);
+  const uint32_t n = std::min(ws->n_timed, kTimingRing);
+  *n_calls = 0;
+  *n_phases = 0;
+  for (int i = 0; i < KMA_MAX_PHASES; ++i) {
+    phase_ms[i] = 0.0;
+    if (phase_names) phase_names[i] = nullptr;
+  }
+  if (n == 0) return KMA_OK;
+  const uint32_t last = (ws->n_timed - 1) % kTimingRing;  // calls laid out like the last one
+  const char* const* names = ws->names[last];
+  const int np = ws->n_phases[last];
+  for (uint32_t i = 0; i < n; ++i) {
+    if (ws->names[i] != names) continue;
+    hipEvent_t* e = &ws->events[kMaxEv * i];
+    KMA_HIP(hipEventSynchronize(e[np]));
+    for (int ph = 0; ph < np; ++ph) {
+      float ms = 0;
+      KMA_HIP(hipEventElapsedTime(&ms, e[ph], e[ph + 1]));
+      phase_ms[ph] += ms;
+    }
+    ++*n_calls;
+  }
+  *n_phases = np;
+  if (phase_names)
+    for (int ph = 0; ph < np; ++ph) phase_names[ph] = names[ph];
   ws->n_timed = 0;
   return KMA_OK;
 }
@@ -931,22 +1117,15 @@ int kma_workspace_timing(kma_workspace* ws, int enable) {
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
                               double* rest_ms) {
   if (!ws || !n_calls || !kernel_ms || !rest_ms) return fail(KMA_E_INVALID, "null argument");
-  DeviceScope ds(ws->device);
-  const uint32_t n = std::min(ws->n_timed, kTimingRing);
-  double p = 0, v = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    hipEvent_t* e = &ws->events[3 * i];
-    KMA_HIP(hipEventSynchronize(e[2]));
-    float a = 0, b = 0;
-    KMA_HIP(hipEventElapsedTime(&a, e[0], e[1]));
-    KMA_HIP(hipEventElapsedTime(&b, e[1], e[2]));
-    p += a;
-    v += b;
-  }
-  *n_calls = n;
-  *kernel_ms = p;
-  *rest_ms = v;
-  ws->n_timed = 0;
+  double ms[KMA_MAX_PHASES];
+  const char* names[KMA_MAX_PHASES];
+  int np = 0;
+  if (int rc = kma_workspace_phases_read(ws, n_calls, &np, ms, names)) return rc;
+  // contigs: (probe, scan + emit); proteins: the whole path (every phase), nothing after it
+  const bool contigs = np > 0 && names[0] == kContigPhases[0];
+  *kernel_ms = 0;
+  *rest_ms = 0;
+  for (int ph = 0; ph < np; ++ph) (contigs && ph > 0 ? *rest_ms : *kernel_ms) += ms[ph];
   return KMA_OK;
 }
 
@@ -954,7 +1133,7 @@ int kma_workspace_destroy(kma_workspace* ws) {
   if (!ws) return KMA_OK;
   DeviceScope ds(ws->device);
   for (auto& e : ws->events) (void)hipEventDestroy(e);
-  if (ws->d_gset) (void)hipFree(ws->d_gset);
+  free_protein_scratch(ws);
   free_contig_scratch(ws);
   delete ws;
   return KMA_OK;
@@ -1045,18 +1224,15 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
                 (unsigned long long)ws->contig_cap, (unsigned long long)n_bases);
   const kma::ContigArgs a =
       contig_args(t, *r, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid);
-  hipEvent_t* ev = nullptr;  // timing mode: (start, after the probe kernel, end)
-  if (ws->timing) {
-    ev = &ws->events[3 * (ws->n_timed++ % kTimingRing)];
-    KMA_HIP(hipEventRecord(ev[0], s));
-  }
+  PhaseClock clk(ws, s, kContigPhases, 2);
+  KMA_HIP(clk.mark());
   const uint64_t nb = contig_blocks(n_bases);
   KMA_HIP(kma::launch_contigs_probe(a, nb, s));
-  if (ev) KMA_HIP(hipEventRecord(ev[1], s));
+  KMA_HIP(clk.mark());
   size_t tb = ws->ctemp_bytes;
   KMA_HIP(kma::launch_contig_scan(ws->d_ccounts, ws->d_cprefix, nb, ws->d_ctemp, &tb, s));
   const int rc = enqueue_contig_emit(a, d_hits, cap, d_n_hits, s);
-  if (rc == KMA_OK && ev) KMA_HIP(hipEventRecord(ev[2], s));
+  if (rc == KMA_OK) KMA_HIP(clk.mark());
   return rc;
 }
 

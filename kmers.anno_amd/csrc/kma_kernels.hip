@@ -20,123 +20,12 @@
 
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
+#include "kma_device.h"
 
 
 namespace kma {
 namespace {
 
-// Wave-wide reductions (all 64 lanes active; result wave-uniform): DPP inside each row of 16
-// lanes (quad swaps, half-row and row mirrors: ALU-speed, no LDS round trip as ds_bpermute
-// takes), then the four row results by readlane.
-template <typename Op>
-__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, Op op) {
-  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
-  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false));   // [2,3,0,1]
-  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false));  // half mirror
-  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false));  // row mirror
-  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
-  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-  return op(op(r0, r1), op(r2, r3));
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  return wave_reduce(v, [](uint32_t x, uint32_t y) { return x + y; });
-}
-// Number of set bits of m in lanes below this lane (v_mbcnt).
-__device__ __forceinline__ uint32_t popc_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// The residues of the window starting at byte `pos` as one little-endian u64 (byte j = residue
-// j). Two aligned 8-byte loads + a funnel shift: consecutive lanes read consecutive words.
-__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
-  return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
-}
-__device__ __forceinline__ uint64_t window_bytes(const uint8_t* __restrict__ res, uint64_t pos) {
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
-  return funnel(src[0], src[1], (uint32_t)(pos & 7) * 8u);
-}
-// The two aligned words of a window, combined later (funnel) so that the load is not consumed
-// in the step that issues it.
-struct WinWords {
-  uint64_t lo, hi;
-  uint32_t sh;
-};
-__device__ __forceinline__ WinWords window_words(const uint8_t* __restrict__ res, uint64_t pos) {
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
-  return WinWords{src[0], src[1], (uint32_t)(pos & 7) * 8u};
-}
-
-// 5-bit packing through the table's residue LUT (LDS); false if a byte is not encodable.
-template <int K>
-__device__ __forceinline__ bool pack_window(const uint8_t* lut, uint64_t bytes, uint64_t& key) {
-  uint32_t c[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) c[j] = lut[(uint32_t)(bytes >> (8 * j)) & 0xFFu];
-  uint64_t v = 0;
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    ok = ok && c[j] != 0u;
-    v = (v << 5) | c[j];
-  }
-  key = v;
-  return ok;
-}
-
-// One lane's scan of a whole bucket (the rare chain walk): the bucket's slots are loaded 64
-// bytes at a time (4 dwordx4) and compared; hit (+ fid, slot index) / empty slot seen.
-constexpr int kBucketQuads = kBucketBytes / 16;  // dwordx4 pieces per bucket
-__device__ __forceinline__ void scan_half(const uint4 (&q)[4], int half, uint64_t key, bool& hit,
-                                          bool& empty, uint32_t& fid, uint32_t& slot) {
-  const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32) << 24;
-  const uint32_t lo[8] = {q[0].x, q[0].z, q[1].x, q[1].z, q[2].x, q[2].z, q[3].x, q[3].z};
-  const uint32_t hi[8] = {q[0].y, q[0].w, q[1].y, q[1].w, q[2].y, q[2].w, q[3].y, q[3].w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool m = lo[j] == klo && (hi[j] & kKeyHiMask) == khi;
-    fid = m ? (hi[j] & kFidMask) : fid;
-    slot = m ? (uint32_t)(8 * half + j) : slot;
-    hit = hit || m;
-    empty = empty || lo[j] == 0u;
-  }
-}
-
-__device__ __forceinline__ void scan_bucket(const uint64_t* __restrict__ slots, uint32_t b,
-                                            uint64_t key, bool& hit, bool& empty, uint32_t& fid,
-                                            uint32_t& slot) {
-  const uint4* bp = reinterpret_cast<const uint4*>(slots + (uint64_t)b * kSlotsPerBucket);
-  hit = false;
-  empty = false;
-#pragma unroll
-  for (int half = 0; half < kBucketHalves; ++half) {
-    uint4 q[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q[i] = bp[4 * half + i];
-    scan_half(q, half, key, hit, empty, fid, slot);
-  }
-}
-
-// Walk the overflow chain after home bucket `b` (the key missed there and its overflow bit is
-// set): stop at the key or at the first bucket with an empty slot. Returns true on a hit, with
-// the key's fid and slot id (bucket * slots + slot: the key's identity in this table).
-__device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, uint32_t n_buckets,
-                                           uint32_t b, uint64_t key, uint32_t& fid,
-                                           uint32_t& sid) {
-  bool hit = false, empty = false;
-  uint32_t slot = 0;
-  for (uint32_t step = 1; step < n_buckets && !hit && !empty; ++step) {  // bounded
-    b = (b + 1 == n_buckets) ? 0 : b + 1;
-    scan_bucket(slots, b, key, hit, empty, fid, slot);
-  }
-  sid = b * kSlotsPerBucket + slot;
-  return hit;
-}
 
 // ---------------------------------------------------------------------------------------------
 // Table construction. Insert: claim the first empty slot of the probe chain with a 64-bit CAS
@@ -237,63 +126,6 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 // of workspace memory (2 u32 per residue at its residues' offset), so any protein length is
 // voted exactly. Windows that straddle two proteins are not probed.
 // ---------------------------------------------------------------------------------------------
-template <int R>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, R * 0x55, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint32_t quad_or(uint32_t v) {
-  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
-  return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-}
-
-// One quad's verdict on a bucket it loaded cooperatively: lane `part` holds slots 2part and
-// 2part + 1 of each 64-byte half h of the bucket in v[h] (slots 8h + 2part, 8h + 2part + 1)
-// for key (kl, kh): fid + 1 of the matching slot in bits 0..23 (0 = not in this bucket), the
-// slot's index in the bucket from bit 24, and bit 31 = the key's overflow bit (chain walk
-// needed if there is no match). Keys are unique in a table, so at most one lane matches and OR
-// is the reduction. Every lane of the quad must call it (DPP). Branch-free on purpose: a
-// short-circuit here lets the compiler split the 16-byte loads into a lazily loaded tail
-// behind a branch and a vmcnt(0).
-__device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
-                                               uint32_t kh, uint32_t part) {
-  if constexpr (kBucketHalves == 1) {  // 64-byte buckets (fewest registers)
-    const uint4 x = v[0];
-    const uint32_t m0 = (uint32_t)(x.x == kl) & (uint32_t)((x.y & kKeyHiMask) == kh);
-    const uint32_t m1 = (uint32_t)(x.z == kl) & (uint32_t)((x.w & kKeyHiMask) == kh);
-    uint32_t w = (m0 * ((x.y & kFidMask) + 1u)) | (m1 * ((x.w & kFidMask) + 1u));
-    w |= (m0 | m1) * ((2u * part + m1) << kSlotShift);  // slot within the bucket
-    const uint32_t ob = ovf_index(kl);
-    const uint32_t hi = (ob & 1u) ? x.w : x.y;
-    w |= (uint32_t)((ob >> 1) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
-    return quad_or(w);
-  }
-  uint32_t w = 0;
-#pragma unroll
-  for (int h = 0; h < kBucketHalves; ++h) {
-    const uint32_t m0 = (uint32_t)(v[h].x == kl) & (uint32_t)((v[h].y & kKeyHiMask) == kh);
-    const uint32_t m1 = (uint32_t)(v[h].z == kl) & (uint32_t)((v[h].w & kKeyHiMask) == kh);
-    w |= (m0 * ((v[h].y & kFidMask) + 1u)) | (m1 * ((v[h].w & kFidMask) + 1u));
-    w |= (m0 | m1) * ((8u * h + 2u * part + m1) << kSlotShift);  // slot within the bucket
-  }
-  const uint32_t ob = ovf_index(kl);  // slot 8h + 2p + (0|1) carries the key's filter bit
-  uint32_t hi = 0;
-#pragma unroll
-  for (int h = 0; h < kBucketHalves; ++h)
-    hi = (ob >> 3) == (uint32_t)h ? ((ob & 1u) ? v[h].w : v[h].y) : hi;
-  w |= (uint32_t)(((ob >> 1) & 3u) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
-  return quad_or(w);
-}
-
-// kNone: a window that does not probe. The protein kernel packs the block's protein index
-// above the bucket index (buckets < 2^28).
-constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kBucketBits = 32 - kSlotBits;  // buckets < kMaxBuckets
-constexpr uint32_t kBucketIdx = (1u << kBucketBits) - 1u;
-
-// Set-entry index of `key` in a set of `cap` entries (fast range, any capacity).
-__device__ __forceinline__ uint32_t set_slot(uint32_t key, uint32_t cap) {
-  return (uint32_t)(((uint64_t)mix32(key * 0x9E3779B1u) * cap) >> 32);
-}
 
 // Per-block protein records (LDS). The layout keeps 7 blocks per CU resident (<= 23,405 B).
 template <int P>
@@ -359,15 +191,13 @@ __device__ __forceinline__ uint32_t protein_at(const uint32_t (&pb)[P + 1], uint
   return p;
 }
 
+// The block's proteins [p0, p0 + np) (np <= P), contiguous in the batch.
 template <int K, int M, int P>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(
-    ProteinArgs a) {
+__device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P>& sm,
+                                               const uint32_t p0, const uint32_t np) {
   constexpr int U = kProbeWin;
-  __shared__ ProteinSmem<P> sm;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
-  const uint32_t p0 = blockIdx.x * (uint32_t)P;
-  const uint32_t np = min((uint32_t)P, a.n_seq - p0);
   const uint64_t o0 = a.offsets[0];
   sm.lut[t] = a.lut[t];
   if (wave == 0) {  // the block's protein records
@@ -545,6 +375,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     a.out_fid[p0 + t] = fid_out;
     a.out_count[p0 + t] = cnt_out;
     a.out_status[p0 + t] = st;
+  }
+}
+
+template <int K, int M, int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(
+    ProteinArgs a) {
+  __shared__ ProteinSmem<P> sm;
+  const uint32_t p0 = blockIdx.x * (uint32_t)P;
+  annotate_block<K, M, P>(a, sm, p0, min((uint32_t)P, a.n_seq - p0));
+}
+
+// The direct path for a device list of proteins (giant ones, and those of partitioned-path
+// chunks that crowd one region): one protein per block step, persistent blocks.
+template <int K, int M, int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void
+annotate_list_kernel(ProteinArgs a) {
+  __shared__ ProteinSmem<P> sm;
+  const uint32_t n = *a.list_n;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    annotate_block<K, M, P>(a, sm, a.list[i], 1u);
+    __syncthreads();  // the records are read before the next protein's are written
   }
 }
 
@@ -900,32 +751,6 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
   return hipGetLastError();
 }
 
-// Kernels are instantiated per (K, layout): the minimizer length is a template parameter so
-// that the m-mer loop unrolls; layouts are m = min(K, 6), min(K, 7) and 0 (flat).
-template <int K, template <int, int> class Launch, typename... Args>
-static hipError_t dispatch_m(int m, Args&&... args) {
-  constexpr int M6 = K < 6 ? K : 6;
-  constexpr int M7 = K < 7 ? M6 : 7;
-  if (m == 0) return Launch<K, 0>::run(args...);
-  if (m == M6) return Launch<K, M6>::run(args...);
-  if (m == M7) return Launch<K, M7>::run(args...);
-  return hipErrorInvalidValue;
-}
-template <template <int, int> class Launch, typename... Args>
-static hipError_t dispatch_km(int k, int m, Args&&... args) {
-  switch (k) {
-    case 1: return dispatch_m<1, Launch>(m, args...);
-    case 2: return dispatch_m<2, Launch>(m, args...);
-    case 3: return dispatch_m<3, Launch>(m, args...);
-    case 4: return dispatch_m<4, Launch>(m, args...);
-    case 5: return dispatch_m<5, Launch>(m, args...);
-    case 6: return dispatch_m<6, Launch>(m, args...);
-    case 7: return dispatch_m<7, Launch>(m, args...);
-    case 8: return dispatch_m<8, Launch>(m, args...);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 template <int K, int M>
 struct AnnotateLaunch {
   static hipError_t run(const ProteinArgs& a, hipStream_t stream) {
@@ -939,6 +764,19 @@ struct AnnotateLaunch {
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream) {
   if (a.n_seq == 0) return hipSuccess;
   return dispatch_km<AnnotateLaunch>(a.k, a.mlen, a, stream);
+}
+
+template <int K, int M>
+struct AnnotateListLaunch {
+  static hipError_t run(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
+    hipLaunchKernelGGL((annotate_list_kernel<K, M, kBlockProteins>), dim3(blocks), dim3(256), 0,
+                       stream, a);
+    return hipGetLastError();
+  }
+};
+
+hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
+  return dispatch_km<AnnotateListLaunch>(a.k, a.mlen, a, blocks ? blocks : 1u, stream);
 }
 
 template <int K, int M>

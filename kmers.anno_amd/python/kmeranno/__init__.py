@@ -34,6 +34,7 @@ EXPORTS = (
     "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures", "kma_table_layout_for",
     "kma_table_create_replicated", "kma_table_replicate", "kma_table_replicas",
     "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
+    "kma_workspace_reserve_batch", "kma_workspace_phases_read",
 )
 
 
@@ -100,6 +101,9 @@ def load(path: str | None = None):
         L.kma_workspace_timing.argtypes = [_vp, _int]
         L.kma_workspace_timing_read.argtypes = [_vp, C.POINTER(_u32), C.POINTER(C.c_double),
                                                 C.POINTER(C.c_double)]
+        L.kma_workspace_reserve_batch.argtypes = [_vp, _u64, _u64]
+        L.kma_workspace_phases_read.argtypes = [_vp, C.POINTER(_u32), C.POINTER(_int),
+                                                C.POINTER(C.c_double), C.POINTER(C.c_char_p)]
         L.kma_annotate_proteins.argtypes = [_vp, _u8p, _u64p, _u32, _int, _u32, _i32p, _i32p,
                                             _u8p, _vp, _u32]
         L.kma_annotate_proteins_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _u32,
@@ -262,14 +266,19 @@ class SignatureTable:
 
 
 class Workspace:
-    def __init__(self, device: int = 0, n_residues: int = 0):
+    def __init__(self, device: int = 0, n_residues: int = 0, n_seq: int = 0):
         self._h = _vp()
         _check(load().kma_workspace_create(device, C.byref(self._h)))
         if n_residues:
-            self.reserve(n_residues)
+            self.reserve(n_residues, n_seq)
 
-    def reserve(self, n_residues: int):
-        _check(load().kma_workspace_reserve(self._h, n_residues))
+    def reserve(self, n_residues: int, n_seq: int = 0):
+        """Scratch for device calls of up to n_residues residues and n_seq proteins (0: the
+        library's default of n_residues / 16 + 256)."""
+        if n_seq:
+            _check(load().kma_workspace_reserve_batch(self._h, n_residues, n_seq))
+        else:
+            _check(load().kma_workspace_reserve(self._h, n_residues))
 
     def reserve_contigs(self, n_bases: int):
         _check(load().kma_workspace_reserve_contigs(self._h, n_bases))
@@ -283,6 +292,15 @@ class Workspace:
         n, p, v = _u32(), C.c_double(), C.c_double()
         _check(load().kma_workspace_timing_read(self._h, C.byref(n), C.byref(p), C.byref(v)))
         return n.value, p.value, v.value
+
+    def phases_read(self):
+        """(n_calls, {phase name: summed ms}) of the calls laid out like the last one (same
+        path) since the last read; clears them."""
+        n, k = _u32(), _int()
+        ms = (C.c_double * 8)()
+        names = (C.c_char_p * 8)()
+        _check(load().kma_workspace_phases_read(self._h, C.byref(n), C.byref(k), ms, names))
+        return n.value, {names[i].decode(): ms[i] for i in range(k.value)}
 
     def close(self):
         if self._h:

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 2
+    assert native_lib.kma_abi_version() == 3
     assert isinstance(native_lib.kma_last_error(), bytes)
 
 

@@ -33,6 +33,20 @@ def layout(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["direct", "part"])
+def path(request, monkeypatch):
+    """Protein paths: the direct kernel, and the region-partitioned path (forced, with 64-bucket
+    regions so that the small test tables still cut into hundreds of regions; chunks that crowd
+    one region fall back to the direct list kernel). KMA_PATH / KMA_REGION_BITS are read per
+    call."""
+    if request.param == "direct":
+        monkeypatch.setenv("KMA_PATH", "direct")
+    else:
+        monkeypatch.setenv("KMA_PATH", "partitioned")
+        monkeypatch.setenv("KMA_REGION_BITS", "6")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def kma(native_lib):
     import kmeranno
@@ -66,7 +80,7 @@ def _oracle_apply(oracle_c, rows, prots, min_hits=5, flags=0):
     return [[int(s), inv.get(int(f)), int(n)] for f, n, s in zip(efid, ecnt, est)]
 
 
-def test_edge_cases_golden(kma, layout):
+def test_edge_cases_golden(kma, layout, path):
     for c in json.load(open(os.path.join(GOLDEN, "apply_edge.json"))):
         got = _gpu_apply(kma, [tuple(r) for r in c["rows"]], c["proteins"], c["min_hits"],
                          c["flags"])
@@ -98,7 +112,7 @@ def test_min_hits_must_be_positive(kma):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2])
-def test_config1_golden(kma, layout, flags):
+def test_config1_golden(kma, layout, flags, path):
     z = np.load(os.path.join(GOLDEN, "apply_c1.npz"))
     with kma.SignatureTable.from_rows([bytes(r).decode() for r in z["table_kmers"]],
                                       z["table_fids"], K) as t:
@@ -111,26 +125,26 @@ def test_config1_golden(kma, layout, flags):
     assert (tally == np.bincount(called, minlength=100)).all()
 
 
-@pytest.mark.parametrize("lf", [0.5, 0.9, 0.95])
-def test_synthetic_vs_oracle(kma, oracle_c, layout, lf):
+@pytest.mark.parametrize("lf,flags", [(0.5, 0), (0.5, 1), (0.5, 2), (0.9, 0), (0.95, 0)])
+def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags):
     """2,000 proteins vs a 200k-entry table (seeded), packed-key table path, load factors up
-    to 0.95 (overflow chains and filter bits)."""
+    to 0.95 (overflow chains and filter bits), both window conventions and multiset counting."""
     from kmeranno import synth
     wl = synth.make_workload(2000, 200_000, 2000, seed=11)
     kmers = [synth.unpack_key(x) for x in wl.keys]
     ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
-    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
+    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, flags)
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
         assert t.info.n_entries == ot.size
         assert t.info.minimizer_len == {"auto": 6, "7": 7, "0": 0}[layout]
         if lf == 0.9:
             assert t.info.max_probe >= 2 and t.info.n_displaced > 0
-        fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0)
+        fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, flags)
     assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
     assert (st == 1).sum() > 500 and (st == 2).sum() > 50
 
 
-def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout):
+def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path):
     """Proteins whose distinct-kmer sets do not fit the block's LDS pool keep them in workspace
     memory: long ones, and short ones behind a long one in the same block; duplicates inside
     them still count once."""
@@ -151,7 +165,7 @@ def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout):
     assert _gpu_apply(kma, rows, prots) == exp
 
 
-def test_giant_proteins_any_length(kma, oracle_c):
+def test_giant_proteins_any_length(kma, oracle_c, path):
     """No length limit (ABI 1 returned TOO_LONG beyond 2^16 windows): proteins of 70k and
     200k residues with repeated blocks, one role and two roles, voted exactly."""
     rng = np.random.default_rng(17)
@@ -166,7 +180,7 @@ def test_giant_proteins_any_length(kma, oracle_c):
     assert _gpu_apply(kma, rows, prots) == exp
 
 
-def test_empty_and_ragged_batches(kma, oracle_c):
+def test_empty_and_ragged_batches(kma, oracle_c, path):
     rows = [("ACDEFGHI", "R1"), ("CDEFGHIK", "R1")]
     prots = ["", "ACDEFGHIK", "", "A" * 7, "ACDEFGHIK" * 40, ""]
     assert _gpu_apply(kma, rows, prots, 1) == [
@@ -177,7 +191,7 @@ def test_empty_and_ragged_batches(kma, oracle_c):
     assert len(st) == 0
 
 
-def test_adversarial_minimizer_keys_fall_back_flat(kma, oracle_c):
+def test_adversarial_minimizer_keys_fall_back_flat(kma, oracle_c, path):
     """Keys built to share a minimizer (every 8-mer holding one of 40 fixed 6-mers) pile onto
     a few home buckets under the minimizer layout; the creator rebuilds the table flat, and
     the answers stay exact."""
@@ -214,7 +228,7 @@ def test_adversarial_minimizer_keys_fall_back_flat(kma, oracle_c):
     assert _gpu_apply(kma, rows, prots) == _oracle_apply(oracle_c, rows, prots)
 
 
-def test_replicated_table_host_fan_out(kma, oracle_c):
+def test_replicated_table_host_fan_out(kma, oracle_c, path):
     """A table with two replicas (both on device 0 here: two host threads and streams, the
     same code path as two GPUs) shards a host call by residues; outputs and the summed tally
     equal the single-replica call. On a multi-GPU box, replicas on devices 0 and 1 too."""
@@ -265,7 +279,7 @@ def _config_table(kma, sig, lf=0.5):
     return kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=lf)
 
 
-def test_config2_size_vs_oracle(kma, oracle_c):
+def test_config2_size_vs_oracle(kma, oracle_c, path):
     """BASELINE configs[1] at full size: 10k proteins vs the 10^7-entry table, bit-exact
     against the oracle on the rows the batch can look up (tests/helpers.py)."""
     from kmeranno import synth
@@ -284,7 +298,7 @@ def test_config2_size_vs_oracle(kma, oracle_c):
 
 
 @pytest.mark.timeout(600)
-def test_config5_size_sample_and_properties(kma, oracle_c):
+def test_config5_size_sample_and_properties(kma, oracle_c, monkeypatch):
     """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 7 layout) and
     the 1M-protein batch. A random 20k-protein sample of the batch is bit-exact against the
     oracle; the whole batch is checked by properties: a second call on shuffled-size shards
@@ -300,7 +314,15 @@ def test_config5_size_sample_and_properties(kma, oracle_c):
     with _config_table(kma, sig) as t:
         assert t.info.minimizer_len == 7 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
         assert t.info.n_entries > 0.99 * t_size
+        monkeypatch.delenv("KMA_PATH", raising=False)  # automatic: the partitioned path here
+        monkeypatch.delenv("KMA_REGION_BITS", raising=False)
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+        # property 0: the direct path gives the same outputs on the whole batch
+        monkeypatch.setenv("KMA_PATH", "direct")
+        got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+        for a, b in zip(got, (fid, cnt, st, tally)):
+            assert (a == b).all()
+        monkeypatch.delenv("KMA_PATH")
         # property 1: the same batch cut into uneven shards through the device entry point
         d_res = torch.from_numpy(res).to(dev)
         d_off = torch.from_numpy(off.view(np.int64)).to(dev)
@@ -463,6 +485,20 @@ def test_workspace_timing(kma):
         calls, kernel_ms, rest_ms = ws.timing_read()
         assert calls == 3 and kernel_ms > 0 and rest_ms >= 0
         assert ws.timing_read()[0] == 0
+        for forced, phases in (("direct", ["annotate_kernel"]),
+                               ("partitioned", ["chunking", "partition_kernel",
+                                                "probe_regions_kernel", "vote_chunks_kernel",
+                                                "annotate_list_kernel"])):
+            os.environ["KMA_PATH"] = forced
+            try:
+                for _ in range(2):
+                    kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res,
+                                                 5, 0, *[o.data_ptr() for o in outs], 0, 0,
+                                                 stream)
+            finally:
+                del os.environ["KMA_PATH"]
+            calls, ph = ws.phases_read()
+            assert calls == 2 and list(ph) == phases and all(v >= 0 for v in ph.values())
         with pytest.raises(kma.KmerAnnoError) as e:  # reservation too small
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res + 1, 5,
                                          0, *[o.data_ptr() for o in outs], 0, 0, stream)
