@@ -293,7 +293,7 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
     """The dominant kernel's line: algorithmic bytes / duration against the 8 TB/s spec, and the
     line-request rate against the live random-gather ceiling of a buffer of the table's size."""
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, reqs, src = pmc_traffic(workload, kernel)
+    traffic, reqs, src = pmc_traffic(workload, kernel.split(" (")[0])
     ceil = gather_ceiling(table_bytes) if live else None
     out = {"bound": "hbm" if table_bytes > MALL_BYTES else "infinity-cache",
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -339,7 +339,7 @@ def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
     name = {"partition_kernel": f"partition_kernel<{K}, {m}>",
             "probe_regions_kernel": f"probe_regions_kernel<{K}, {m}>",
             "vote_chunks_kernel": "vote_chunks_kernel"}[dom]
-    traffic, reqs, src = pmc_traffic(workload, dom)
+    traffic, reqs, src = pmc_traffic(workload, name)
     out = {"bound": "hbm", "achieved": per[dom]["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": per[dom]["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
            "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "

@@ -152,6 +152,47 @@ __global__ __launch_bounds__(256) void gather_hex(const uint4* __restrict__ buf,
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// l16 / l8: each lane reads ONE random 16-byte (dwordx4) / 8-byte (dwordx2) piece: the access of
+// a fingerprint-bucket probe (is an L2-resident random read capped per line or per load?).
+template <int I, bool NT>
+__global__ __launch_bounds__(256) void gather_l16(const uint4* __restrict__ buf, uint32_t n_lines,
+                                                  uint32_t* __restrict__ sink, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n16 = n_lines * 4;
+  uint32_t acc = 0;
+  for (int r = 0; r < kSteps; r += I) {
+    uint4 v[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const uint32_t piece = (uint32_t)(((uint64_t)mix32(tid * 0x9E3779B1u + (r + j) * 0x85EBCA77u + salt) * n16) >> 32);
+      v[j] = ld<NT>(buf + piece);
+    }
+#pragma unroll
+    for (int j = 0; j < I; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int I, bool NT>
+__global__ __launch_bounds__(256) void gather_l8(const uint4* __restrict__ buf, uint32_t n_lines,
+                                                 uint32_t* __restrict__ sink, uint32_t salt) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n8 = n_lines * 8;
+  const uint2* b8 = reinterpret_cast<const uint2*>(buf);
+  uint32_t acc = 0;
+  for (int r = 0; r < kSteps; r += I) {
+    uint2 v[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const uint32_t piece = (uint32_t)(((uint64_t)mix32(tid * 0x9E3779B1u + (r + j) * 0x85EBCA77u + salt) * n8) >> 32);
+      v[j] = b8[piece];
+    }
+#pragma unroll
+    for (int j = 0; j < I; ++j) acc ^= v[j].x ^ v[j].y;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <class F>
 double time_kernel(F launch, double bytes) {
   hipEvent_t a, b;
@@ -181,6 +222,7 @@ int main(int argc, char** argv) {
   const uint64_t mib = std::strtoull(argv[1], nullptr, 10);
   const bool quad = !std::strcmp(argv[2], "quad"), oct = !std::strcmp(argv[2], "oct");
   const bool quad2 = !std::strcmp(argv[2], "quad2"), hex = !std::strcmp(argv[2], "hex");
+  const bool l16 = !std::strcmp(argv[2], "l16"), l8 = !std::strcmp(argv[2], "l8");
   const int inflight = std::atoi(argv[3]);
   const bool nt = argc > 4 && std::atoi(argv[4]);
   const int bpc = argc > 5 ? std::atoi(argv[5]) : 8;
@@ -197,7 +239,7 @@ int main(int argc, char** argv) {
   // requests (lines of the shape's size: 128 B for oct, else 64 B)
   const double lines =
       (double)blocks * 256 * kSteps / (hex ? 16 : oct ? 8 : (quad || quad2) ? 4 : 1);
-  const double line_bytes = hex ? 256 : (oct || quad2) ? 128 : 64;
+  const double line_bytes = l8 ? 8 : l16 ? 16 : hex ? 256 : (oct || quad2) ? 128 : 64;
   double gbs = 0;
 #define RUN(KERNEL, I, NTV)                                                                   \
   gbs = time_kernel([&](uint32_t salt) {                                                      \
@@ -209,7 +251,8 @@ int main(int argc, char** argv) {
   else if (inflight == 2) { if (nt) RUN(KERNEL, 2, true); else RUN(KERNEL, 2, false); } \
   else if (inflight == 4) { if (nt) RUN(KERNEL, 4, true); else RUN(KERNEL, 4, false); } \
   else if (inflight == 8) { if (nt) RUN(KERNEL, 8, true); else RUN(KERNEL, 8, false); }
-  if (hex) { CASES(gather_hex) } else if (quad2) { CASES(gather_quad2) }
+  if (l16) { CASES(gather_l16) } else if (l8) { CASES(gather_l8) }
+  else if (hex) { CASES(gather_hex) } else if (quad2) { CASES(gather_quad2) }
   else if (oct) { CASES(gather_oct) } else if (quad) { CASES(gather_quad) } else { CASES(gather_lane) }
   if (gbs == 0) {
     std::fprintf(stderr, "unsupported inflight %d\n", inflight);
@@ -219,7 +262,8 @@ int main(int argc, char** argv) {
               "\"blocks_per_cu\": %d, \"GBps\": %.1f, \"lines_per_s\": %.4g, "
               "\"lines_per_launch\": %.0f}\n",
               (unsigned long long)mib,
-              hex ? "hex" : quad2 ? "quad2" : oct ? "oct" : quad ? "quad" : "lane", inflight, (int)nt,
+              l16 ? "l16" : l8 ? "l8" : hex ? "hex" : quad2 ? "quad2" : oct ? "oct" : quad ? "quad" : "lane",
+              inflight, (int)nt,
               bpc, gbs, gbs * 1e9 / line_bytes, lines);
   CHECK(hipFree(buf));
   return 0;

@@ -839,7 +839,8 @@ int protein_path(const kma_table* t, const kma_workspace* ws, uint32_t n_seq, ui
   const char* e = getenv("KMA_PATH");
   if (e && !strcmp(e, "direct")) return 0;
   if (e && !strcmp(e, "partitioned")) return fits ? 1 : 0;
-  return fits && regions >= (uint64_t)kma::kMinRegions && n_res >= 4 * t->n_buckets ? 1 : 0;
+  (void)regions;
+  return 0;  // automatic: direct (measured faster at c4 and c5)
 }
 
 // The protein path on one replica (device buffers, asynchronous on s).
