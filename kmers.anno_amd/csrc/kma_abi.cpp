@@ -818,6 +818,16 @@ const char* const kPartPhases[] = {"chunking", "partition_kernel", "probe_region
                                    "vote_chunks_kernel", "annotate_list_kernel"};
 const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
+// Proteins per annotate_kernel block: 4 (KMA_BLOCK_PROTEINS=1..8 overrides, read per call).
+// Measured on MI355X (profiles/r02f_block_proteins.log): c2 65.1 / 65.5 / 65.6 / 73.9 us and c5
+// 4.53 / 4.53 / 4.66 / 4.86 ms for the automatic tail-minimising choice / 4 / 6 / 8 per block:
+// the partial last wave of blocks at c2 is not what bounds it, so the simple 4 stays.
+uint32_t block_proteins() {
+  const char* e = getenv("KMA_BLOCK_PROTEINS");
+  const int f = (e && *e) ? atoi(e) : 0;
+  return (f >= 1 && f <= kma::kBlockProteins) ? (uint32_t)f : 4u;
+}
+
 // Region bits of the partitioned path (KMA_REGION_BITS=4..16 overrides, read per call).
 int region_bits() {
   const char* e = getenv("KMA_REGION_BITS");
@@ -867,6 +877,7 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
+  a.block_proteins = block_proteins();
   const int rb = region_bits();
   if (!protein_path(t, ws, n_seq, n_residues, rb)) {
     PhaseClock clk(ws, s, kDirectPhases, 1);

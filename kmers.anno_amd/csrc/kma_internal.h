@@ -116,7 +116,7 @@ constexpr uint32_t kMaxChain = 32;
 // a protein that does not fit keeps its set in workspace memory instead (2 u32 per residue,
 // at its own residues' offset: disjoint per protein). No words or slot ids go to HBM.
 #ifndef KMA_BLOCK_PROTEINS
-#define KMA_BLOCK_PROTEINS 4
+#define KMA_BLOCK_PROTEINS 8
 #endif
 #ifndef KMA_SET_POOL
 #define KMA_SET_POOL 4096
@@ -151,6 +151,7 @@ struct ProteinArgs {
   uint32_t* tally;  // may be null
   uint32_t n_fid;
   uint32_t* gset;   // workspace: 2 u32 per residue, sets of proteins that do not fit in LDS
+  uint32_t block_proteins;  // proteins per block (1 .. kBlockProteins; the host sizes it)
   // List form (annotate_list_kernel): the proteins list[0 .. *list_n), one per block step.
   const uint32_t* list;
   const uint32_t* list_n;
@@ -256,6 +257,8 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
+// Resident annotate_kernel blocks per CU (occupancy API).
+int annotate_occupancy(int k, int m);
 // The direct path over a device list of proteins (a.list / a.list_n), `blocks` persistent blocks.
 hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream);
 // The partitioned path (kma_partition.hip): chunking (flags, scan, index), P1, P2, P3. temp:

@@ -382,8 +382,8 @@ template <int K, int M, int P>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(
     ProteinArgs a) {
   __shared__ ProteinSmem<P> sm;
-  const uint32_t p0 = blockIdx.x * (uint32_t)P;
-  annotate_block<K, M, P>(a, sm, p0, min((uint32_t)P, a.n_seq - p0));
+  const uint32_t p0 = blockIdx.x * a.block_proteins;
+  annotate_block<K, M, P>(a, sm, p0, min(a.block_proteins, a.n_seq - p0));
 }
 
 // The direct path for a device list of proteins (giant ones, and those of partitioned-path
@@ -755,7 +755,9 @@ template <int K, int M>
 struct AnnotateLaunch {
   static hipError_t run(const ProteinArgs& a, hipStream_t stream) {
     constexpr int P = kBlockProteins;
-    const unsigned blocks = (a.n_seq + P - 1) / P;
+    const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= (uint32_t)P ? a.block_proteins : 4u;
+    if (bp != a.block_proteins) return hipErrorInvalidValue;
+    const unsigned blocks = (a.n_seq + bp - 1) / bp;
     hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
   }
@@ -774,6 +776,19 @@ struct AnnotateListLaunch {
     return hipGetLastError();
   }
 };
+
+template <int K, int M>
+struct AnnotateOccupancy {
+  static hipError_t run(int* out) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, annotate_kernel<K, M, kBlockProteins>,
+                                                        256, 0);
+  }
+};
+int annotate_occupancy(int k, int m) {
+  int n = 0;
+  if (dispatch_km<AnnotateOccupancy>(k, m, &n) != hipSuccess || n < 1) n = 1;
+  return n;
+}
 
 hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
   return dispatch_km<AnnotateListLaunch>(a.k, a.mlen, a, blocks ? blocks : 1u, stream);
