@@ -288,6 +288,36 @@ int kma_connect_pegs(const kma_table* peg_table, const uint8_t* dna, const uint6
                      uint32_t n_contig, int genetic_code, int strict, kma_hit* out_hits,
                      uint64_t cap, uint64_t* n_hits);
 
+/* ---- proposal sweep of the projector (KmerProcessor.java:209-264) ----------------------------
+ * The connections of one close genome (kma_connect_pegs hits, fid = peg index, in its canonical
+ * (contig, left) order) are grouped into framed location lists (FramedLocationLists.connect,
+ * FramedLocationLists.java:156-171): one list per frame (strand and the phase of a location's
+ * end point) and peg, sorted by (contig, left). For peg p with protein length peg_len[p] (aa),
+ * pegLen = 3 peg_len[p], maxLen = (int)(pegLen max_fuzz + 1), minLen = (int)(pegLen min_fuzz),
+ * minKmers = (int)(pegLen (min_strength / 3)) (:222-228); a list shorter than minKmers is
+ * skipped; every start i <= size - minKmers gets evidence = 1 + #{later locations on i's contig
+ * with right < left_i + maxLen} and right = the largest such right edge (or its own), and is a
+ * proposal unless right < left_i + minLen (:233-257). Proposals come out in list order (frame
+ * '-' phases 0..2, '+' phases 0..2; peg index; start) — Java visits pegs in HashMap order.
+ * stats[4]: lists, lists with too few kmers, too-short starts, proposals. The sweep runs on
+ * `device`; KMA_E_CAPACITY with *n_out = needed if cap is too small; KMA_E_INVALID if the hits
+ * are not in (contig, left) order or a fid >= n_peg. Defaults of the reference: min_strength
+ * 0.5, max_fuzz 1.5, min_fuzz 0.8 (KmerProcessor.setDefaults, :141-146).                    */
+typedef struct kma_proposal {
+  uint32_t peg;
+  uint32_t contig;
+  int32_t left;
+  int32_t right;     /* bestEdge                                      */
+  uint32_t evidence; /* kmers of evidence (the first location included) */
+  uint8_t strand;    /* '+' or '-'                                    */
+  uint8_t frame;     /* list frame: 0..2 '-' phases, 3..5 '+' phases   */
+  uint16_t pad;
+} kma_proposal;
+int kma_propose_pegs(const kma_hit* hits, uint64_t n_hits, const uint32_t* peg_len,
+                     uint32_t n_peg, int k, double min_strength, double max_fuzz,
+                     double min_fuzz, int device, kma_proposal* out, uint64_t cap,
+                     uint64_t* n_out, uint64_t* stats);
+
 /* ---- signature-table construction (BuildKmerProcessor.java:137-223, RoleCounter.java) -------
  * After role resolution by the host (Feature.getUsefulRoles + the interesting-role filter):
  * roles[s] >= 0 is the single good role of an interesting peg, -1 marks a protein buffered for

@@ -1673,3 +1673,77 @@ int kma_protein_best_match(const uint8_t* residues, const uint64_t* offsets, uin
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int kma_propose_pegs(const kma_hit* hits, uint64_t n_hits, const uint32_t* peg_len,
+                     uint32_t n_peg, int k, double min_strength, double max_fuzz,
+                     double min_fuzz, int device, kma_proposal* out, uint64_t cap,
+                     uint64_t* n_out, uint64_t* stats) {
+  if (!n_out || !stats) return fail(KMA_E_INVALID, "null argument");
+  if (int rc = check_k(k)) return rc;
+  *n_out = 0;
+  stats[0] = stats[1] = stats[2] = stats[3] = 0;
+  if (n_hits == 0) return KMA_OK;
+  if (!hits || !peg_len || n_peg == 0) return fail(KMA_E_INVALID, "null argument");
+  if (cap && !out) return fail(KMA_E_INVALID, "null output");
+  if (n_hits >= (1ull << 31)) return fail(KMA_E_INVALID, "more than 2^31 connections");
+  if ((uint64_t)n_peg * 6 >= (1ull << 32)) return fail(KMA_E_INVALID, "too many pegs");
+  for (uint64_t i = 0; i < n_hits; ++i) {
+    const kma_hit& h = hits[i];
+    if (h.fid >= n_peg) return fail(KMA_E_INVALID, "connection %llu: peg %u >= %u",
+                                    (unsigned long long)i, h.fid, n_peg);
+    if (h.strand != '+' && h.strand != '-')
+      return fail(KMA_E_INVALID, "connection %llu: strand must be '+' or '-'",
+                  (unsigned long long)i);
+    if (i && (h.contig < hits[i - 1].contig ||
+              (h.contig == hits[i - 1].contig && h.left < hits[i - 1].left)))
+      return fail(KMA_E_INVALID, "connections are not in (contig, left) order at %llu",
+                  (unsigned long long)i);
+  }
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  const uint64_t n = n_hits;
+  DevBufs b;
+  kma::PropArgs a{};
+  kma_hit* d_hits;
+  uint32_t* d_len;
+  KMA_HIP(b.alloc(&d_hits, n * sizeof(kma_hit)));
+  KMA_HIP(b.alloc(&d_len, n_peg * 4ull));
+  for (uint32_t** p : {&a.keys, &a.skeys, &a.idx, &a.sidx, &a.head, &a.list_no, &a.scontig,
+                       &a.keep, &a.evidence, &a.out_pos})
+    KMA_HIP(b.alloc(p, n * 4));
+  KMA_HIP(b.alloc(&a.starts, (n + 1) * 4));
+  KMA_HIP(b.alloc(&a.sleft, n * 4));
+  KMA_HIP(b.alloc(&a.best, n * 4));
+  KMA_HIP(b.alloc(&a.stats, 32));
+  KMA_HIP(b.alloc(&a.out, n * sizeof(kma_proposal)));
+  a.hits = d_hits;
+  a.n = (uint32_t)n;
+  a.peg_len = d_len;
+  a.n_peg = n_peg;
+  a.k = k;
+  a.min_strength = min_strength;
+  a.max_fuzz = max_fuzz;
+  a.min_fuzz = min_fuzz;
+  a.cap = n;
+  size_t tb = 0;
+  KMA_HIP(kma::launch_propose(a, nullptr, &tb, nullptr));
+  void* d_temp;
+  KMA_HIP(b.alloc(&d_temp, tb ? tb : 1));
+  KMA_HIP(hipMemcpy(d_hits, hits, n * sizeof(kma_hit), hipMemcpyHostToDevice));
+  KMA_HIP(hipMemcpy(d_len, peg_len, n_peg * 4ull, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(a.stats, 0, 32));
+  KMA_HIP(kma::launch_propose(a, d_temp, &tb, nullptr));
+  KMA_HIP(hipMemcpy(stats, a.stats, 32, hipMemcpyDeviceToHost));
+  *n_out = stats[3];
+  const uint64_t take = std::min<uint64_t>(stats[3], cap);
+  if (take) KMA_HIP(hipMemcpy(out, a.out, take * sizeof(kma_proposal), hipMemcpyDeviceToHost));
+  if (stats[3] > cap)
+    return fail(KMA_E_CAPACITY, "%llu proposals, capacity %llu", (unsigned long long)stats[3],
+                (unsigned long long)cap);
+  return KMA_OK;
+}
+
+}  // extern "C"

@@ -248,6 +248,26 @@ struct ContigArgs {
 };
 constexpr int kContigTile = 256;  // forward positions per block
 
+// ---- the projector's proposal sweep (kma_proposals.hip) ----------------------------------------
+struct PropArgs {
+  const kma_hit* hits;  // n connections in canonical (contig, left) order
+  uint32_t n;
+  const uint32_t* peg_len;  // n_peg protein lengths
+  uint32_t n_peg;
+  int32_t k;
+  double min_strength, max_fuzz, min_fuzz;
+  uint32_t *keys, *skeys, *idx, *sidx;      // list keys / sort permutation
+  uint32_t *head, *list_no, *starts;        // list boundaries (starts: lists + 1)
+  uint32_t* scontig;
+  int32_t* sleft;
+  uint32_t *keep, *evidence, *out_pos;
+  int32_t* best;
+  uint64_t* stats;      // 4: lists, too few kmers, too short, proposals
+  kma_proposal* out;
+  uint64_t cap;
+};
+hipError_t launch_propose(PropArgs a, void* temp, size_t* temp_bytes, hipStream_t stream);
+
 // ---- launchers (kma_kernels.hip) --------------------------------------------------------------
 // status[0] = table full; stats (finalize) = {entries, max chain, displaced keys}.
 hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets, int k,

@@ -34,7 +34,7 @@ EXPORTS = (
     "kma_peg_table_create", "kma_connect_pegs", "kma_build_signatures", "kma_table_layout_for",
     "kma_table_create_replicated", "kma_table_replicate", "kma_table_replicas",
     "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
-    "kma_workspace_reserve_batch", "kma_workspace_phases_read",
+    "kma_workspace_reserve_batch", "kma_workspace_phases_read", "kma_propose_pegs",
 )
 
 
@@ -54,6 +54,9 @@ class TableInfo(C.Structure):
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
                       ("frame", "u1"), ("pad", "<u2")])
+PROPOSAL_DTYPE = np.dtype([("peg", "<u4"), ("contig", "<u4"), ("left", "<i4"), ("right", "<i4"),
+                           ("evidence", "<u4"), ("strand", "u1"), ("frame", "u1"),
+                           ("pad", "<u2")])
 
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C")
 _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
@@ -119,6 +122,8 @@ def load(path: str | None = None):
                                            C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_connect_pegs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _int, _vp, _u64,
                                        C.POINTER(_u64)]
+        L.kma_propose_pegs.argtypes = [_vp, _u64, _u32p, _u32, _int, C.c_double, C.c_double,
+                                       C.c_double, _int, _vp, _u64, C.POINTER(_u64), _u64p]
         L.kma_contig_window_count.restype = _u64
         L.kma_contig_window_count.argtypes = [_u64p, _u32, _int]
         _lib = L
@@ -405,6 +410,28 @@ def connect_pegs(peg_table: SignatureTable, dna: np.ndarray, offsets: np.ndarray
             continue
         _check(rc)
         return hits[:nh.value]
+
+
+def propose_pegs(hits: np.ndarray, peg_len, k: int = 8, min_strength: float = 0.5,
+                 max_fuzz: float = 1.5, min_fuzz: float = 0.8, device: int = 0):
+    """KmerProcessor.java:209-264 on the GPU: the proposal sweep over the framed location lists
+    of connect_pegs' hits (fid = peg index). Returns (PROPOSAL_DTYPE array, stats[4] =
+    lists, too few kmers, too short, proposals)."""
+    hits = np.ascontiguousarray(hits, HIT_DTYPE)
+    peg_len = np.ascontiguousarray(peg_len, np.uint32)
+    stats = np.zeros(4, np.uint64)
+    cap = max(16, len(hits) // 4)
+    while True:
+        out = np.empty(cap, PROPOSAL_DTYPE)
+        n = _u64()
+        rc = load().kma_propose_pegs(hits.ctypes.data if len(hits) else None, len(hits), peg_len,
+                                     len(peg_len), k, min_strength, max_fuzz, min_fuzz, device,
+                                     out.ctypes.data, cap, C.byref(n), stats)
+        if rc == E_CAPACITY:
+            cap = n.value
+            continue
+        _check(rc)
+        return out[:n.value], stats
 
 
 def build_signatures(residues: np.ndarray, offsets: np.ndarray, roles, k: int = 8,

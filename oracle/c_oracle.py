@@ -200,3 +200,31 @@ def protein_distances(residues, offsets, pair_a, pair_b, k: int = 8, flags: int 
                                 pa, pb, n, sim, sa, sb, dist)
     return sim, sa, sb, dist
 
+
+
+def propose(contig, left, strand, peg, peg_len, k: int = 8, min_strength: float = 0.5,
+            max_fuzz: float = 1.5, min_fuzz: float = 0.8):
+    """The projector's proposal sweep (KmerProcessor.java:209-264) over the connections
+    (contig, left, strand, peg): (proposal arrays dict, stats[4])."""
+    L = lib()
+    if not getattr(L, "_propose_typed", False):
+        L.orc_propose.restype = C.c_uint64
+        L._propose_typed = True
+    n = len(contig)
+    args = [np.ascontiguousarray(contig, np.uint32), np.ascontiguousarray(left, np.int32),
+            np.ascontiguousarray(strand, np.uint8), np.ascontiguousarray(peg, np.uint32)]
+    pl = np.ascontiguousarray(peg_len, np.uint32)
+    st = np.zeros(4, np.uint64)
+    ptr = [a.ctypes.data_as(C.c_void_p) for a in args]
+    cfg = [C.c_uint64(n), pl.ctypes.data_as(C.c_void_p), C.c_int(k), C.c_double(min_strength),
+           C.c_double(max_fuzz), C.c_double(min_fuzz)]
+    z = [None] * 7
+    m = L.orc_propose(*ptr, *cfg, *z, C.c_uint64(0), st.ctypes.data_as(C.c_void_p))
+    out = {"peg": np.empty(m, np.uint32), "contig": np.empty(m, np.uint32),
+           "strand": np.empty(m, np.uint8), "left": np.empty(m, np.int32),
+           "right": np.empty(m, np.int32), "evidence": np.empty(m, np.uint32),
+           "frame": np.empty(m, np.uint8)}
+    outs = [out[key].ctypes.data_as(C.c_void_p) for key in
+            ("peg", "contig", "strand", "left", "right", "evidence", "frame")]
+    L.orc_propose(*ptr, *cfg, *outs, C.c_uint64(m), st.ctypes.data_as(C.c_void_p))
+    return out, st

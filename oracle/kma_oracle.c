@@ -601,3 +601,106 @@ void orc_protein_distances(const uint8_t* residues, const uint64_t* offsets, int
   free(sa.slots), free(sa.order), free(sb.slots), free(sb.order);
 }
 
+
+/* ---- (f)2: the proposal sweep of the projector ----------------------------------------------
+ * KmerProcessor.annotateGenome, KmerProcessor.java:209-264, over the framed location lists of
+ * one close genome's connections (FramedLocationLists.connect, FramedLocationLists.java:156-171).
+ * Restated external semantics (org.theseed.locations Location / SortedLocationList / Frame are
+ * not in the reference; parity unpinned for them):
+ *   - a kmer location is (contig, strand, left .. left + 3K - 1); its frame is its strand and the
+ *     phase (mod 3) of its end point (right on '+', left on '-'); any definition by absolute
+ *     coordinates mod 3 puts the same locations in one list, only the frames' ORDER differs;
+ *   - SortedLocationList orders by (contig, left); contigRange(i) = the locations after i on
+ *     i's contig;
+ *   - lists are visited frame by frame ('-' phases 0, 1, 2, then '+' phases 0, 1, 2) and by peg
+ *     index within a frame (Java: HashMap order of the peg ids); starts in list order.
+ * Per list: pegLen = 3 * protein length; maxLen = (int)(pegLen * maxFuzz + 1); minLen =
+ * (int)(pegLen * minFuzz); minKmers = (int)(pegLen * (minStrength / 3)) (:222-228). A list
+ * shorter than minKmers counts as too few; otherwise every start i <= size - minKmers gets
+ * evidence = 1 + #{j in contigRange(i) : right_j < left_i + maxLen} and bestEdge = the largest
+ * such right (or right_i) (:233-246); bestEdge < left_i + minLen counts as too short, else a
+ * proposal (contig, strand, left_i, bestEdge, evidence) for the list's peg (:248-257).
+ * Deviation: a start past the list end (minKmers <= 0, which makes the Java loop read past the
+ * list) is not visited. stats: [0] lists, [1] too few kmers, [2] too short, [3] proposals. */
+typedef struct {
+  uint32_t contig, peg;
+  int32_t left;
+  uint8_t strand, frame;
+} orc_loc;
+
+static uint8_t orc_frame_idx(uint8_t strand, int32_t left, int K) {
+  const int32_t end = strand == '+' ? left + 3 * K - 1 : left;
+  return (uint8_t)((strand == '+' ? 3 : 0) + end % 3);
+}
+
+static int loc_cmp(const void* a, const void* b) {
+  const orc_loc *x = (const orc_loc*)a, *y = (const orc_loc*)b;
+  if (x->frame != y->frame) return x->frame < y->frame ? -1 : 1;
+  if (x->peg != y->peg) return x->peg < y->peg ? -1 : 1;
+  if (x->contig != y->contig) return x->contig < y->contig ? -1 : 1;
+  if (x->left != y->left) return x->left < y->left ? -1 : 1;
+  return 0;
+}
+
+uint64_t orc_propose(const uint32_t* contig, const int32_t* left, const uint8_t* strand,
+                     const uint32_t* peg, uint64_t n, const uint32_t* peg_len, int K,
+                     double min_strength, double max_fuzz, double min_fuzz, uint32_t* o_peg,
+                     uint32_t* o_contig, uint8_t* o_strand, int32_t* o_left, int32_t* o_right,
+                     uint32_t* o_evidence, uint8_t* o_frame, uint64_t cap, uint64_t* stats) {
+  orc_loc* L = (orc_loc*)malloc(sizeof(orc_loc) * (n + 1));
+  for (uint64_t i = 0; i < n; i++) {
+    orc_loc l = {contig[i], peg[i], left[i], strand[i], orc_frame_idx(strand[i], left[i], K)};
+    L[i] = l;
+  }
+  qsort(L, n, sizeof(orc_loc), loc_cmp);
+  const int32_t span = 3 * K - 1;  /* right = left + span */
+  const double real_strength = min_strength / 3;
+  uint64_t n_out = 0;
+  stats[0] = stats[1] = stats[2] = stats[3] = 0;
+  for (uint64_t s = 0; s < n;) {
+    uint64_t e = s + 1;
+    while (e < n && L[e].frame == L[s].frame && L[e].peg == L[s].peg) e++;
+    const int64_t size = (int64_t)(e - s);
+    const int32_t peg_bp = (int32_t)peg_len[L[s].peg] * 3;
+    const int32_t max_len = (int32_t)(peg_bp * max_fuzz + 1);
+    const int32_t min_len = (int32_t)(peg_bp * min_fuzz);
+    const int32_t min_kmers = (int32_t)(peg_bp * real_strength);
+    stats[0]++;
+    if (min_kmers > size) {
+      stats[1]++;
+    } else {
+      const int64_t last = size - min_kmers;
+      for (int64_t i = 0; i <= last && i < size; i++) {
+        const orc_loc* f = &L[s + i];
+        int32_t evidence = 1;
+        const int32_t max_edge = f->left + max_len, min_edge = f->left + min_len;
+        int32_t best = f->left + span;
+        for (int64_t j = i + 1; j < size && L[s + j].contig == f->contig; j++) {
+          const int32_t r = L[s + j].left + span;
+          if (r < max_edge) {
+            evidence++;
+            best = r > best ? r : best;
+          }
+        }
+        if (best < min_edge) {
+          stats[2]++;
+        } else {
+          if (n_out < cap) {
+            o_peg[n_out] = f->peg;
+            o_contig[n_out] = f->contig;
+            o_strand[n_out] = f->strand;
+            o_left[n_out] = f->left;
+            o_right[n_out] = best;
+            o_evidence[n_out] = (uint32_t)evidence;
+            o_frame[n_out] = f->frame;
+          }
+          n_out++;
+          stats[3]++;
+        }
+      }
+    }
+    s = e;
+  }
+  free(L);
+  return n_out;
+}

@@ -183,3 +183,47 @@ def best_match(query: str, cands, max_dist: float, k: int = 8):
             best, found = d, i
     return found, best
 
+
+
+def frame_of(strand: str, left: int, k: int = 8) -> int:
+    """Location.getFrame restated: strand and phase of the end point ('-' 0..2, '+' 3..5)."""
+    end = left + 3 * k - 1 if strand == "+" else left
+    return (3 if strand == "+" else 0) + end % 3
+
+
+def propose(connections, peg_len, k: int = 8, min_strength: float = 0.5, max_fuzz: float = 1.5,
+            min_fuzz: float = 0.8):
+    """KmerProcessor.java:209-264 over FramedLocationLists (:156-171): connections are
+    (contig, left, strand, peg); returns (proposals [(peg, contig, strand, left, right,
+    evidence, frame)], [lists, too_few, too_short, proposals])."""
+    framer = {}
+    for ct, lf, sd, pg in connections:
+        framer.setdefault((frame_of(sd, lf, k), pg), []).append((ct, lf))
+    span = 3 * k - 1
+    real = min_strength / 3
+    out, stats = [], [0, 0, 0, 0]
+    for (fr, pg) in sorted(framer):
+        lst = sorted(framer[(fr, pg)])
+        peg_bp = peg_len[pg] * 3
+        max_len, min_len = int(peg_bp * max_fuzz + 1), int(peg_bp * min_fuzz)
+        min_kmers = int(peg_bp * real)
+        stats[0] += 1
+        if min_kmers > len(lst):
+            stats[1] += 1
+            continue
+        strand = "+" if fr >= 3 else "-"
+        for i in range(min(len(lst) - min_kmers + 1, len(lst))):
+            ct, lf = lst[i]
+            evidence, best = 1, lf + span
+            for ct2, lf2 in lst[i + 1:]:
+                if ct2 != ct:
+                    break
+                if lf2 + span < lf + max_len:
+                    evidence += 1
+                    best = max(best, lf2 + span)
+            if best < lf + min_len:
+                stats[2] += 1
+            else:
+                out.append((pg, ct, strand, lf, best, evidence, fr))
+                stats[3] += 1
+    return out, stats
