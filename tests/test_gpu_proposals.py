@@ -63,7 +63,7 @@ def _check(kma, oracle_c, hits, peg_len, **kw):
 def test_proposals_small_gto_vs_oracle(kma, oracle_c, joined, params, strict):
     hits = joined[1] if strict else joined[0]
     got, st = _check(kma, oracle_c, hits, joined[2], **params)
-    assert st[0] > 1000 and st[3] > 100, st  # lists examined, proposals made
+    assert st[0] > 500 and st[3] > 100, st  # lists examined, proposals made
     # every proposal's first location is one of its peg's connections on that strand
     keys = set(zip(hits["fid"].tolist(), hits["contig"].tolist(), hits["left"].tolist()))
     assert all((p, c, l) in keys for p, c, l in zip(got["peg"].tolist(), got["contig"].tolist(),
