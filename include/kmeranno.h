@@ -318,6 +318,23 @@ int kma_propose_pegs(const kma_hit* hits, uint64_t n_hits, const uint32_t* peg_l
                      double min_fuzz, int device, kma_proposal* out, uint64_t cap,
                      uint64_t* n_out, uint64_t* stats);
 
+/* ---- hash annotator scoring (HashAnnotationProcessor.java:221-328) ---------------------------
+ * A genome's distinct protein sequences (the caller keys features by MD5, as GenomeProteinKmers
+ * does; proteins holding '*' are left out, :239-241) against the prototypes of the role
+ * annotation file in file order (:253-271; the caller drops prototypes shorter than minLen,
+ * :148-152). GenomeProteinKmers (external) restated: ProteinKmers sets of distinct K-mers
+ * (windows i = 0..L-K), similarity = shared / (|A| + |B| - shared) in double, a prototype
+ * becomes a protein's proposal when similarity >= min_sim and above the current one (earlier
+ * prototypes win ties). out_best[g] = prototype index or -1 (the default proposal: the old
+ * annotation with score 0.0, :285-288), out_sim[g] = its similarity (0.0 if none),
+ * out_count[p] = proteins with similarity >= min_sim (processProposal's return). K 2..12,
+ * 0 <= min_sim < 1; KMA_E_ALPHABET for bytes outside A-Z / '*'. Runs on `device` (sorts and
+ * scans; see kma_hashanno.hip).                                                              */
+int kma_hash_annotate(const uint8_t* genome_residues, const uint64_t* genome_offsets,
+                      uint32_t n_genome, const uint8_t* proto_residues,
+                      const uint64_t* proto_offsets, uint32_t n_proto, int k, double min_sim,
+                      int device, int32_t* out_best, double* out_sim, uint32_t* out_count);
+
 /* ---- signature-table construction (BuildKmerProcessor.java:137-223, RoleCounter.java) -------
  * After role resolution by the host (Feature.getUsefulRoles + the interesting-role filter):
  * roles[s] >= 0 is the single good role of an interesting peg, -1 marks a protein buffered for

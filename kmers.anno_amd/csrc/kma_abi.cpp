@@ -26,6 +26,7 @@
 
 #include "../../include/kmeranno.h"
 #include "kma_distance.h"
+#include "kma_hashanno.h"
 #include "kma_internal.h"
 
 namespace {
@@ -1743,6 +1744,206 @@ int kma_propose_pegs(const kma_hit* hits, uint64_t n_hits, const uint32_t* peg_l
   if (stats[3] > cap)
     return fail(KMA_E_CAPACITY, "%llu proposals, capacity %llu", (unsigned long long)stats[3],
                 (unsigned long long)cap);
+  return KMA_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// Window keys, per-protein sort and distinct sizes of a batch (device buffers in b): the
+// ProteinKmers sets of kma_hash_annotate's two sides.
+struct KmerSets {
+  uint8_t* res = nullptr;
+  uint64_t* off = nullptr;
+  uint64_t *keys = nullptr, *sorted = nullptr;
+  uint32_t *size = nullptr, *owner = nullptr;
+  uint8_t* first = nullptr;
+  uint64_t total = 0;
+};
+
+int kmer_sets(DevBufs& b, const uint8_t* residues, const uint64_t* offsets, uint32_t n, int k,
+              uint32_t* d_alpha, KmerSets& ks) {
+  const uint64_t base = offsets[0];
+  ks.total = offsets[n] - base;
+  std::vector<uint64_t> rel(offsets, offsets + n + 1);
+  for (auto& o : rel) o -= base;
+  const uint64_t nw = std::max<uint64_t>(ks.total, 1);
+  KMA_HIP(b.alloc(&ks.res, ks.total + 64));
+  KMA_HIP(b.alloc(&ks.off, (n + 1) * 8ull));
+  KMA_HIP(b.alloc(&ks.keys, nw * 8));
+  KMA_HIP(b.alloc(&ks.sorted, nw * 8));
+  KMA_HIP(b.alloc(&ks.size, std::max<uint64_t>(n, 1) * 4));
+  KMA_HIP(b.alloc(&ks.owner, nw * 4));
+  KMA_HIP(b.alloc(&ks.first, nw));
+  KMA_HIP(hipMemcpy(ks.res, residues + base, ks.total, hipMemcpyHostToDevice));
+  KMA_HIP(hipMemset(ks.res + ks.total, 0, 64));
+  KMA_HIP(hipMemcpy(ks.off, rel.data(), (n + 1) * 8ull, hipMemcpyHostToDevice));
+  KMA_HIP(kma::launch_window_keys(ks.res, ks.off, n, k, 0, ks.keys, d_alpha, nullptr));
+  size_t tb = 0;
+  KMA_HIP(kma::launch_segmented_sort(nullptr, &tb, ks.keys, ks.sorted, ks.total, n, ks.off,
+                                     ks.off + 1, 5 * k, nullptr));
+  void* d_temp;
+  KMA_HIP(b.alloc(&d_temp, tb ? tb : 1));
+  KMA_HIP(kma::launch_segmented_sort(d_temp, &tb, ks.keys, ks.sorted, ks.total, n, ks.off,
+                                     ks.off + 1, 5 * k, nullptr));
+  KMA_HIP(kma::launch_distinct(ks.sorted, ks.off, n, ks.size, nullptr));
+  KMA_HIP(kma::launch_owner_first(ks.sorted, ks.off, n, ks.owner, ks.first, nullptr));
+  return KMA_OK;
+}
+
+int check_batch(const uint8_t* residues, const uint64_t* offsets, uint32_t n, const char* what) {
+  if (n && (!residues || !offsets)) return fail(KMA_E_INVALID, "null %s", what);
+  for (uint32_t s = 0; s < n; ++s)
+    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "%s offsets decrease at %u", what, s);
+  if (n && offsets[n] - offsets[0] >= (1ull << 31))
+    return fail(KMA_E_INVALID, "more than 2^31 %s residues", what);
+  return KMA_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
+                      const uint8_t* pres, const uint64_t* poff, uint32_t n_pt, int k,
+                      double min_sim, int device, int32_t* out_best, double* out_sim,
+                      uint32_t* out_count) {
+  if (k < 2 || k > 12) return fail(KMA_E_INVALID, "kmer size %d outside 2..12", k);
+  if (!(min_sim >= 0.0 && min_sim < 1.0))
+    return fail(KMA_E_INVALID, "Minimum similarity score must be between 0 and 1.");
+  if ((n_gp && (!out_best || !out_sim)) || (n_pt && !out_count))
+    return fail(KMA_E_INVALID, "null output");
+  if (int rc = check_batch(gres, goff, n_gp, "genome protein")) return rc;
+  if (int rc = check_batch(pres, poff, n_pt, "prototype")) return rc;
+  for (uint32_t i = 0; i < n_gp; ++i) {
+    out_best[i] = -1;
+    out_sim[i] = 0.0;
+  }
+  if (n_pt) std::memset(out_count, 0, n_pt * 4ull);
+  if (n_gp == 0 || n_pt == 0) return KMA_OK;
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
+                                        hipGetErrorString(ds.err));
+  DevBufs b;
+  uint32_t* d_alpha;
+  uint64_t* d_n;  // [0] genome pairs, [1] unique keys, [2] runs
+  KMA_HIP(b.alloc(&d_alpha, 4));
+  KMA_HIP(b.alloc(&d_n, 32));
+  KMA_HIP(hipMemset(d_alpha, 0, 4));
+  KMA_HIP(hipMemset(d_n, 0, 32));
+  KmerSets g, p;
+  if (int rc = kmer_sets(b, gres, goff, n_gp, k, d_alpha, g)) return rc;
+  if (int rc = kmer_sets(b, pres, poff, n_pt, k, d_alpha, p)) return rc;
+  uint32_t alpha = 0;
+  KMA_HIP(hipMemcpy(&alpha, d_alpha, 4, hipMemcpyDeviceToHost));
+  if (alpha) return fail(KMA_E_ALPHABET, "a protein window holds a byte outside A-Z and '*'");
+  const int kb = 5 * k;
+  // genome (key, protein) pairs of distinct keys, sorted by key; unique keys and ranges
+  const uint64_t gw = std::max<uint64_t>(g.total, 1);
+  uint64_t *gpk, *skey, *ukeys;
+  uint32_t *gpp, *sprot, *uidx, *ustart;
+  uint8_t* uhead;
+  for (uint64_t** q : {&gpk, &skey, &ukeys}) KMA_HIP(b.alloc(q, gw * 8));
+  for (uint32_t** q : {&gpp, &sprot, &uidx}) KMA_HIP(b.alloc(q, gw * 4));
+  KMA_HIP(b.alloc(&ustart, (gw + 1) * 4));
+  KMA_HIP(b.alloc(&uhead, gw));
+  size_t need = 0, tb = 0;
+  auto grow = [&](size_t t) { need = std::max(need, t); };
+  KMA_HIP(kma::cub_select_flagged_u64(nullptr, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
+  grow(tb);
+  KMA_HIP(kma::cub_select_flagged_u32(nullptr, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
+  grow(tb);
+  KMA_HIP(kma::cub_sort_pairs_u64_u32(nullptr, &tb, gpk, skey, gpp, sprot, g.total, kb, nullptr));
+  grow(tb);
+  KMA_HIP(kma::cub_excl_sum_u32_u64(nullptr, &tb, nullptr, nullptr, std::max<uint64_t>(p.total, 1), nullptr));
+  grow(tb);
+  void* temp;
+  KMA_HIP(b.alloc(&temp, need ? need : 1));
+  tb = need;
+  KMA_HIP(kma::cub_select_flagged_u64(temp, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
+  tb = need;
+  KMA_HIP(kma::cub_select_flagged_u32(temp, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
+  uint64_t n_pairs = 0;
+  KMA_HIP(hipMemcpy(&n_pairs, d_n, 8, hipMemcpyDeviceToHost));
+  tb = need;
+  KMA_HIP(kma::cub_sort_pairs_u64_u32(temp, &tb, gpk, skey, gpp, sprot, n_pairs, kb, nullptr));
+  KMA_HIP(kma::launch_run_heads(skey, n_pairs, uhead, uidx, nullptr));
+  tb = need;
+  KMA_HIP(kma::cub_select_flagged_u64(temp, &tb, skey, uhead, ukeys, d_n + 1, n_pairs, nullptr));
+  tb = need;
+  KMA_HIP(kma::cub_select_flagged_u32(temp, &tb, uidx, uhead, ustart, d_n + 1, n_pairs, nullptr));
+  KMA_HIP(kma::launch_set_end(ustart, d_n + 1, n_pairs, nullptr));
+  // candidates: one (prototype, protein) per shared distinct key
+  kma::HashArgs a{};
+  a.n_ppos = p.total;
+  a.pfirst = p.first;
+  a.psorted = p.sorted;
+  a.powner = p.owner;
+  a.psize = p.size;
+  a.ukeys = ukeys;
+  a.n_u = d_n + 1;
+  a.ustart = ustart;
+  a.gprot = sprot;
+  a.gsize = g.size;
+  a.min_sim = min_sim;
+  const uint64_t pw = std::max<uint64_t>(p.total, 1);
+  uint64_t* coff;
+  KMA_HIP(b.alloc(&a.ccount, pw * 4));
+  KMA_HIP(b.alloc(&a.cu, pw * 4));
+  KMA_HIP(b.alloc(&coff, pw * 8));
+  a.coff = coff;
+  KMA_HIP(kma::launch_cand_count(a, nullptr));
+  tb = need;
+  KMA_HIP(kma::cub_excl_sum_u32_u64(temp, &tb, a.ccount, coff, p.total, nullptr));
+  uint64_t last_off = 0;
+  uint32_t last_cnt = 0;
+  if (p.total) {
+    KMA_HIP(hipMemcpy(&last_off, coff + p.total - 1, 8, hipMemcpyDeviceToHost));
+    KMA_HIP(hipMemcpy(&last_cnt, a.ccount + p.total - 1, 4, hipMemcpyDeviceToHost));
+  }
+  const uint64_t n_cand = last_off + last_cnt;
+  KMA_HIP(b.alloc(&a.out_count, n_pt * 4ull));
+  KMA_HIP(b.alloc(&a.best_bits, n_gp * 8ull));
+  KMA_HIP(b.alloc(&a.best_proto, n_gp * 4ull));
+  KMA_HIP(hipMemset(a.out_count, 0, n_pt * 4ull));
+  KMA_HIP(hipMemset(a.best_bits, 0, n_gp * 8ull));
+  KMA_HIP(hipMemset(a.best_proto, 0xFF, n_gp * 4ull));
+  if (n_cand) {
+    uint64_t *cand, *csorted, *runs;
+    uint32_t* run_len;
+    KMA_HIP(b.alloc(&cand, n_cand * 8));
+    KMA_HIP(b.alloc(&csorted, n_cand * 8));
+    KMA_HIP(b.alloc(&runs, n_cand * 8));
+    KMA_HIP(b.alloc(&run_len, n_cand * 4));
+    a.cand = cand;
+    KMA_HIP(kma::launch_cand_emit(a, nullptr));
+    int pbits = 1;
+    while (pbits < 32 && (1ull << pbits) < n_pt) ++pbits;
+    size_t t2 = 0, t3 = 0;
+    KMA_HIP(kma::cub_sort_keys_u64(nullptr, &t2, cand, csorted, n_cand, 32 + pbits, nullptr));
+    KMA_HIP(kma::cub_rle_u64(nullptr, &t3, csorted, runs, run_len, d_n + 2, n_cand, nullptr));
+    void* temp2;
+    const size_t t23 = std::max(t2, t3);
+    KMA_HIP(b.alloc(&temp2, t23 ? t23 : 1));
+    t2 = t23;
+    KMA_HIP(kma::cub_sort_keys_u64(temp2, &t2, cand, csorted, n_cand, 32 + pbits, nullptr));
+    t3 = t23;
+    KMA_HIP(kma::cub_rle_u64(temp2, &t3, csorted, runs, run_len, d_n + 2, n_cand, nullptr));
+    a.runs = runs;
+    a.run_len = run_len;
+    a.n_runs = d_n + 2;
+    KMA_HIP(kma::launch_score(a, n_cand, nullptr));
+    KMA_HIP(kma::launch_choose(a, n_cand, nullptr));
+  }
+  std::vector<uint64_t> bits(n_gp);
+  std::vector<uint32_t> proto(n_gp);
+  KMA_HIP(hipMemcpy(bits.data(), a.best_bits, n_gp * 8ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(proto.data(), a.best_proto, n_gp * 4ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(out_count, a.out_count, n_pt * 4ull, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n_gp; ++i) {
+    if (proto[i] == 0xFFFFFFFFu) continue;
+    std::memcpy(&out_sim[i], &bits[i], 8);
+    out_best[i] = (int32_t)proto[i];
+  }
   return KMA_OK;
 }
 

@@ -35,6 +35,7 @@ EXPORTS = (
     "kma_table_create_replicated", "kma_table_replicate", "kma_table_replicas",
     "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
     "kma_workspace_reserve_batch", "kma_workspace_phases_read", "kma_propose_pegs",
+    "kma_hash_annotate",
 )
 
 
@@ -122,6 +123,8 @@ def load(path: str | None = None):
                                            C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_connect_pegs.argtypes = [_vp, _u8p, _u64p, _u32, _int, _int, _vp, _u64,
                                        C.POINTER(_u64)]
+        L.kma_hash_annotate.argtypes = [_u8p, _u64p, _u32, _u8p, _u64p, _u32, _int, C.c_double,
+                                        _int, _vp, _vp, _vp]
         L.kma_propose_pegs.argtypes = [_vp, _u64, _u32p, _u32, _int, C.c_double, C.c_double,
                                        C.c_double, _int, _vp, _u64, C.POINTER(_u64), _u64p]
         L.kma_contig_window_count.restype = _u64
@@ -432,6 +435,25 @@ def propose_pegs(hits: np.ndarray, peg_len, k: int = 8, min_strength: float = 0.
             continue
         _check(rc)
         return out[:n.value], stats
+
+
+def hash_annotate(genome_residues, genome_offsets, proto_residues, proto_offsets, k: int = 8,
+                  min_sim: float = 0.0125, device: int = 0):
+    """HashAnnotationProcessor.java:233-306 scoring on the GPU: (best prototype per genome
+    protein or -1, its similarity (0.0 if none), matches per prototype)."""
+    gr = np.ascontiguousarray(genome_residues, np.uint8)
+    go = np.ascontiguousarray(genome_offsets, np.uint64)
+    pr = np.ascontiguousarray(proto_residues, np.uint8)
+    po = np.ascontiguousarray(proto_offsets, np.uint64)
+    n_g, n_p = len(go) - 1, len(po) - 1
+    best = np.empty(max(n_g, 1), np.int32)
+    sim = np.empty(max(n_g, 1), np.float64)
+    cnt = np.empty(max(n_p, 1), np.uint32)
+    _check(load().kma_hash_annotate(gr if len(gr) else np.zeros(1, np.uint8), go, n_g,
+                                    pr if len(pr) else np.zeros(1, np.uint8), po, n_p, k,
+                                    min_sim, device, best.ctypes.data, sim.ctypes.data,
+                                    cnt.ctypes.data))
+    return best[:n_g], sim[:n_g], cnt[:n_p]
 
 
 def build_signatures(residues: np.ndarray, offsets: np.ndarray, roles, k: int = 8,

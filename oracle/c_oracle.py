@@ -228,3 +228,21 @@ def propose(contig, left, strand, peg, peg_len, k: int = 8, min_strength: float 
             ("peg", "contig", "strand", "left", "right", "evidence", "frame")]
     L.orc_propose(*ptr, *cfg, *outs, C.c_uint64(m), st.ctypes.data_as(C.c_void_p))
     return out, st
+
+
+def hash_annotate(gres, goff, pres, poff, k: int = 8, min_sim: float = 0.0125):
+    """HashAnnotationProcessor's scoring loop: (best prototype per genome protein or -1,
+    its similarity, matches per prototype)."""
+    L = lib()
+    n_gp, n_pt = len(goff) - 1, len(poff) - 1
+    best = np.empty(n_gp, np.int32)
+    sim = np.empty(n_gp, np.float64)
+    cnt = np.empty(n_pt, np.uint32)
+    vp = C.c_void_p
+    L.orc_hash_annotate(np.ascontiguousarray(gres, np.uint8).ctypes.data_as(vp),
+                        np.ascontiguousarray(goff, np.uint64).ctypes.data_as(vp), C.c_uint32(n_gp),
+                        np.ascontiguousarray(pres, np.uint8).ctypes.data_as(vp),
+                        np.ascontiguousarray(poff, np.uint64).ctypes.data_as(vp), C.c_uint32(n_pt),
+                        C.c_int(k), C.c_double(min_sim), best.ctypes.data_as(vp),
+                        sim.ctypes.data_as(vp), cnt.ctypes.data_as(vp))
+    return best, sim, cnt

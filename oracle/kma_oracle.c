@@ -704,3 +704,81 @@ uint64_t orc_propose(const uint32_t* contig, const int32_t* left, const uint8_t*
   free(L);
   return n_out;
 }
+
+/* ---- (f)3: the hash annotator's scoring loop ---------------------------------------------------
+ * HashAnnotationProcessor.processGenome (HashAnnotationProcessor.java:221-328) with
+ * GenomeProteinKmers (external org.theseed.proteins.kmers; restated, parity unpinned):
+ * addProtein gives each distinct genome protein a default proposal (score 0.0); processProposal
+ * (:259-271) is called for every prototype in file order: for every genome protein sharing at
+ * least one distinct K-mer (ProteinKmers windows i = 0..L-K), sim = shared / (|A| + |B| -
+ * shared); sim >= minSim counts as a match (the call's return) and, when above the protein's
+ * current score, makes the prototype its proposal. Literal restatement: every (prototype,
+ * protein) pair by a merge of the two sorted distinct key lists. */
+static uint64_t pack_kmer(const uint8_t* p, int K, int* ok) {
+  uint64_t v = 0;
+  *ok = 1;
+  for (int j = 0; j < K; j++) {
+    const uint8_t c = p[j];
+    uint32_t code = (c >= 'A' && c <= 'Z') ? (uint32_t)(c - 'A' + 1) : (c == '*' ? 27u : 0u);
+    if (!code) *ok = 0;
+    v = (v << 5) | code;
+  }
+  return v;
+}
+
+static int u64_cmp(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* distinct sorted keys of each sequence: keys[off[s]..off[s]+size[s]) */
+static uint64_t* distinct_sets(const uint8_t* res, const uint64_t* off, uint32_t n, int K,
+                               uint32_t* size) {
+  uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (off[n] - off[0] + 1));
+  for (uint32_t s = 0; s < n; s++) {
+    const uint64_t lo = off[s] - off[0];
+    const int64_t nw = (int64_t)(off[s + 1] - off[s]) - K + 1;
+    uint32_t m = 0;
+    for (int64_t i = 0; i < nw; i++) {
+      int ok;
+      keys[lo + m++] = pack_kmer(res + off[s] + i, K, &ok);
+    }
+    qsort(keys + lo, m, sizeof(uint64_t), u64_cmp);
+    uint32_t d = 0;
+    for (uint32_t i = 0; i < m; i++)
+      if (i == 0 || keys[lo + i] != keys[lo + i - 1]) keys[lo + d++] = keys[lo + i];
+    size[s] = d;
+  }
+  return keys;
+}
+
+void orc_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
+                       const uint8_t* pres, const uint64_t* poff, uint32_t n_pt, int K,
+                       double min_sim, int32_t* out_best, double* out_sim, uint32_t* out_count) {
+  uint32_t* gs = (uint32_t*)malloc(sizeof(uint32_t) * (n_gp + 1));
+  uint32_t* ps = (uint32_t*)malloc(sizeof(uint32_t) * (n_pt + 1));
+  uint64_t* gk = distinct_sets(gres, goff, n_gp, K, gs);
+  uint64_t* pk = distinct_sets(pres, poff, n_pt, K, ps);
+  for (uint32_t g = 0; g < n_gp; g++) out_best[g] = -1, out_sim[g] = 0.0;
+  for (uint32_t p = 0; p < n_pt; p++) {
+    const uint64_t* a = pk + (poff[p] - poff[0]);
+    uint32_t matches = 0;
+    for (uint32_t g = 0; g < n_gp; g++) {
+      const uint64_t* b = gk + (goff[g] - goff[0]);
+      uint32_t i = 0, j = 0, shared = 0;
+      while (i < ps[p] && j < gs[g]) {
+        if (a[i] < b[j]) i++;
+        else if (a[i] > b[j]) j++;
+        else shared++, i++, j++;
+      }
+      if (!shared) continue;
+      const double sim = (double)shared / ((double)ps[p] + (double)gs[g] - (double)shared);
+      if (sim >= min_sim) {
+        matches++;
+        if (sim > out_sim[g]) out_sim[g] = sim, out_best[g] = (int32_t)p;
+      }
+    }
+    out_count[p] = matches;
+  }
+  free(gs), free(ps), free(gk), free(pk);
+}

@@ -227,3 +227,25 @@ def propose(connections, peg_len, k: int = 8, min_strength: float = 0.5, max_fuz
                 out.append((pg, ct, strand, lf, best, evidence, fr))
                 stats[3] += 1
     return out, stats
+
+
+def hash_annotate(genome_prots, protos, k: int = 8, min_sim: float = 0.0125):
+    """GenomeProteinKmers restated (HashAnnotationProcessor.java:233-306): per genome protein
+    the first prototype reaching the best similarity >= min_sim (-1 / 0.0 if none), and the
+    matches of every prototype."""
+    gsets = [{p[i:i + k] for i in range(len(p) - k + 1)} for p in genome_prots]
+    best, sim, counts = [-1] * len(genome_prots), [0.0] * len(genome_prots), []
+    for pi, pr in enumerate(protos):
+        a = {pr[i:i + k] for i in range(len(pr) - k + 1)}
+        m = 0
+        for gi, b in enumerate(gsets):
+            shared = len(a & b)
+            if not shared:
+                continue
+            s = shared / (len(a) + len(b) - shared)
+            if s >= min_sim:
+                m += 1
+                if s > sim[gi]:
+                    sim[gi], best[gi] = s, pi
+        counts.append(m)
+    return best, sim, counts
