@@ -277,8 +277,6 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
-// Resident annotate_kernel blocks per CU (occupancy API).
-int annotate_occupancy(int k, int m);
 // The direct path over a device list of proteins (a.list / a.list_n), `blocks` persistent blocks.
 hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream);
 // The partitioned path (kma_partition.hip): chunking (flags, scan, index), P1, P2, P3. temp:

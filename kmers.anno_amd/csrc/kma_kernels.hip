@@ -777,19 +777,6 @@ struct AnnotateListLaunch {
   }
 };
 
-template <int K, int M>
-struct AnnotateOccupancy {
-  static hipError_t run(int* out) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(out, annotate_kernel<K, M, kBlockProteins>,
-                                                        256, 0);
-  }
-};
-int annotate_occupancy(int k, int m) {
-  int n = 0;
-  if (dispatch_km<AnnotateOccupancy>(k, m, &n) != hipSuccess || n < 1) n = 1;
-  return n;
-}
-
 hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
   return dispatch_km<AnnotateListLaunch>(a.k, a.mlen, a, blocks ? blocks : 1u, stream);
 }
