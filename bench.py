@@ -231,7 +231,8 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
 
         m = kmeranno.layout_for(K, nb)
         st, ms = build(m)
-        if m and (st[3] > 0.15 * st[1] or st[2] > 32):
+        forced = os.environ.get("KMA_MINIMIZER", "") in ("0", "6", "7")  # A/B runs: keep it
+        if m and not forced and (st[3] > 0.15 * st[1] or st[2] > 32):
             sf, msf = build(0)
             if 2 * sf[3] < st[3] or (st[2] > 32 and 2 * sf[2] < st[2]):
                 m, st, ms = 0, sf, msf
