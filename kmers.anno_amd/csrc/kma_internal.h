@@ -122,10 +122,11 @@ constexpr uint32_t kMaxChain = 32;
 #define KMA_SET_POOL 4096
 #endif
 #ifndef KMA_PROBE_WIN
-#define KMA_PROBE_WIN (KMA_BUCKET_SLOTS == 16 ? 1 : 3)
+#define KMA_PROBE_WIN (KMA_BUCKET_SLOTS == 16 ? 1 : 2)
 #endif
 // Windows per lane per step: each costs 4 dwordx4 per bucket half (16 VGPRs per 64 bytes) in
-// flight (3 with 64-byte buckets: 70 VGPRs, 7 waves/SIMD; 4 measured 9% slower in round 1).
+// flight. With the single protein kernel, 2 measured best on MI355X (profiles/r02i_variants.log:
+// c5 4.39 vs 4.52 ms for 3, c2 65.4 vs 66.3 us; 4 is 23% slower at c2).
 constexpr int kProbeWin = KMA_PROBE_WIN;
 constexpr int kBlockProteins = KMA_BLOCK_PROTEINS;
 constexpr int kSetPool = KMA_SET_POOL;
@@ -246,7 +247,13 @@ struct ContigArgs {
   int32_t strict_pass;         // 0 = off
   uint8_t codon_codes[64];     // by value (TCAG order): 5-bit aa code, 0 = stop
 };
-constexpr int kContigTile = 256;  // forward positions per block
+#ifndef KMA_CONTIG_POS
+#define KMA_CONTIG_POS 1
+#endif
+// Forward positions per lane of the 6-frame probe (2 windows each). 2 raises the kernel to 97
+// VGPRs (4 waves/SIMD) and measured slower at c3 (0.139 vs 0.124 ms, profiles/r02i_variants.log).
+constexpr int kContigPos = KMA_CONTIG_POS;
+constexpr int kContigTile = 256 * kContigPos;  // forward positions per block
 
 // ---- the projector's proposal sweep (kma_proposals.hip) ----------------------------------------
 struct PropArgs {

@@ -464,7 +464,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   __shared__ uint8_t aa_p[kSpan], aa_m[kSpan];
   __shared__ uint64_t offc[kOffCache + 1];
   __shared__ uint32_t crange[2];
-  __shared__ uint32_t wave_tot[kWavesPerBlock];
+  __shared__ uint32_t wave_tot[kWavesPerBlock * kContigPos];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const uint64_t base = a.offsets[0], end = base + a.total_bases;
   const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
@@ -495,103 +495,121 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   }
   __syncthreads();
 
-  const uint64_t r = r0 + t, g = base + r;
-  uint32_t contig = c_lo;
-  int64_t x = 0, len = 0;
-  if (g < end) {
-    if (nc <= (uint32_t)kOffCache) {
-      uint32_t lo = 0, hi = nc;  // largest i < nc with offc[i] <= g
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (offc[mid] <= g) lo = mid; else hi = mid;
+  // Each lane owns positions t + 256 h (h < kContigPos): both windows of every one of them are
+  // probed with all their dwordx4 in flight before any compare.
+  constexpr int CP = kContigPos;
+  uint32_t contig[CP];
+  int64_t xs[CP], lens[CP];
+  uint64_t key[CP][2];
+  uint32_t bk[CP][2];
+#pragma unroll
+  for (int h = 0; h < CP; ++h) {
+    const uint32_t tt = t + 256u * h;
+    const uint64_t g = base + r0 + tt;
+    contig[h] = c_lo;
+    int64_t x = 0, len = 0;
+    if (g < end) {
+      if (nc <= (uint32_t)kOffCache) {
+        uint32_t lo = 0, hi = nc;  // largest i < nc with offc[i] <= g
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (offc[mid] <= g) lo = mid; else hi = mid;
+        }
+        contig[h] = c_lo + lo;
+        x = (int64_t)(g - offc[lo]);
+        len = (int64_t)(offc[lo + 1] - offc[lo]);
+      } else {
+        contig[h] = contig_of(a.offsets, a.n_contig, g);
+        x = (int64_t)(g - a.offsets[contig[h]]);
+        len = (int64_t)(a.offsets[contig[h] + 1] - a.offsets[contig[h]]);
       }
-      contig = c_lo + lo;
-      x = (int64_t)(g - offc[lo]);
-      len = (int64_t)(offc[lo + 1] - offc[lo]);
-    } else {
-      contig = contig_of(a.offsets, a.n_contig, g);
-      x = (int64_t)(g - a.offsets[contig]);
-      len = (int64_t)(a.offsets[contig + 1] - a.offsets[contig]);
     }
-  }
-  bool pv = g < end && x + 3 * K + 3 <= len, mv = g < end && x >= 3 && x + 3 * K <= len;
-  uint64_t key[2] = {0, 0};
+    xs[h] = x;
+    lens[h] = len;
+    bool pv = g < end && x + 3 * K + 3 <= len, mv = g < end && x >= 3 && x + 3 * K <= len;
+    key[h][0] = key[h][1] = 0;
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const uint32_t cp = aa_p[t + 3 * j], cm = aa_m[t + 3 * j];
-    pv = pv && cp != 0u;
-    mv = mv && cm != 0u;
-    key[0] = (key[0] << 5) | cp;
-    key[1] |= (uint64_t)cm << (5 * j);
-  }
-  uint32_t bk[2], klo[2], khi[2];
-  bk[0] = pv ? home_bucket(key[0], K, M, nb) : kNone;
-  bk[1] = mv ? home_bucket(key[1], K, M, nb) : kNone;
-  uint4 q[2][4][kBucketHalves];  // both windows' quad buckets: all dwordx4 in flight
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    klo[j] = (uint32_t)key[j];
-    khi[j] = (uint32_t)(key[j] >> 32) << 24;
-    const uint32_t b0 = quad_bcast<0>(bk[j]), b1 = quad_bcast<1>(bk[j]);
-    const uint32_t b2 = quad_bcast<2>(bk[j]), b3 = quad_bcast<3>(bk[j]);
-    const uint32_t bb[4] = {b0, b1, b2, b3};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint4* bp = reinterpret_cast<const uint4*>(a.slots) + part +
-                        (uint64_t)(bb[r] == kNone ? 0u : bb[r]) * kBucketQuads;
-#pragma unroll
-      for (int h = 0; h < kBucketHalves; ++h) q[j][r][h] = bp[4 * h];
+    for (int j = 0; j < K; ++j) {
+      const uint32_t cp = aa_p[tt + 3 * j], cm = aa_m[tt + 3 * j];
+      pv = pv && cp != 0u;
+      mv = mv && cm != 0u;
+      key[h][0] = (key[h][0] << 5) | cp;
+      key[h][1] |= (uint64_t)cm << (5 * j);
     }
+    bk[h][0] = pv ? home_bucket(key[h][0], K, M, nb) : kNone;
+    bk[h][1] = mv ? home_bucket(key[h][1], K, M, nb) : kNone;
   }
-  uint32_t word[2];
+  uint4 q[CP][2][4][kBucketHalves];  // every window's quad buckets: all dwordx4 in flight
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    word[j] = 0;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const uint32_t kl = rr == 0 ? quad_bcast<0>(klo[j]) : rr == 1 ? quad_bcast<1>(klo[j])
-                        : rr == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
-      const uint32_t kh = rr == 0 ? quad_bcast<0>(khi[j]) : rr == 1 ? quad_bcast<1>(khi[j])
-                        : rr == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
-      const uint32_t v = match_part(q[j][rr], kl, kh, part);
-      word[j] = part == rr ? v : word[j];
-    }
-  }
-  bool hit[2];
-  uint32_t fid[2], sid[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const uint32_t w = bk[j] != kNone ? word[j] : 0u;
-    hit[j] = (w & kWordFid) != 0u;
-    fid[j] = (w & kWordFid) - 1u;
-    sid[j] = bk[j] * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask);
-    if (w == 0x80000000u)  // rare: the home bucket missed with the key's overflow bit set
-      hit[j] = walk_chain(a.slots, nb, bk[j], key[j], fid[j], sid[j]);
-  }
-  if (a.strict_pass) {  // KmerFactory.Strict: a key's locations counted by its slot id
+  for (int h = 0; h < CP; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (!hit[j]) continue;
-      if (a.strict_pass == 1) atomicAdd(a.slot_count + sid[j], 1u);
-      else hit[j] = a.slot_count[sid[j]] == 1u;
+      const uint32_t b0 = quad_bcast<0>(bk[h][j]), b1 = quad_bcast<1>(bk[h][j]);
+      const uint32_t b2 = quad_bcast<2>(bk[h][j]), b3 = quad_bcast<3>(bk[h][j]);
+      const uint32_t bb[4] = {b0, b1, b2, b3};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint4* bp = reinterpret_cast<const uint4*>(a.slots) + part +
+                          (uint64_t)(bb[r] == kNone ? 0u : bb[r]) * kBucketQuads;
+#pragma unroll
+        for (int hh = 0; hh < kBucketHalves; ++hh) q[h][j][r][hh] = bp[4 * hh];
+      }
     }
+  bool hit[CP][2];
+  uint32_t fid[CP][2];
+#pragma unroll
+  for (int h = 0; h < CP; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t klo = (uint32_t)key[h][j], khi = (uint32_t)(key[h][j] >> 32) << 24;
+      uint32_t word = 0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const uint32_t kl = rr == 0 ? quad_bcast<0>(klo) : rr == 1 ? quad_bcast<1>(klo)
+                          : rr == 2 ? quad_bcast<2>(klo) : quad_bcast<3>(klo);
+        const uint32_t kh = rr == 0 ? quad_bcast<0>(khi) : rr == 1 ? quad_bcast<1>(khi)
+                          : rr == 2 ? quad_bcast<2>(khi) : quad_bcast<3>(khi);
+        const uint32_t v = match_part(q[h][j][rr], kl, kh, part);
+        word = part == rr ? v : word;
+      }
+      const uint32_t w = bk[h][j] != kNone ? word : 0u;
+      hit[h][j] = (w & kWordFid) != 0u;
+      fid[h][j] = (w & kWordFid) - 1u;
+      uint32_t sid = bk[h][j] * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask);
+      if (w == 0x80000000u)  // rare: the home bucket missed with the key's overflow bit set
+        hit[h][j] = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+      if (a.strict_pass && hit[h][j]) {  // KmerFactory.Strict: locations counted by slot id
+        if (a.strict_pass == 1) atomicAdd(a.slot_count + sid, 1u);
+        else hit[h][j] = a.slot_count[sid] == 1u;
+      }
+      if (a.tally && hit[h][j] && fid[h][j] < a.n_fid)
+        atomicAdd(a.tally + (uint64_t)contig[h] * a.n_fid + fid[h][j], 1u);
+    }
+  (void)xs;
+  (void)lens;
+  // Block-local compaction in canonical order (position, '+' before '-'): positions of the
+  // first 256 before those of the next.
+  uint64_t bp[CP], bm[CP];
+#pragma unroll
+  for (int h = 0; h < CP; ++h) {
+    bp[h] = __ballot(hit[h][0]);
+    bm[h] = __ballot(hit[h][1]);
+    if (lane == 0) wave_tot[h * kWavesPerBlock + wave] = (uint32_t)(__popcll(bp[h]) + __popcll(bm[h]));
   }
-  if (a.tally) {
-    if (hit[0] && fid[0] < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fid[0], 1u);
-    if (hit[1] && fid[1] < a.n_fid) atomicAdd(a.tally + (uint64_t)contig * a.n_fid + fid[1], 1u);
-  }
-  // Block-local compaction in canonical order (position, '+' before '-').
-  const uint64_t bp = __ballot(hit[0]), bm = __ballot(hit[1]);
-  if (lane == 0) wave_tot[wave] = (uint32_t)(__popcll(bp) + __popcll(bm));
   __syncthreads();
-  uint32_t o = popc_below(bp) + popc_below(bm), total = 0;
-  for (int w = 0; w < kWavesPerBlock; ++w) {
-    if (w < wave) o += wave_tot[w];
-    total += wave_tot[w];
-  }
+  uint32_t total = 0;
   uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
-  if (hit[0]) st[o++] = (r << 25) | fid[0];               // strand bit 24 = 0: '+'
-  if (hit[1]) st[o] = (r << 25) | (1ull << 24) | fid[1];  // '-'
+#pragma unroll
+  for (int h = 0; h < CP; ++h) {
+    uint32_t o = total + popc_below(bp[h]) + popc_below(bm[h]);
+    for (int w = 0; w < kWavesPerBlock; ++w) {
+      if (w < wave) o += wave_tot[h * kWavesPerBlock + w];
+      total += wave_tot[h * kWavesPerBlock + w];
+    }
+    const uint64_t r = r0 + t + 256u * h;
+    if (hit[h][0]) st[o++] = (r << 25) | fid[h][0];               // strand bit 24 = 0: '+'
+    if (hit[h][1]) st[o] = (r << 25) | (1ull << 24) | fid[h][1];  // '-'
+  }
   if (t == 0) a.block_counts[blockIdx.x] = total;
 }
 
