@@ -130,7 +130,10 @@ constexpr uint32_t kMaxChain = 32;
 constexpr int kProbeWin = KMA_PROBE_WIN;
 constexpr int kBlockProteins = KMA_BLOCK_PROTEINS;
 constexpr int kSetPool = KMA_SET_POOL;
-constexpr int kChainQ = 384;   // deferred overflow-chain walks per wave (u32 positions)
+#ifndef KMA_CHAIN_Q
+#define KMA_CHAIN_Q 384
+#endif
+constexpr int kChainQ = KMA_CHAIN_Q;  // deferred overflow-chain walks per wave (u32 positions)
 constexpr uint32_t kGlobalSet = 0xFFFFFFFFu;  // pset[] marker: the set lives in workspace memory
 constexpr int kWavesPerBlock = 4;
 

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+  timeout -k 10 600 python -u -m pytest $TESTS ${K_EXPR:+-k "$K_EXPR"} -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
   rc=$?; tail -2 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 for r in $RUNS; do
