@@ -11,7 +11,7 @@ fi
 for r in $RUNS; do
   v=${r%%:*}; wl=${r##*:}
   lib=kmers.anno_amd/build/libkmeranno.so; [ $v = main ] || lib=kmers.anno_amd/build/$v/libkmeranno.so
-  KMERANNO_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --workload $wl --no-cpu-baseline --no-extras > $OUT/var_${v}_$wl.log 2>&1
+  KMERANNO_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --workload $wl --no-cpu-baseline --no-extras ${EXTRA:-} > $OUT/var_${v}_$wl.log 2>&1
   rc=$?; echo "$v $wl rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/var_${v}_$wl.log) $(grep -o '"phases_ms": {[^}]*}' $OUT/var_${v}_$wl.log)"
   [ $rc -eq 0 ] || exit $rc
 done
