@@ -829,6 +829,20 @@ uint32_t block_proteins() {
   return (f >= 1 && f <= kma::kBlockProteins) ? (uint32_t)f : 4u;
 }
 
+// Deferral of short groups (annotate_kernel's two-pass grid), in probe steps: groups below it
+// are annotated after every longer one has started. A fixed-count grid is dispatched in
+// block order, so without it a long group dispatched late ends the call alone: at c2 the
+// kernel's last ~25 of ~65 us ran with a shrinking set of late long blocks
+// (profiles/r02m_block_clock.jsonl; with the groups pre-sorted longest first the kernel took
+// 50 us). Automatic for grids of more than one and at most 16 resident waves of blocks (7 per
+// CU); KMA_DEFER=0 disables it, KMA_DEFER=<steps> forces it on any batch (read per call).
+uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
+  const uint64_t slots = 7ull * (uint64_t)std::max(ws->n_cu, 1);
+  const char* e = getenv("KMA_DEFER");
+  if (e && *e) return (uint32_t)std::max(0, std::min(64, atoi(e)));
+  return n_groups > slots && n_groups <= 16 * slots ? 3u : 0u;
+}
+
 // Region bits of the partitioned path (KMA_REGION_BITS=4..16 overrides, read per call).
 int region_bits() {
   const char* e = getenv("KMA_REGION_BITS");
@@ -879,6 +893,8 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
   a.block_proteins = block_proteins();
+  a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
+  a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
   const int rb = region_bits();
   if (!protein_path(t, ws, n_seq, n_residues, rb)) {
     PhaseClock clk(ws, s, kDirectPhases, 1);
@@ -1068,6 +1084,7 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
   KMA_HIP(hipMalloc(&ws->d_cfb, chunks));
   KMA_HIP(hipMalloc(&ws->d_pcounts, 16));
   KMA_HIP(hipMalloc(&ws->d_runoff, chunks * (kma::kMaxRegions + 1) * 2));
+
   kma::PartArgs q{};
   q.n_seq = (uint32_t)std::max<uint64_t>(n_seq, 1);
   size_t tb = 0;

@@ -156,6 +156,11 @@ struct ProteinArgs {
   uint32_t n_fid;
   uint32_t* gset;   // workspace: 2 u32 per residue, sets of proteins that do not fit in LDS
   uint32_t block_proteins;  // proteins per block (1 .. kBlockProteins; the host sizes it)
+  // Two-pass grid (defer_below > 0): 2 n_groups blocks; block b < n_groups annotates group b
+  // (block_proteins proteins) if it has >= defer_below probe steps, block n_groups + b if it
+  // has fewer, so that short groups start after every long one.
+  uint32_t defer_below;
+  uint32_t n_groups;
   // List form (annotate_list_kernel): the proteins list[0 .. *list_n), one per block step.
   const uint32_t* list;
   const uint32_t* list_n;

@@ -137,6 +137,7 @@ struct ProteinSmem {
   uint32_t pset[P];      // set base in `pool`, or kGlobalSet
   uint32_t pcap[P];      // set capacity (0: no set)
   uint32_t pmin[P], pmax[P], pcnt[P];  // smallest / largest fid hit; distinct keys (or hits)
+  uint32_t skip;                       // two-pass grid: the group belongs to the other pass
   uint8_t lut[256];
 };
 static_assert(sizeof(ProteinSmem<kBlockProteins>) <= 163840 / 7,
@@ -191,10 +192,13 @@ __device__ __forceinline__ uint32_t protein_at(const uint32_t (&pb)[P + 1], uint
   return p;
 }
 
-// The block's proteins [p0, p0 + np) (np <= P), contiguous in the batch.
+// The block's proteins [p0, p0 + np) (np <= P), contiguous in the batch. pass 0 / 1: a block
+// of the two-pass grid, which annotates its group only if the group is long (pass 0) / short
+// (pass 1: fewer than defer_below probe steps); pass -1: always.
 template <int K, int M, int P>
 __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P>& sm,
-                                               const uint32_t p0, const uint32_t np) {
+                                               const uint32_t p0, const uint32_t np,
+                                               const int pass = -1) {
   constexpr int U = kProbeWin;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
@@ -205,6 +209,10 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     if (lane <= (int)np) beg = a.offsets[p0 + lane] - o0;
     const uint64_t end = __shfl_down(beg, 1, 64);
     const uint64_t lo = __shfl(beg, 0, 64), span_end = __shfl(beg, (int)np, 64);
+    if (pass >= 0 && lane == 0) {  // two-pass grid: is the group this pass's?
+      const bool short_group = span_end - lo < (uint64_t)a.defer_below * 256u * kProbeWin;
+      sm.skip = short_group != (pass == 1) ? 1u : 0u;
+    }
     if (lane <= P) sm.pbeg[lane] = (uint32_t)((lane <= (int)np ? beg : span_end) - lo);
     if (lane < P) {
       uint32_t nw = 0;
@@ -232,6 +240,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     }
   }
   __syncthreads();
+  if (pass >= 0 && sm.skip) return;  // block-uniform
   const uint32_t used = sm.chain_q[0][0];
   uint32_t pb[P + 1], pw[P];
 #pragma unroll
@@ -382,8 +391,14 @@ template <int K, int M, int P>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(
     ProteinArgs a) {
   __shared__ ProteinSmem<P> sm;
-  const uint32_t p0 = blockIdx.x * a.block_proteins;
-  annotate_block<K, M, P>(a, sm, p0, min(a.block_proteins, a.n_seq - p0));
+  // Two-pass grid (defer_below > 0): blocks [0, n_groups) annotate the long groups, blocks
+  // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
+  // one (blocks are dispatched in index order); a block whose group is the other pass's exits
+  // after reading its offsets.
+  const bool second = a.defer_below && blockIdx.x >= a.n_groups;
+  const uint32_t p0 = (blockIdx.x - (second ? a.n_groups : 0u)) * a.block_proteins;
+  annotate_block<K, M, P>(a, sm, p0, min(a.block_proteins, a.n_seq - p0),
+                          a.defer_below ? (second ? 1 : 0) : -1);
 }
 
 // The direct path for a device list of proteins (giant ones, and those of partitioned-path
@@ -776,7 +791,9 @@ struct AnnotateLaunch {
     const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= (uint32_t)P ? a.block_proteins : 4u;
     if (bp != a.block_proteins) return hipErrorInvalidValue;
     const unsigned blocks = (a.n_seq + bp - 1) / bp;
-    hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(blocks), dim3(256), 0, stream, a);
+    if (a.defer_below && a.n_groups != blocks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(a.defer_below ? 2 * blocks : blocks),
+                       dim3(256), 0, stream, a);
     return hipGetLastError();
   }
 };

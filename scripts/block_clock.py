@@ -1,0 +1,92 @@
+"""Per-block timeline of annotate_kernel (tuning only).
+
+Needs a library built with the block clock:
+    make -C kmers.anno_amd variant VNAME=clk VFLAGS=-DKMA_BLOCK_CLOCK
+    KMERANNO_LIB=kmers.anno_amd/build/clk/libkmeranno.so python scripts/block_clock.py c2
+
+Prints the kernel span, the block-duration distribution against each block's residue span, the
+number of blocks resident over time and when the tail starts.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+import bench  # noqa: E402
+from bench import K, MIN_HITS, kmeranno, synth  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    bp = int(os.environ.get("KMA_BLOCK_PROTEINS", "4"))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    sp = torch.cuda.current_stream().cuda_stream
+    n_seq, t_size, n_fid, seed = synth.CONFIGS[wl]
+    sig = synth.make_table(t_size, n_fid, seed, K)
+    residues, offsets, _, _ = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
+    if os.environ.get("ORDER") == "lpt":  # experiment: the same groups, longest span first
+        lens = np.diff(offsets).astype(np.int64)
+        gs = np.arange(0, n_seq, bp)
+        order = np.argsort(-np.add.reduceat(lens, gs), kind="stable")
+        perm = np.concatenate([np.arange(gs[g], min(gs[g] + bp, n_seq)) for g in order])
+        residues = np.concatenate([residues[offsets[i]:offsets[i + 1]] for i in perm])
+        offsets = np.concatenate([[0], np.cumsum(lens[perm])]).astype(offsets.dtype)
+    table, _ = bench.build_table(sig.keys, sig.fids, t_size, 0.5, dev, sp, 0, 1)
+    n_res = int(offsets[-1] - offsets[0])
+    ws = kmeranno.Workspace(0, n_res)
+    d_res = torch.from_numpy(residues).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    d_fid = torch.empty(n_seq, dtype=torch.int32, device=dev)
+    d_cnt = torch.empty(n_seq, dtype=torch.int32, device=dev)
+    d_st = torch.empty(n_seq, dtype=torch.uint8, device=dev)
+    for _ in range(5):
+        kmeranno.annotate_proteins_device(table, ws, d_res.data_ptr(), d_off.data_ptr(), n_seq,
+                                          n_res, MIN_HITS, 0, d_fid.data_ptr(), d_cnt.data_ptr(),
+                                          d_st.data_ptr(), 0, 0, sp)
+    torch.cuda.synchronize()
+    lib = C.CDLL(os.environ["KMERANNO_LIB"])
+    rg = os.environ.get("KMA_RANGE", "")
+    nb = min(int(rg) if rg not in ("", "0") else (n_seq + bp - 1) // bp, 65536)
+    if rg == "":  # automatic: the library's choice is not visible here; assume fixed-count
+        nb = min((n_seq + bp - 1) // bp, 65536)
+    nb = min(nb, 65535)
+    full = np.zeros(8 * 65536, np.uint64)
+    assert lib.kma_debug_block_clock(full.ctypes.data_as(C.c_void_p), C.c_uint64(8 * 65536)) == 0
+    pre = full[8 * 65535:8 * 65535 + 5].astype(np.int64)  # group_order_kernel marks
+    c = full[:8 * nb].reshape(nb, 8)
+    clk = c[:, :6].astype(np.int64)
+    live = clk[:, 5] > 0
+    clk, steps, hw = clk[live], c[live, 7].astype(np.int64), c[live, 6]
+    base = clk[:, 0].min()
+    us = (clk - base) * 10.0 / 1e3  # wall_clock64: 100 MHz
+    s, e = us[:, 0], us[:, 5]
+    dur = e - s
+    ph = np.diff(us, axis=1)  # 0-1 records, 1-2 first step, 2-3 other steps, 3-4 chains, 4-5 vote
+    pre_us = ((pre - base) * 10.0 / 1e3).tolist() if pre[1] > 0 else None
+    out = {"prepass_us": pre_us, "workload": wl, "block_proteins": bp, "range": rg, "order": os.environ.get("ORDER"), "blocks": int(live.sum()),
+           "kernel_span_us": float(e.max()), "last_start_us": float(s.max()),
+           "dur_us_pct": {q: float(np.percentile(dur, q)) for q in (5, 25, 50, 75, 95, 100)},
+           "phase_us_median": {n: float(np.median(ph[:, i])) for i, n in enumerate(
+               ["records", "first_step", "other_steps", "chain_walks", "vote"])},
+           "phase_us_p95": {n: float(np.percentile(ph[:, i], 95)) for i, n in enumerate(
+               ["records", "first_step", "other_steps", "chain_walks", "vote"])}}
+    m = steps > 1
+    if m.any():
+        out["per_later_step_us_median"] = float(np.median(ph[m, 2] / (steps[m] - 1)))
+    for st in sorted(set(steps.tolist()))[:10]:
+        mm = steps == st
+        out.setdefault("dur_by_steps", {})[int(st)] = [int(mm.sum()), float(np.median(dur[mm]))]
+    grid = np.linspace(0, e.max(), 41)
+    out["resident"] = [int(((s <= g) & (e > g)).sum()) for g in grid]
+    xcc = (hw >> np.uint64(32)).astype(np.int64)
+    out["xcc_end_us"] = [float(e[xcc == x].max()) if (xcc == x).any() else 0.0 for x in range(8)]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

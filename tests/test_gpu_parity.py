@@ -33,14 +33,17 @@ def layout(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["direct", "part"])
+@pytest.fixture(params=["direct", "defer", "part"])
 def path(request, monkeypatch):
-    """Protein paths: the direct kernel, and the region-partitioned path (forced, with 64-bucket
-    regions so that the small test tables still cut into hundreds of regions; chunks that crowd
-    one region fall back to the direct list kernel). KMA_PATH / KMA_REGION_BITS are read per
-    call."""
-    if request.param == "direct":
+    """Protein paths: the direct kernel with every group in block order (KMA_DEFER=0), the
+    direct kernel's two-pass grid deferring groups of fewer than 2 probe steps (forced on
+    every batch; automatic only for grids of 1-16 resident waves), and the region-partitioned
+    path (forced, with 64-bucket regions so that the small test tables still cut into hundreds
+    of regions; chunks that crowd one region fall back to the direct list kernel). KMA_PATH /
+    KMA_DEFER / KMA_REGION_BITS are read per call."""
+    if request.param in ("direct", "defer"):
         monkeypatch.setenv("KMA_PATH", "direct")
+        monkeypatch.setenv("KMA_DEFER", "0" if request.param == "direct" else "2")
     else:
         monkeypatch.setenv("KMA_PATH", "partitioned")
         monkeypatch.setenv("KMA_REGION_BITS", "6")
@@ -142,6 +145,26 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags):
         fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, flags)
     assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
     assert (st == 1).sum() > 500 and (st == 2).sum() > 50
+
+
+@pytest.mark.parametrize("defer", ["64", "3", "1"])
+def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defer):
+    """The direct kernel's two-pass grid: every group deferred to the second pass (64 steps),
+    the automatic threshold (3) and none (1 step); four calls in a row, block sizes 4 and 1."""
+    from kmeranno import synth
+    wl = synth.make_workload(9000, 200_000, 2000, seed=23)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
+    monkeypatch.setenv("KMA_PATH", "direct")
+    monkeypatch.setenv("KMA_DEFER", defer)
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        for bp in ("4", "1", "4", "1"):
+            monkeypatch.setenv("KMA_BLOCK_PROTEINS", bp)
+            fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0,
+                                                        n_fid=2000)
+            assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+            assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
 
 
 def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path):
@@ -279,9 +302,10 @@ def _config_table(kma, sig, lf=0.5):
     return kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=lf)
 
 
-def test_config2_size_vs_oracle(kma, oracle_c, path):
+def test_config2_size_vs_oracle(kma, oracle_c, path, monkeypatch):
     """BASELINE configs[1] at full size: 10k proteins vs the 10^7-entry table, bit-exact
-    against the oracle on the rows the batch can look up (tests/helpers.py)."""
+    against the oracle on the rows the batch can look up (tests/helpers.py). The direct case
+    also runs the automatic choice (short groups deferred here, as bench.py runs it)."""
     from kmeranno import synth
     n_seq, t_size, n_fid, seed = synth.CONFIGS["c2"]
     sig = synth.make_table(t_size, n_fid, seed, K)
@@ -290,6 +314,11 @@ def test_config2_size_vs_oracle(kma, oracle_c, path):
         assert t.info.n_buckets == 20_000_000 // kma.bucket_slots()
         assert t.info.minimizer_len == 6
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+        if path == "direct":
+            monkeypatch.delenv("KMA_DEFER")
+            got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+            for a, b in zip(got, (fid, cnt, st, tally)):
+                assert (a == b).all()
     ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, res)
     efid, ecnt, est = oracle_c.apply(ot, res, off, K, 5, 0)
     assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
