@@ -834,13 +834,15 @@ uint32_t block_proteins() {
 // block order, so without it a long group dispatched late ends the call alone: at c2 the
 // kernel's last ~25 of ~65 us ran with a shrinking set of late long blocks
 // (profiles/r02m_block_clock.jsonl; with the groups pre-sorted longest first the kernel took
-// 50 us). Automatic for grids of more than one and at most 16 resident waves of blocks (7 per
-// CU); KMA_DEFER=0 disables it, KMA_DEFER=<steps> forces it on any batch (read per call).
+// 50 us). Automatic for grids of more than one and at most 4 resident waves of blocks (7 per
+// CU): measured (profiles/r02m_defer_ab.log) c2 (1.4 waves) 66 -> 54 us, 40k proteins (5.6)
+// even, 100k (14) 3% slower, c4 / c5 7% / 3% slower when forced. KMA_DEFER=0 disables it,
+// KMA_DEFER=<steps> forces it on any batch (read per call).
 uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
   const uint64_t slots = 7ull * (uint64_t)std::max(ws->n_cu, 1);
   const char* e = getenv("KMA_DEFER");
   if (e && *e) return (uint32_t)std::max(0, std::min(64, atoi(e)));
-  return n_groups > slots && n_groups <= 16 * slots ? 3u : 0u;
+  return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
 }
 
 // Region bits of the partitioned path (KMA_REGION_BITS=4..16 overrides, read per call).

@@ -127,6 +127,26 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 // voted exactly. Windows that straddle two proteins are not probed.
 // ---------------------------------------------------------------------------------------------
 
+#ifdef KMA_BLOCK_CLOCK
+// Tuning builds only (make variant VNAME=clk VFLAGS=-DKMA_BLOCK_CLOCK, scripts/block_clock.py):
+// per block of the last protein launch, wall clock at 0 start, 1 records ready, 2 first step
+// matched, 3 steps done, 4 chain walks done, 5 end; 6 hardware ids; 7 steps.
+__device__ uint64_t g_block_clk[8 * 65536];
+#define KMA_CLK_SET(i, v)                                          \
+  do {                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 65535)                    \
+      g_block_clk[8 * blockIdx.x + (i)] = (v);                     \
+  } while (0)
+#define KMA_CLK(i) KMA_CLK_SET(i, wall_clock64())
+#define KMA_CLK_HW()                                                \
+  KMA_CLK_SET(6, (uint64_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32 | \
+                     (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)))
+#else
+#define KMA_CLK_SET(i, v) ((void)0)
+#define KMA_CLK(i) ((void)0)
+#define KMA_CLK_HW() ((void)0)
+#endif
+
 // Per-block protein records (LDS). The layout keeps 7 blocks per CU resident (<= 23,405 B).
 template <int P>
 struct ProteinSmem {
@@ -251,6 +271,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   const uint32_t span = pb[P];
   __syncthreads();  // `used` has been read by every wave
   uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
+  KMA_CLK(1);
   for (uint32_t i = t; i < used / 4; i += 256) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int p = 0; p < P; ++p) {  // block-uniform: sets in workspace memory (long proteins)
     if (sm.pset[p] != kGlobalSet || sm.pcap[p] == 0) continue;
@@ -364,8 +385,12 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       cn += (uint32_t)__popcll(m);
     }
     if (cn > (uint32_t)(kChainQ - 64 * U)) chain_flush();
+    if (x0 == 0) KMA_CLK(2);
   }
+  KMA_CLK(3);
+  KMA_CLK_SET(7, (span + stride - 1) / stride);
   if (cn) chain_flush();
+  KMA_CLK(4);
   __syncthreads();  // every record is final
   if (t < (int)np) {
     const uint32_t mn = sm.pmin[t], mx = sm.pmax[t], cnt = sm.pcnt[t];
@@ -395,11 +420,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
   // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
   // one (blocks are dispatched in index order); a block whose group is the other pass's exits
   // after reading its offsets.
+  KMA_CLK(0);
   const bool second = a.defer_below && blockIdx.x >= a.n_groups;
   const uint32_t p0 = (blockIdx.x - (second ? a.n_groups : 0u)) * a.block_proteins;
   annotate_block<K, M, P>(a, sm, p0, min(a.block_proteins, a.n_seq - p0),
                           a.defer_below ? (second ? 1 : 0) : -1);
+  KMA_CLK(5);
+  KMA_CLK_HW();
 }
+
+#ifdef KMA_BLOCK_CLOCK
+}  // namespace
+}  // namespace kma
+extern "C" int kma_debug_block_clock(uint64_t* out, uint64_t n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(kma::g_block_clk), 8 * n, 0,
+                                  hipMemcpyDeviceToHost);
+}
+namespace kma {
+namespace {
+#endif
 
 // The direct path for a device list of proteins (giant ones, and those of partitioned-path
 // chunks that crowd one region): one protein per block step, persistent blocks.

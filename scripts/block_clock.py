@@ -50,31 +50,32 @@ def main():
                                           d_st.data_ptr(), 0, 0, sp)
     torch.cuda.synchronize()
     lib = C.CDLL(os.environ["KMERANNO_LIB"])
-    rg = os.environ.get("KMA_RANGE", "")
-    nb = min(int(rg) if rg not in ("", "0") else (n_seq + bp - 1) // bp, 65536)
-    if rg == "":  # automatic: the library's choice is not visible here; assume fixed-count
-        nb = min((n_seq + bp - 1) // bp, 65536)
-    nb = min(nb, 65535)
+    n_groups = (n_seq + bp - 1) // bp
+    slots = 7 * torch.cuda.get_device_properties(0).multi_processor_count
+    dv = os.environ.get("KMA_DEFER", "")
+    two_pass = (int(dv) > 0) if dv else slots < n_groups <= 4 * slots  # kma_abi.cpp defer_below
+    nb = min(2 * n_groups if two_pass else n_groups, 65535)
     full = np.zeros(8 * 65536, np.uint64)
     assert lib.kma_debug_block_clock(full.ctypes.data_as(C.c_void_p), C.c_uint64(8 * 65536)) == 0
-    pre = full[8 * 65535:8 * 65535 + 5].astype(np.int64)  # group_order_kernel marks
     c = full[:8 * nb].reshape(nb, 8)
     clk = c[:, :6].astype(np.int64)
-    live = clk[:, 5] > 0
-    clk, steps, hw = clk[live], c[live, 7].astype(np.int64), c[live, 6]
     base = clk[:, 0].min()
+    work = clk[:, 1] > 0  # blocks that annotated a group (two-pass: the others exited early)
     us = (clk - base) * 10.0 / 1e3  # wall_clock64: 100 MHz
     s, e = us[:, 0], us[:, 5]
-    dur = e - s
-    ph = np.diff(us, axis=1)  # 0-1 records, 1-2 first step, 2-3 other steps, 3-4 chains, 4-5 vote
-    pre_us = ((pre - base) * 10.0 / 1e3).tolist() if pre[1] > 0 else None
-    out = {"prepass_us": pre_us, "workload": wl, "block_proteins": bp, "range": rg, "order": os.environ.get("ORDER"), "blocks": int(live.sum()),
-           "kernel_span_us": float(e.max()), "last_start_us": float(s.max()),
+    w = us[work]
+    steps = c[work, 7].astype(np.int64)
+    dur = w[:, 5] - w[:, 0]
+    ph = np.diff(w, axis=1)  # records, first step, other steps, chain walks, vote
+    names = ["records", "first_step", "other_steps", "chain_walks", "vote"]
+    out = {"workload": wl, "block_proteins": bp, "two_pass": bool(two_pass),
+           "order": os.environ.get("ORDER"),
+           "blocks": int(nb), "working_blocks": int(work.sum()),
+           "kernel_span_us": float(e.max()), "last_work_start_us": float(w[:, 0].max()),
+           "skipped_block_us_median": float(np.median((e - s)[~work])) if (~work).any() else None,
            "dur_us_pct": {q: float(np.percentile(dur, q)) for q in (5, 25, 50, 75, 95, 100)},
-           "phase_us_median": {n: float(np.median(ph[:, i])) for i, n in enumerate(
-               ["records", "first_step", "other_steps", "chain_walks", "vote"])},
-           "phase_us_p95": {n: float(np.percentile(ph[:, i], 95)) for i, n in enumerate(
-               ["records", "first_step", "other_steps", "chain_walks", "vote"])}}
+           "phase_us_median": {n: float(np.median(ph[:, i])) for i, n in enumerate(names)},
+           "phase_us_p95": {n: float(np.percentile(ph[:, i], 95)) for i, n in enumerate(names)}}
     m = steps > 1
     if m.any():
         out["per_later_step_us_median"] = float(np.median(ph[m, 2] / (steps[m] - 1)))
@@ -82,9 +83,10 @@ def main():
         mm = steps == st
         out.setdefault("dur_by_steps", {})[int(st)] = [int(mm.sum()), float(np.median(dur[mm]))]
     grid = np.linspace(0, e.max(), 41)
-    out["resident"] = [int(((s <= g) & (e > g)).sum()) for g in grid]
-    xcc = (hw >> np.uint64(32)).astype(np.int64)
-    out["xcc_end_us"] = [float(e[xcc == x].max()) if (xcc == x).any() else 0.0 for x in range(8)]
+    out["resident_working"] = [int(((w[:, 0] <= g) & (w[:, 5] > g)).sum()) for g in grid]
+    xcc = (c[work, 6] >> np.uint64(32)).astype(np.int64)
+    out["xcc_end_us"] = [float(w[xcc == x, 5].max()) if (xcc == x).any() else 0.0
+                         for x in range(8)]
     print(json.dumps(out))
 
 

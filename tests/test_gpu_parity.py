@@ -37,7 +37,7 @@ def layout(request, monkeypatch):
 def path(request, monkeypatch):
     """Protein paths: the direct kernel with every group in block order (KMA_DEFER=0), the
     direct kernel's two-pass grid deferring groups of fewer than 2 probe steps (forced on
-    every batch; automatic only for grids of 1-16 resident waves), and the region-partitioned
+    every batch; automatic only for grids of 1-4 resident waves), and the region-partitioned
     path (forced, with 64-bucket regions so that the small test tables still cut into hundreds
     of regions; chunks that crowd one region fall back to the direct list kernel). KMA_PATH /
     KMA_DEFER / KMA_REGION_BITS are read per call."""
