@@ -222,11 +222,29 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   constexpr int U = kProbeWin;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  // wave 0: the proteins' offsets (issued first); every wave: the span start (scalar)
+  const uint64_t beg_raw = wave == 0 && lane <= (int)np ? a.offsets[p0 + lane] : 0u;
   const uint64_t o0 = a.offsets[0];
+  const uint64_t span_lo = a.offsets[p0] - o0;
+  // The span's residues from the aligned word at or below its first byte (d_residues is
+  // 8-byte aligned): window x of the span starts at byte x + mis of `res`. The first step's
+  // words are loaded now, under the records' round trip (clamped to the batch, which is
+  // readable 32 bytes past its end; windows past the span are masked in the loop).
+  const uint8_t* res0 = a.residues + o0 + span_lo;
+  const uint32_t mis = (uint32_t)((uintptr_t)res0 & 7u);
+  const uint8_t* __restrict__ res = res0 - mis;
+  WinWords ww[U];
+  {
+    const uint64_t lim = a.n_residues - span_lo;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint32_t x = j * 256u + t;
+      ww[j] = window_words(res, (x < lim ? x : 0u) + mis);
+    }
+  }
   sm.lut[t] = a.lut[t];
   if (wave == 0) {  // the block's protein records
-    uint64_t beg = 0;
-    if (lane <= (int)np) beg = a.offsets[p0 + lane] - o0;
+    const uint64_t beg = lane <= (int)np ? beg_raw - o0 : 0u;
     const uint64_t end = __shfl_down(beg, 1, 64);
     const uint64_t lo = __shfl(beg, 0, 64), span_end = __shfl(beg, (int)np, 64);
     if (pass >= 0 && lane == 0) {  // two-pass grid: is the group this pass's?
@@ -267,7 +285,6 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   for (int i = 0; i <= P; ++i) pb[i] = __builtin_amdgcn_readfirstlane(sm.pbeg[i]);
 #pragma unroll
   for (int i = 0; i < P; ++i) pw[i] = __builtin_amdgcn_readfirstlane(sm.pwin[i]);
-  const uint64_t span_lo = a.offsets[p0] - o0;
   const uint32_t span = pb[P];
   __syncthreads();  // `used` has been read by every wave
   uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
@@ -281,11 +298,6 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   }
   __syncthreads();
 
-  // The span's residues from the aligned word at or below its first byte (d_residues is
-  // 8-byte aligned): window x of the span starts at byte x + mis of `res`.
-  const uint8_t* res0 = a.residues + o0 + span_lo;
-  const uint32_t mis = (uint32_t)((uintptr_t)res0 & 7u);
-  const uint8_t* __restrict__ res = res0 - mis;
   const uint64_t* __restrict__ slots = a.slots;
   const uint32_t nb = a.n_buckets;
   const uint8_t* lut = sm.lut;
@@ -308,12 +320,6 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   };
   // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
   // flight, so a wave's only exposed latency per step is the bucket gather.
-  WinWords ww[U];
-#pragma unroll
-  for (int j = 0; j < U; ++j) {
-    const uint32_t x = j * 256u + t;
-    ww[j] = window_words(res, (x < span ? x : 0u) + mis);
-  }
   for (uint32_t x0 = 0; x0 < span; x0 += stride) {
     uint32_t klo[U], khi[U], bk[U];  // bk: protein << kBucketBits | home bucket, or kNone
 #pragma unroll
