@@ -327,7 +327,7 @@ def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
     rate is listed, the dominant one is the headline."""
     if "annotate_kernel" in ph and len(ph) == 1:
         return roofline("windows x 64 B + residues", workload,
-                        f"annotate_kernel<{K}, {m}, 4> (direct path: probe + sets + vote)",
+                        f"annotate_kernel<{K}, {m}, 8> (direct path: probe + sets + vote)",
                         ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP + n_res, table_bytes,
                         n_win, live=live)
     alg = {"partition_kernel": (n_res + 8 * n_win, "residues + 8-B record per window"),
