@@ -965,6 +965,42 @@ int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
 }
 
 // One shard [lo, hi) of a host protein call on replica r (host buffers, synchronous).
+// Host bytes -> pinned staging -> device, pipelined: `len` bytes are cut into 8 MiB chunks;
+// up to 8 threads copy chunks into the pinned buffer and queue each chunk's DMA on `s` as soon
+// as it is staged, so the copies into pinned memory overlap each other and the transfers.
+// Small inputs take one plain copy.
+hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size_t len,
+                     int device, hipStream_t s) {
+  constexpr size_t kChunk = 8u << 20;
+  const size_t n_chunks = (len + kChunk - 1) / kChunk;
+  if (n_chunks <= 2) {
+    std::memcpy(h_pinned, src, len);
+    return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
+  }
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t n_threads = std::min<size_t>({8, hw, n_chunks});
+  std::atomic<size_t> next{0};
+  std::atomic<int> err{(int)hipSuccess};
+  auto work = [&]() {
+    if (hipSetDevice(device) != hipSuccess) {
+      err = (int)hipErrorInvalidDevice;
+      return;
+    }
+    for (size_t i; (i = next++) < n_chunks;) {
+      const size_t off = i * kChunk, n = std::min(kChunk, len - off);
+      std::memcpy(h_pinned + off, src + off, n);
+      const hipError_t e = hipMemcpyAsync(d_dst + off, h_pinned + off, n,
+                                          hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) err = (int)e;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t i = 1; i < n_threads; ++i) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return (hipError_t)err.load();
+}
+
 int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                   const uint64_t* offsets, uint32_t lo, uint32_t hi, int min_hits,
                   uint32_t flags, int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
@@ -989,14 +1025,15 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   KMA_HIP(c->h_in.reserve(in_bytes + off_bytes));
   KMA_HIP(c->h_out.reserve(out_bytes));
   if (int rc = kma_workspace_reserve_batch(c->ws, nres, n)) return rc;
-  // Stage: residues (zero padded) then rebased offsets, in one pinned buffer.
+  // Stage: residues then their zero padding, then rebased offsets, in one pinned buffer.
   uint8_t* hin = c->h_in.p;
-  std::memcpy(hin, residues + base, nres);
+  hipStream_t s = c->stream;
+  KMA_HIP(stage_h2d(c->d_in.p, hin, residues + base, nres, r.device, s));
   std::memset(hin + nres, 0, in_bytes - nres);
+  KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres, hipMemcpyHostToDevice,
+                         s));
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
   for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
-  hipStream_t s = c->stream;
-  KMA_HIP(hipMemcpyAsync(c->d_in.p, hin, in_bytes, hipMemcpyHostToDevice, s));
   KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, s));
   uint8_t* dout = c->d_out.p;
   int32_t* d_fid = reinterpret_cast<int32_t*>(dout);
@@ -1296,12 +1333,13 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
   KMA_HIP(c->d_off.reserve(n + 1));
   KMA_HIP(c->h_in.reserve(in_bytes + off_bytes + tb));
   uint8_t* hin = c->h_in.p;
-  std::memcpy(hin, dna + base, total);
+  hipStream_t s = c->stream;
+  KMA_HIP(stage_h2d(c->d_in.p, hin, dna + base, total, r.device, s));
   std::memset(hin + total, 0, in_bytes - total);
+  KMA_HIP(hipMemcpyAsync(c->d_in.p + total, hin + total, in_bytes - total,
+                         hipMemcpyHostToDevice, s));
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
   for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
-  hipStream_t s = c->stream;
-  KMA_HIP(hipMemcpyAsync(c->d_in.p, hin, in_bytes, hipMemcpyHostToDevice, s));
   KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, s));
   // d_out: [n_hits u64, pad | tally]; slot counts (strict) in d_aux; hits in d_hits.
   KMA_HIP(c->d_out.reserve(16 + tb));
