@@ -525,11 +525,32 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   __shared__ uint64_t offc[kOffCache + 1];
   __shared__ uint32_t crange[2];
   __shared__ uint32_t wave_tot[kWavesPerBlock * kContigPos];
+  __shared__ uint8_t codon[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const uint64_t base = a.offsets[0], end = base + a.total_bases;
   const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
   const uint32_t nb = a.n_buckets;
-  if (wave < 2) {  // wave 0: the tile's first contig (and its offsets), wave 1: its last
+  KMA_CLK(0);
+  if (wave == 3) codon[lane] = a.codon_codes[lane];  // LDS copy of the kernel-argument table
+  if (a.n_contig < (uint32_t)kOffCache) {
+    // Every offset fits the cache: wave 0 loads them once and finds the tile's first / last
+    // contig by ballot (the largest c with offsets[c] <= g is a prefix count; offsets[0] = base).
+    if (wave == 0) {
+      const uint32_t n = a.n_contig;
+      const uint64_t last = r0 + kContigTile < a.total_bases ? r0 + kContigTile : a.total_bases;
+      const uint64_t v = a.offsets[min((uint32_t)lane, n)];
+      const uint32_t lo = (uint32_t)__popcll(__ballot((uint32_t)lane < n && v <= base + r0)) - 1u;
+      const uint32_t hi =
+          (uint32_t)__popcll(__ballot((uint32_t)lane < n && v <= base + last - 1)) - 1u;
+      offc[lane] = __shfl(v, (int)min(lo + (uint32_t)lane, n), 64);  // offsets[min(lo + i, n)]
+      const uint64_t vn = __shfl(v, (int)n, 64);
+      if (lane == 0) {
+        offc[kOffCache] = vn;
+        crange[0] = lo;
+        crange[1] = hi;
+      }
+    }
+  } else if (wave < 2) {  // wave 0: the tile's first contig (and its offsets), wave 1: its last
     const uint64_t last = r0 + kContigTile < a.total_bases ? r0 + kContigTile : a.total_bases;
     const uint32_t c = contig_of_wave(a.offsets, a.n_contig, base + (wave ? last - 1 : r0));
     if (lane == 0) crange[wave] = c;
@@ -543,17 +564,19 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     bases[i] = (uint8_t)(g < end ? base2(a.dna[g]) : 4u);
   }
   __syncthreads();
+  KMA_CLK(1);  // tile loaded, contigs found
   const uint32_t c_lo = crange[0], nc = crange[1] - c_lo + 1;  // contigs meeting the tile
   for (int i = t; i < kSpan - 2; i += blockDim.x) {
     const uint32_t b0 = bases[i], b1 = bases[i + 1], b2 = bases[i + 2];
     if ((b0 | b1 | b2) & 4u) {
       aa_p[i] = aa_m[i] = 0;  // 'X'
     } else {
-      aa_p[i] = a.codon_codes[b0 * 16 + b1 * 4 + b2];
-      aa_m[i] = a.codon_codes[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
+      aa_p[i] = codon[b0 * 16 + b1 * 4 + b2];
+      aa_m[i] = codon[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
     }
   }
   __syncthreads();
+  KMA_CLK(2);  // translated
 
   // Each lane owns positions t + 256 h (h < kContigPos): both windows of every one of them are
   // probed with all their dwordx4 in flight before any compare.
@@ -615,6 +638,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
         for (int hh = 0; hh < kBucketHalves; ++hh) q[h][j][r][hh] = bp[4 * hh];
       }
     }
+  KMA_CLK(3);  // bucket loads issued
   bool hit[CP][2];
   uint32_t fid[CP][2];
 #pragma unroll
@@ -647,6 +671,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     }
   (void)xs;
   (void)lens;
+  KMA_CLK(4);  // matched (chain walks done)
   // Block-local compaction in canonical order (position, '+' before '-'): positions of the
   // first 256 before those of the next.
   uint64_t bp[CP], bm[CP];
@@ -671,6 +696,8 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     if (hit[h][1]) st[o] = (r << 25) | (1ull << 24) | fid[h][1];  // '-'
   }
   if (t == 0) a.block_counts[blockIdx.x] = total;
+  KMA_CLK(5);
+  KMA_CLK_HW();
 }
 
 // Peg windows (KmerReference.countPegKmers, KmerReference.java:124-147): one wave per peg;

@@ -20,8 +20,50 @@ import bench  # noqa: E402
 from bench import K, MIN_HITS, kmeranno, synth  # noqa: E402
 
 
+def contigs_timeline():
+    """c3: contigs_probe_quad_kernel's blocks (256 positions each): clock 0 start, 1 tile
+    loaded + contigs found, 2 translated, 3 bucket loads issued, 4 matched, 5 end."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    sp = torch.cuda.current_stream().cuda_stream
+    wl = synth.make_contig_workload(5_000_000, 20, 3, 10_000_000, 10_000, K)
+    n_bases = int(wl.offsets[-1] - wl.offsets[0])
+    table, _ = bench.build_table(wl.keys, wl.fids, 10_000_000, 0.5, dev, sp, 0, 1)
+    ws = kmeranno.Workspace(0)
+    ws.reserve_contigs(n_bases)
+    d_dna = torch.from_numpy(wl.dna).to(dev)
+    d_off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
+    cap = 1 << 22
+    d_hits = torch.empty(cap * kmeranno.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_nh = torch.zeros(1, dtype=torch.int64, device=dev)
+    for _ in range(5):
+        kmeranno.annotate_contigs_device(table, ws, d_dna.data_ptr(), d_off.data_ptr(),
+                                         len(wl.offsets) - 1, n_bases, 11, d_hits.data_ptr(), cap,
+                                         d_nh.data_ptr(), 0, 0, sp)
+    torch.cuda.synchronize()
+    lib = C.CDLL(os.environ["KMERANNO_LIB"])
+    nb = min((n_bases + 255) // 256, 65535)
+    full = np.zeros(8 * 65536, np.uint64)
+    assert lib.kma_debug_block_clock(full.ctypes.data_as(C.c_void_p), C.c_uint64(8 * 65536)) == 0
+    clk = full[:8 * nb].reshape(nb, 8)[:, :6].astype(np.int64)
+    us = (clk - clk[:, 0].min()) * 10.0 / 1e3
+    ph = np.diff(us, axis=1)
+    names = ["tile_and_contigs", "translate", "issue", "match", "compact_store"]
+    s, e = us[:, 0], us[:, 5]
+    grid = np.linspace(0, e.max(), 41)
+    return {"workload": "c3", "blocks": int(nb), "kernel_span_us": float(e.max()),
+            "last_start_us": float(s.max()),
+            "dur_us_pct": {q: float(np.percentile(e - s, q)) for q in (5, 50, 95, 100)},
+            "phase_us_median": {n: float(np.median(ph[:, i])) for i, n in enumerate(names)},
+            "phase_us_p95": {n: float(np.percentile(ph[:, i], 95)) for i, n in enumerate(names)},
+            "resident": [int(((s <= g) & (e > g)).sum()) for g in grid]}
+
+
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    if wl == "c3":
+        print(json.dumps(contigs_timeline()))
+        return
     bp = int(os.environ.get("KMA_BLOCK_PROTEINS", "4"))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)

@@ -401,14 +401,16 @@ def test_contigs_golden(kma, layout):
     assert (tally == expect).all()
 
 
-@pytest.mark.parametrize("gcode", [11, 4])
-def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, gcode):
+@pytest.mark.parametrize("gcode,extra", [(11, 0), (4, 0), (11, 70)])
+def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, gcode, extra):
     """All five small.gto contigs plus boundary-length contigs, ambiguous bases and RNA 'u'/'U'
     bases: every 6-frame window hit equals the oracle's, and (AppTest.java:131-138) each hit's
-    kmer is the translation of the DNA at its location."""
+    kmer is the translation of the DNA at its location. extra: that many short contigs more
+    (past 64 contigs the kernel searches the offsets instead of caching them all)."""
     contigs = [c["dna"] for c in small_gto["contigs"]]
     contigs[2] = contigs[2][:50000] + "nnnNacgtRYk" + contigs[2][50000:]
     contigs += [contigs[0][100:100 + n] for n in range(20, 36)]  # 3K-4 .. 3K+11 bases
+    contigs += [contigs[3][1000 * i:1000 * i + 40 + 37 * i] for i in range(extra)]
     # RNA bases: a stretch of contig 1 as is, with t -> u, and upper case with T -> U
     s = contigs[1][20000:26000]
     contigs += [s, s.replace("t", "u"), s.upper().replace("T", "U")]
