@@ -108,13 +108,15 @@ __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, u
                                            uint32_t b, uint64_t key, uint32_t& fid,
                                            uint32_t& sid) {
   bool hit = false, empty = false;
+  const uint32_t home = b;
   uint32_t slot = 0, steps = 1;
   while (!hit && !empty && steps < n_buckets) {  // bounded
     uint32_t bb[kWalkGroup];
     uint4 q[kWalkGroup][kBucketQuads];
 #pragma unroll
     for (int g = 0; g < kWalkGroup; ++g) {
-      b = (b + 1 == n_buckets) ? 0 : b + 1;
+      const uint32_t i = steps + g;
+      b = chain_bucket(home, i < n_buckets ? i : 0u, n_buckets);
       bb[g] = b;
       const uint4* bp = reinterpret_cast<const uint4*>(slots + (uint64_t)b * kSlotsPerBucket);
 #pragma unroll

@@ -83,10 +83,48 @@ __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
 // request is served by a line the CU just fetched. Exactness is kept by the full-key compare.
 // m = 0 is the flat layout (a hash of the whole key): the fallback for tables whose keys pile
 // onto few minimizers (low-complexity or adversarial kmer sets).
+//
+// Paired homes (KMA_PAIR_HOME = 1, the default; minimizer layouts): the minimizer hash picks a
+// PAIR of adjacent 64-byte buckets — one 128-byte L2 line — and one bit of a hash of the key
+// picks the bucket in it. A probe still reads 64 bytes, windows sharing a minimizer still share
+// a line, and a minimizer's keys spread over two buckets instead of piling into one: displaced
+// keys at c5 (m = 7) 3.55% -> 2.45%, c2 3.60% -> 2.18%; c5 4.54 -> 4.50 ms and 4.56 -> 4.52 ms
+// on two boxes, c3 / c2 even (profiles/r02q_pair/). 0 = one bucket per minimizer (round 2's
+// first layout); 2 = also walk the partner bucket first in a chain (measured no faster).
+#ifndef KMA_PAIR_HOME
+#define KMA_PAIR_HOME 1
+#endif
+__host__ __device__ inline uint32_t home_from_hash(uint32_t h, uint64_t key, int m,
+                                                   uint32_t n_buckets) {
+  if (KMA_PAIR_HOME && m != 0 && n_buckets >= 2) {
+    const uint32_t pair = (uint32_t)(((uint64_t)h * (n_buckets >> 1)) >> 32);
+    return 2u * pair + (((uint32_t)key * 0x2C1B3C6Du) >> 31);
+  }
+  return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
+}
 __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
   const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
                             : mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
-  return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
+  return home_from_hash(h, key, m, n_buckets);
+}
+
+// Step i of the probe chain of a key homed at `home` (step 0 = home; every bucket once in the
+// first n_buckets steps). Linear, or with KMA_PAIR_HOME >= 2 the home's partner in its 128-byte
+// line first (a key displaced from its home usually lands there, in the line the home probe
+// just brought into L2), then linearly on from the end of the pair.
+__host__ __device__ inline bool chain_paired(uint32_t home, uint32_t n_buckets) {
+  return KMA_PAIR_HOME >= 2 && (home | 1u) < n_buckets;
+}
+__host__ __device__ inline uint32_t chain_bucket(uint32_t home, uint32_t i, uint32_t n_buckets) {
+  if (chain_paired(home, n_buckets) && i < 2u) return home ^ i;
+  const uint64_t b = (uint64_t)(chain_paired(home, n_buckets) ? home & ~1u : home) + i;
+  return (uint32_t)(b >= n_buckets ? b - n_buckets : b);
+}
+// Inverse: the step at which the chain of `home` reaches bucket b.
+__host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32_t n_buckets) {
+  if (chain_paired(home, n_buckets) && (b ^ home) <= 1u) return b ^ home;
+  const uint32_t s = chain_paired(home, n_buckets) ? home & ~1u : home;
+  return b >= s ? b - s : b + n_buckets - s;
 }
 
 // Layout (minimizer length m, 0 = flat) of a table of n_buckets buckets for K-mers. Keys

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
     uint32_t b = home;
     bool done = false;
     for (uint32_t p = 0; p < n_buckets && !done; ++p) {
+      b = chain_bucket(home, p, n_buckets);
       for (int j = 0; j < kSlotsPerBucket; ++j) {
         uint64_t* sp = slots + (uint64_t)b * kSlotsPerBucket + j;
         uint64_t v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -61,7 +62,6 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
           break;
         }
       }
-      if (!done) b = (b + 1 == n_buckets) ? 0 : b + 1;
     }
     if (!done) {
       atomicOr(status, 1u);  // table full: cannot happen at load factor < 1
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
     const uint64_t v = slots[i];
     slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
     const uint32_t b = (uint32_t)(i / kSlotsPerBucket), h = home_bucket(slot_key(v), k, m, n_buckets);
-    const uint32_t d = (b >= h ? b - h : b + n_buckets - h) + 1u;
+    const uint32_t d = chain_step(h, b, n_buckets) + 1u;
     entries++;
     displaced += d > 1u ? 1u : 0u;
     max_probe = max(max_probe, d);

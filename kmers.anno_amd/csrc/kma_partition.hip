@@ -174,7 +174,7 @@ __device__ __forceinline__ void for_windows(const uint32_t* __restrict__ codes_w
       } else {
         h = mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u));
       }
-      f(x, p, key, (uint32_t)(((uint64_t)h * nb) >> 32));
+      f(x, p, key, home_from_hash(h, key, M, nb));
     }
   }
 }
