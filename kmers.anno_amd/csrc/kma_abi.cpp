@@ -280,9 +280,12 @@ struct Replica {
 };
 
 // Per-call resources of the host entry points on one device (kept in the table's pool).
+constexpr int kMaxPieces = 16;  // host protein calls: H2D / kernel pipeline depth (events)
 struct HostCtx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy = nullptr;            // H2D of piece i + 1 under the kernel of piece i
+  hipEvent_t piece_ready[kMaxPieces] = {};
   kma_workspace* ws = nullptr;
   Grow<uint8_t> d_in;     // residues / DNA (+ padding)
   Grow<uint64_t> d_off;   // offsets
@@ -313,6 +316,9 @@ void destroy_ctx(HostCtx* c) {
   DeviceScope ds(c->device);
   if (c->ws) kma_workspace_destroy(c->ws);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->copy) (void)hipStreamDestroy(c->copy);
+  for (hipEvent_t e : c->piece_ready)
+    if (e) (void)hipEventDestroy(e);
   c->d_in.release();
   c->d_off.release();
   c->d_out.release();
@@ -339,9 +345,12 @@ int acquire_ctx(kma_table* t, int device, HostCtx** out) {
   HostCtx* c = new HostCtx();
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  for (int i = 0; i < kMaxPieces && e == hipSuccess; ++i)
+    e = hipEventCreateWithFlags(&c->piece_ready[i], hipEventDisableTiming);
   if (e != hipSuccess) {
-    delete c;
-    return fail(KMA_E_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    destroy_ctx(c);
+    return fail(KMA_E_DEVICE, "stream / event create: %s", hipGetErrorString(e));
   }
   if (int rc = kma_workspace_create(device, &c->ws)) {
     destroy_ctx(c);
@@ -1025,25 +1034,51 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   KMA_HIP(c->h_in.reserve(in_bytes + off_bytes));
   KMA_HIP(c->h_out.reserve(out_bytes));
   if (int rc = kma_workspace_reserve_batch(c->ws, nres, n)) return rc;
-  // Stage: residues then their zero padding, then rebased offsets, in one pinned buffer.
+  // Stage: rebased offsets, then the residues (and, with the last piece, their zero padding)
+  // in pieces of whole proteins, in one pinned buffer. Copies go on the copy stream; the
+  // kernel of piece i waits for piece i's event on the compute stream, so the staging and
+  // transfer of piece i + 1 run under the kernel of piece i (pieces of >= kPieceBytes residues,
+  // at most KMA_HOST_PIECES (default 8, <= kMaxPieces; read per call); a small call is one
+  // piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (profiles/r02r_host_pipeline/).
+  constexpr uint64_t kPieceBytes = 16ull << 20;
+  const char* pe = std::getenv("KMA_HOST_PIECES");
+  const uint64_t max_pieces = pe ? std::clamp<uint64_t>(std::strtoull(pe, nullptr, 10), 1,
+                                                       kMaxPieces) : 8;
   uint8_t* hin = c->h_in.p;
-  hipStream_t s = c->stream;
-  KMA_HIP(stage_h2d(c->d_in.p, hin, residues + base, nres, r.device, s));
-  std::memset(hin + nres, 0, in_bytes - nres);
-  KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres, hipMemcpyHostToDevice,
-                         s));
+  hipStream_t s = c->stream, cs = c->copy;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
   for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
-  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, s));
+  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, cs));
   uint8_t* dout = c->d_out.p;
   int32_t* d_fid = reinterpret_cast<int32_t*>(dout);
   int32_t* d_cnt = d_fid + n;
   uint32_t* d_tally = tally ? reinterpret_cast<uint32_t*>(d_cnt + n) : nullptr;
   uint8_t* d_st = reinterpret_cast<uint8_t*>(d_cnt + n) + (tally ? n_fid * 4ull : 0);
   if (d_tally) KMA_HIP(hipMemsetAsync(d_tally, 0, n_fid * 4ull, s));
-  if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p, n, nres, min_hits, flags,
-                                    d_fid, d_cnt, d_st, d_tally, n_fid, s))
-    return rc;
+  const int n_pieces = (int)std::max<uint64_t>(1, std::min<uint64_t>(max_pieces, nres / kPieceBytes));
+  uint32_t pa = 0;  // first protein of the piece (relative to lo)
+  for (int i = 0; i < n_pieces; ++i) {
+    uint32_t pb = n;
+    if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
+      const uint64_t target = nres * (uint64_t)(i + 1) / n_pieces;
+      pb = (uint32_t)(std::lower_bound(hoff + pa, hoff + n, target) - hoff);
+    }
+    const uint64_t ra = hoff[pa], rb = i + 1 < n_pieces ? hoff[pb] : nres;
+    KMA_HIP(stage_h2d(c->d_in.p + ra, hin + ra, residues + base + ra, rb - ra, r.device, cs));
+    if (i + 1 == n_pieces) {
+      std::memset(hin + nres, 0, in_bytes - nres);
+      KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres,
+                             hipMemcpyHostToDevice, cs));
+    }
+    KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
+    KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
+    if (pb > pa)
+      if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + pa, pb - pa,
+                                        hoff[pb] - hoff[pa], min_hits, flags, d_fid + pa,
+                                        d_cnt + pa, d_st + pa, d_tally, n_fid, s))
+        return rc;
+    pa = pb;
+  }
   KMA_HIP(hipMemcpyAsync(c->h_out.p, dout, out_bytes - 16, hipMemcpyDeviceToHost, s));
   KMA_HIP(hipStreamSynchronize(s));
   const uint8_t* hout = c->h_out.p;

@@ -326,6 +326,23 @@ def test_config2_size_vs_oracle(kma, oracle_c, path, monkeypatch):
     assert (st == 1).sum() > 0.4 * n_seq
 
 
+@pytest.mark.timeout(300)
+def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c):
+    """A host call of ~48M residues runs as 2-3 pieces whose H2D overlaps the previous
+    piece's kernel (kma_abi.cpp protein_shard): every protein, including those next to piece
+    boundaries, and the tally (summed over the pieces' launches) equal the oracle's."""
+    from kmeranno import synth
+    sig = synth.make_table(1_000_000, 2000, 41, K)
+    res, off, _, _ = synth.make_queries(sig, 160_000, 41 * 1_000_003 + 17)
+    assert off[-1] >= 2 * (16 << 20)  # at least two pieces
+    with _config_table(kma, sig) as t:
+        fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=2000)
+    ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, res)
+    efid, ecnt, est = oracle_c.apply_mt(ot, res, off, K, 5, 0, threads=8)
+    assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
+
+
 @pytest.mark.timeout(600)
 def test_config5_size_sample_and_properties(kma, oracle_c, monkeypatch):
     """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 7 layout) and
