@@ -225,7 +225,9 @@ int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phase
  * residues: raw ASCII proteins concatenated; sequence s is residues[offsets[s]..offsets[s+1]).
  * min_hits >= 1 (ApplyKmerProcessor.java:91-92). out_tally (optional, length n_fid) receives
  * += 1 per CALLED protein at its fid (the APPLY report's role counts before column mapping).
- * Host form: synchronous, host buffers.                                                       */
+ * Host form: synchronous, host buffers. A batch of >= 32 MiB of residues is cut into pieces of
+ * whole proteins (up to 8; KMA_HOST_PIECES in the environment overrides, 1..16) whose staging
+ * and H2D run on the context's copy stream under the previous piece's kernel.                 */
 int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
