@@ -112,16 +112,44 @@ __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint
 // first n_buckets steps). Linear, or with KMA_PAIR_HOME >= 2 the home's partner in its 128-byte
 // line first (a key displaced from its home usually lands there, in the line the home probe
 // just brought into L2), then linearly on from the end of the pair.
+//
+// Hashed chains (KMA_CHAIN_HASH, tables of >= kHashChainMin buckets): step i >= 1 is a
+// pseudo-random bucket other than the home (a hash of (home, i)), so a full bucket's overflow
+// does not pile onto its neighbours (linear probing's primary clustering, which makes chains of
+// hundreds of buckets at load factor 0.9). The sequence may revisit a bucket; a key sits at the
+// first step that had a free slot, and a lookup still stops at the first bucket with an empty
+// slot (slots never empty again), so the walk and its stop rule are unchanged.
+#ifndef KMA_CHAIN_HASH
+#define KMA_CHAIN_HASH 0
+#endif
+constexpr uint32_t kHashChainMin = 1024;
+constexpr uint32_t kChainStepSearch = 4096;  // chain_step gives up (stats only) past this
+__host__ __device__ inline bool chain_hashed(uint32_t n_buckets) {
+  return KMA_CHAIN_HASH && n_buckets >= kHashChainMin;
+}
 __host__ __device__ inline bool chain_paired(uint32_t home, uint32_t n_buckets) {
   return KMA_PAIR_HOME >= 2 && (home | 1u) < n_buckets;
 }
 __host__ __device__ inline uint32_t chain_bucket(uint32_t home, uint32_t i, uint32_t n_buckets) {
+  if (chain_hashed(n_buckets)) {
+    if (i == 0u) return home;
+    if (KMA_CHAIN_HASH == 2 && i == 1u) return home + 1u == n_buckets ? 0u : home + 1u;
+    const uint32_t r = (uint32_t)(((uint64_t)mix32(home * 0x9E3779B1u ^ i * 0x85EBCA77u) *
+                                   (n_buckets - 1u)) >> 32);
+    const uint32_t b = home + 1u + r;  // any bucket but the home
+    return b >= n_buckets ? b - n_buckets : b;
+  }
   if (chain_paired(home, n_buckets) && i < 2u) return home ^ i;
   const uint64_t b = (uint64_t)(chain_paired(home, n_buckets) ? home & ~1u : home) + i;
   return (uint32_t)(b >= n_buckets ? b - n_buckets : b);
 }
 // Inverse: the step at which the chain of `home` reaches bucket b.
 __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32_t n_buckets) {
+  if (chain_hashed(n_buckets)) {  // the first visit (bounded search)
+    for (uint32_t i = 0; i < kChainStepSearch; ++i)
+      if (chain_bucket(home, i, n_buckets) == b) return i;
+    return kChainStepSearch;
+  }
   if (chain_paired(home, n_buckets) && (b ^ home) <= 1u) return b ^ home;
   const uint32_t s = chain_paired(home, n_buckets) ? home & ~1u : home;
   return b >= s ? b - s : b + n_buckets - s;
