@@ -15,7 +15,7 @@ namespace kma {
 //   low dword  = key bits 0..31            (never 0 for a valid key: codes are 1..31)
 //   high dword = key bits 32..39 << 24 | overflow bit << 23 | fid (23 bits)
 // A slot whose low dword is 0 is empty. A key lives in its home bucket or, if that was full,
-// in the next buckets (linear bucket probing, wrapping). The overflow bits of a bucket (one
+// in the next buckets of its probe chain (chain_bucket below: hashed steps by default). The overflow bits of a bucket (one
 // per slot, independent of the slot's key) form a filter of the keys homed there that live
 // further down the chain: overflow bit ovf_index(key) of the home bucket is set for each. A
 // lookup that misses its home bucket walks the chain only if its bit is set (then it stops at
@@ -118,9 +118,12 @@ __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint
 // does not pile onto its neighbours (linear probing's primary clustering, which makes chains of
 // hundreds of buckets at load factor 0.9). The sequence may revisit a bucket; a key sits at the
 // first step that had a free slot, and a lookup still stops at the first bucket with an empty
-// slot (slots never empty again), so the walk and its stop rule are unchanged.
+// slot (slots never empty again), so the walk and its stop rule are unchanged. Default since
+// round 2 (profiles/r02s_chain/): c5 at load factor 0.9 19.9 -> 7.7 ms (longest chain 356 ->
+// 39), 0.75 5.75 -> 4.94 ms, 0.5 even (4.50 / 4.49 ms both ways, two runs); 0 = linear chains;
+// 2 = one linear step, then hashed (7.86 / 5.17 ms at 0.9 / 0.75: not kept).
 #ifndef KMA_CHAIN_HASH
-#define KMA_CHAIN_HASH 0
+#define KMA_CHAIN_HASH 1
 #endif
 constexpr uint32_t kHashChainMin = 1024;
 constexpr uint32_t kChainStepSearch = 4096;  // chain_step gives up (stats only) past this
