@@ -97,8 +97,8 @@ __device__ __forceinline__ void scan_half(const uint4 (&q)[4], int half, uint64_
 // set): stop at the key or at the first bucket with an empty slot. Returns true on a hit, with
 // the key's fid and slot id (bucket * slots + slot: the key's identity in this table). The
 // buckets can be loaded kWalkGroup at a time (all their dwordx4 in flight, then scanned in chain
-// order): ceil(n / kWalkGroup) dependent round trips for n buckets. Measured at c5 LF 0.9 (chains
-// up to 355 buckets): 1, 2, 4 take 20.6, 20.9, 20.6 ms (profiles/r02k_walk_group.log) — high-LF
+// order): ceil(n / kWalkGroup) dependent round trips for n buckets. Measured at c5 LF 0.9 (linear
+// chains then, up to 355 buckets): 1, 2, 4 take 20.6, 20.9, 20.6 ms (profiles/r02k_walk_group.log) — high-LF
 // cost is the walks' request volume, not their latency — so 1 (fewest bytes) is the default.
 #ifndef KMA_WALK_GROUP
 #define KMA_WALK_GROUP 1

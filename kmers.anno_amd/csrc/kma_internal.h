@@ -90,7 +90,7 @@ __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
 // a line, and a minimizer's keys spread over two buckets instead of piling into one: displaced
 // keys at c5 (m = 7) 3.55% -> 2.45%, c2 3.60% -> 2.18%; c5 4.54 -> 4.50 ms and 4.56 -> 4.52 ms
 // on two boxes, c3 / c2 even (profiles/r02q_pair/). 0 = one bucket per minimizer (round 2's
-// first layout); 2 = also walk the partner bucket first in a chain (measured no faster).
+// first layout).
 #ifndef KMA_PAIR_HOME
 #define KMA_PAIR_HOME 1
 #endif
@@ -108,10 +108,7 @@ __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint
   return home_from_hash(h, key, m, n_buckets);
 }
 
-// Step i of the probe chain of a key homed at `home` (step 0 = home; every bucket once in the
-// first n_buckets steps). Linear, or with KMA_PAIR_HOME >= 2 the home's partner in its 128-byte
-// line first (a key displaced from its home usually lands there, in the line the home probe
-// just brought into L2), then linearly on from the end of the pair.
+// Step i of the probe chain of a key homed at `home` (step 0 = home).
 //
 // Hashed chains (KMA_CHAIN_HASH, tables of >= kHashChainMin buckets): step i >= 1 is a
 // pseudo-random bucket other than the home (a hash of (home, i)), so a full bucket's overflow
@@ -120,8 +117,10 @@ __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint
 // first step that had a free slot, and a lookup still stops at the first bucket with an empty
 // slot (slots never empty again), so the walk and its stop rule are unchanged. Default since
 // round 2 (profiles/r02s_chain/): c5 at load factor 0.9 19.9 -> 7.7 ms (longest chain 356 ->
-// 39), 0.75 5.75 -> 4.94 ms, 0.5 even (4.50 / 4.49 ms both ways, two runs); 0 = linear chains;
-// 2 = one linear step, then hashed (7.86 / 5.17 ms at 0.9 / 0.75: not kept).
+// 39), 0.75 5.75 -> 4.94 ms, 0.5 even (4.50 / 4.49 ms both ways, two runs); 0 = linear chains
+// (every bucket once in the first n_buckets steps; also tables below kHashChainMin buckets).
+// Measured and not kept: one linear step, then hashed (7.86 / 5.17 ms at 0.9 / 0.75), and with
+// linear chains, the home's partner in its 128-byte line first (no faster).
 #ifndef KMA_CHAIN_HASH
 #define KMA_CHAIN_HASH 1
 #endif
@@ -130,32 +129,25 @@ constexpr uint32_t kChainStepSearch = 4096;  // chain_step gives up (stats only)
 __host__ __device__ inline bool chain_hashed(uint32_t n_buckets) {
   return KMA_CHAIN_HASH && n_buckets >= kHashChainMin;
 }
-__host__ __device__ inline bool chain_paired(uint32_t home, uint32_t n_buckets) {
-  return KMA_PAIR_HOME >= 2 && (home | 1u) < n_buckets;
-}
 __host__ __device__ inline uint32_t chain_bucket(uint32_t home, uint32_t i, uint32_t n_buckets) {
   if (chain_hashed(n_buckets)) {
     if (i == 0u) return home;
-    if (KMA_CHAIN_HASH == 2 && i == 1u) return home + 1u == n_buckets ? 0u : home + 1u;
     const uint32_t r = (uint32_t)(((uint64_t)mix32(home * 0x9E3779B1u ^ i * 0x85EBCA77u) *
                                    (n_buckets - 1u)) >> 32);
     const uint32_t b = home + 1u + r;  // any bucket but the home
     return b >= n_buckets ? b - n_buckets : b;
   }
-  if (chain_paired(home, n_buckets) && i < 2u) return home ^ i;
-  const uint64_t b = (uint64_t)(chain_paired(home, n_buckets) ? home & ~1u : home) + i;
+  const uint64_t b = (uint64_t)home + i;
   return (uint32_t)(b >= n_buckets ? b - n_buckets : b);
 }
-// Inverse: the step at which the chain of `home` reaches bucket b.
+// Inverse (table statistics): the step at which the chain of `home` first reaches bucket b.
 __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32_t n_buckets) {
-  if (chain_hashed(n_buckets)) {  // the first visit (bounded search)
+  if (chain_hashed(n_buckets)) {
     for (uint32_t i = 0; i < kChainStepSearch; ++i)
       if (chain_bucket(home, i, n_buckets) == b) return i;
     return kChainStepSearch;
   }
-  if (chain_paired(home, n_buckets) && (b ^ home) <= 1u) return b ^ home;
-  const uint32_t s = chain_paired(home, n_buckets) ? home & ~1u : home;
-  return b >= s ? b - s : b + n_buckets - s;
+  return b >= home ? b - home : b + n_buckets - home;
 }
 
 // Layout (minimizer length m, 0 = flat) of a table of n_buckets buckets for K-mers. Keys
