@@ -156,10 +156,14 @@ __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32
 // 1 - 2/(K - m + 2): 1/2 for m = 6, 1/3 for m = 7. Simulated home-bucket loads of uniform
 // keys at load factor 0.5: 8-slot buckets leave 1.8% of 1e7 keys and 12% of
 // 1e8 keys past their home bucket at m = 6, 1.0% / 2.5% at m = 7; 16-slot buckets 0.25% / 4.2%
-// at m = 6. So m = 6 up to kMinimizer6Buckets buckets (16.8M keys at load factor 0.5 either
-// way), else 7 (m <= K). KMA_MINIMIZER=0|6|7 in the environment forces a layout (read per
-// call: tests run every layout in one process). Defined in kma_abi.cpp.
-constexpr uint64_t kMinimizer6Buckets = kSlotsPerBucket == 16 ? (1ull << 21) : (1ull << 22);
+// at m = 6. With paired homes and hashed chains (above) m = 6's displaced keys cost short walks:
+// at c5 (10^8 keys, 2^24.6 buckets) m = 6 displaces 7.7% (chain 10) and takes 4.28 ms against
+// m = 7's 4.50-4.54 (2.4% displaced; two runs each, profiles/r02t_final/layout_ab.log): its 12%
+// fewer line requests win. So m = 6 up to kMinimizer6Buckets buckets (134M keys at load factor
+// 0.5; 20^6 = 64M 6-mers then cover ~2 minimizers per bucket pair), else 7 (m <= K).
+// KMA_MINIMIZER=0|6|7 in the environment forces a layout (read per call: tests run every layout
+// in one process). Defined in kma_abi.cpp.
+constexpr uint64_t kMinimizer6Buckets = kSlotsPerBucket == 16 ? (1ull << 24) : (1ull << 25);
 int minimizer_len(int k, uint64_t n_buckets);
 // The table creators also build a minimizer-layout table flat when more than this fraction of
 // its keys were displaced past their home bucket, or a chain is longer than kMaxChain buckets,

@@ -51,11 +51,11 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
 
 
 def test_table_layout_host_helper(native_lib, monkeypatch):
-    """Layout choice: minimizer m = 6 up to 16.8M keys at load factor 0.5 (2^25 slots), m = 7
+    """Layout choice: minimizer m = 6 up to 134M keys at load factor 0.5 (2^28 slots), m = 7
     beyond; KMA_MINIMIZER forces 0 (flat), 6 or 7, read per call."""
     import kmeranno
     monkeypatch.delenv("KMA_MINIMIZER", raising=False)
-    nb6 = (1 << 25) // kmeranno.bucket_slots()
+    nb6 = (1 << 28) // kmeranno.bucket_slots()
     assert kmeranno.layout_for(8, nb6) == 6
     assert kmeranno.layout_for(8, nb6 + 1) == 7
     assert kmeranno.layout_for(5, 1 << 30) == 5  # m <= K

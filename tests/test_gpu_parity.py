@@ -23,8 +23,8 @@ K = 8
 
 @pytest.fixture(params=["auto", "7", "0"], ids=["m-auto", "m7", "flat"])
 def layout(request, monkeypatch):
-    """Table layouts: the size-derived minimizer layout (m = 6 up to 16.8M keys at load factor
-    0.5), the m = 7 layout of larger tables (c5), and the flat fallback (KMA_MINIMIZER is read
+    """Table layouts: the size-derived minimizer layout (m = 6 up to 134M keys at load factor
+    0.5, c5 included), the m = 7 layout of larger tables, and the flat fallback (KMA_MINIMIZER is read
     per table creation)."""
     if request.param == "auto":
         monkeypatch.delenv("KMA_MINIMIZER", raising=False)
@@ -345,7 +345,7 @@ def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c):
 
 @pytest.mark.timeout(600)
 def test_config5_size_sample_and_properties(kma, oracle_c, monkeypatch):
-    """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 7 layout) and
+    """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 6 layout since hashed chains) and
     the 1M-protein batch. A random 20k-protein sample of the batch is bit-exact against the
     oracle; the whole batch is checked by properties: a second call on shuffled-size shards
     (device entry point on pointer offsets) gives identical outputs, the tally equals the
@@ -358,7 +358,7 @@ def test_config5_size_sample_and_properties(kma, oracle_c, monkeypatch):
     print(f"c5 workload generated: {len(res)} residues", flush=True)
     dev = torch.device("cuda", 0)
     with _config_table(kma, sig) as t:
-        assert t.info.minimizer_len == 7 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
+        assert t.info.minimizer_len == 6 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
         assert t.info.n_entries > 0.99 * t_size
         monkeypatch.delenv("KMA_PATH", raising=False)  # automatic: the partitioned path here
         monkeypatch.delenv("KMA_REGION_BITS", raising=False)
