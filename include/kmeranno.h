@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 3
+#define KMA_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -84,13 +84,17 @@ extern "C" {
 #define KMA_F_MULTISET 0x2u
 
 /* ---- key packing ---------------------------------------------------------------------------
- * A kmer of K <= 8 residues packs into 5*K bits, first residue most significant:
+ * A kmer of K <= 12 residues packs into 5*K bits, first residue most significant:
  *   key = sum_j code(s[j]) << 5*(K-1-j),  code('A'..'Z') = 1..26, code('*') = 27,
  *   codes 28..31 are assigned (in byte order) to at most four other bytes that occur in the
  *   table's kmers; 0 never occurs, so key 0 is the empty-slot sentinel. Packing is injective,
  *   so key equality is exactly the String.equals of the reference's HashMap lookup.
- * A table slot holds the key's 40 bits, an overflow-filter bit and the fid, so fid < 2^23.   */
-#define KMA_MAX_K 8
+ * Tables of K <= 8 ("narrow") keep the key's 40 bits, an overflow-filter bit and the fid in one
+ * 8-byte slot (kma_bucket_slots() per bucket); tables of K = 9..12 ("wide": the projector's
+ * -K, KmerProcessor.java:86-88) use 16-byte slots, four per 64-byte bucket. fid < 2^23.
+ * The protein path (kma_annotate_proteins*) takes narrow tables: apply's ProteinKmers keeps
+ * K = 8 whatever the table holds (ApplyKmerProcessor.java:108 sets KmerReference's K only). */
+#define KMA_MAX_K 12
 #define KMA_MAX_FID ((1u << 23) - 1u)
 
 
@@ -112,7 +116,7 @@ typedef struct kma_table_info {
                             0 = flat (hash of the whole key)                               */
   uint64_t n_displaced;  /* keys stored past their home bucket (overflow chains)            */
   int32_t n_replicas;    /* devices holding a copy of the slot array                        */
-  int32_t reserved;
+  int32_t slots_per_bucket; /* kma_bucket_slots_for(k): 8 (16) narrow, 4 wide               */
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -151,14 +155,17 @@ int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t
                             int device, double load_factor, kma_table** out);
 int kma_table_info_get(const kma_table* table, kma_table_info* out);
 int kma_table_destroy(kma_table* table);
-/* u64 slots per bucket of this build: 8 (64-byte buckets, the default) or 16 (128-byte). */
+/* u64 slots per bucket of this build's narrow tables: 8 (64-byte buckets, the default) or 16
+ * (128-byte). kma_bucket_slots_for(k): slots per bucket of a table of K-mers (narrow: the
+ * former; wide, K 9..12: 4 slots of 16 bytes); 0 for an invalid K.                          */
 int kma_bucket_slots(void);
-/* The table's layout choice: minimizer layouts (m = min(K,6) up to 2^22 buckets, else
- * min(K,7)); when more than 15% of the keys land past their home bucket or a chain exceeds 32
- * buckets (keys that pile onto few minimizers), the creators above also build the table flat
- * (layout 0) and keep it if it halves the displaced keys or the longest chain.
- * kma_table_layout_for gives the size-derived layout (KMA_MINIMIZER=0|6|7 in the environment
- * forces one).                                                                                */
+int kma_bucket_slots_for(int k);
+/* The table's layout choice: minimizer layouts (m = min(K,6) up to 2^25 narrow buckets — 2^24
+ * with 16-slot buckets, 2^26 wide ones — else min(K,7)); when more than 15% of the keys land
+ * past their home bucket or a chain exceeds 32 buckets (keys that pile onto few minimizers),
+ * the creators above also build the table flat (layout 0) and keep it if it halves the
+ * displaced keys or the longest chain. kma_table_layout_for gives the size-derived layout
+ * (KMA_MINIMIZER=0|6|7 in the environment forces one).                                       */
 int kma_table_layout_for(int k, uint64_t n_buckets);
 
 /* ---- replicas (the table replicated on every device of the node) -------------
@@ -175,9 +182,10 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
 
 /* Device-resident construction for hosts that own device memory (e.g. a torch allocation
  * that is later broadcast over RCCL to the other GPUs of the node).
- *   kma_table_buckets_for : bucket count for n keys at the load factor
- *   kma_table_build_device: d_slots (n_buckets * S * 8 bytes) and d_winner (n_buckets * S u32,
- *                           S = kma_bucket_slots()) are
+ *   kma_table_buckets_for : bucket count for n narrow (K <= 8) keys at the load factor;
+ *                           kma_table_buckets_for_k for any K
+ *   kma_table_build_device: d_slots (info.bytes: n_buckets * 64 bytes, 128 in the 16-slot build)
+ *                           and d_winner (n_buckets * S u32, S = kma_bucket_slots_for(k)) are
  *                           caller scratch; keys/fids are device arrays of K-mers; layout -1 =
  *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7); builds on
  *                           `stream`; d_status (4 u32) receives {table full, entries, longest
@@ -185,6 +193,7 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
  *                           displaced keys are many); fids are masked to 23 bits.
  *   kma_table_wrap_device : adopt an already-built slot array of that layout (not owned).    */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
+uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k);
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
                            uint32_t* d_winner, const uint64_t* d_keys, const uint32_t* d_fids,
                            uint64_t n, uint32_t* d_status, void* stream);
@@ -195,11 +204,10 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 
 /* ---- workspaces -----------------------------------------------------------------------------
  * Per-stream scratch of the _device entry points. kma_workspace_reserve_batch sizes it for
- * calls of up to n_residues residues (< 2^32 - 128) and n_seq proteins: 12 bytes per residue
- * of HBM (the distinct-kmer sets of proteins too long for LDS; the partitioned path's 8-byte
- * records and 4-byte results), 20 bytes per protein and the partitioned path's chunk tables.
- * kma_workspace_reserve(ws, n) = _reserve_batch(ws, n, n / 16 + 256). A call with more proteins
- * than reserved takes the direct path. These are the only calls that allocate.              */
+ * calls of up to n_residues residues (< 2^32 - 128; n_seq < 2^31 is checked, nothing is kept
+ * per protein): 8 bytes per residue of HBM (the distinct-kmer sets of proteins too long for
+ * LDS). kma_workspace_reserve(ws, n) = _reserve_batch(ws, n, n / 16 + 256). These are the only
+ * calls that allocate.                                                                       */
 int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t n_seq);
@@ -207,11 +215,10 @@ int kma_workspace_destroy(kma_workspace* ws);
 /* Device timing of the _device calls made with this workspace: with enable = 1 each call
  * records hipEvents on its stream at its phase boundaries. Not for graph capture. Both reads
  * synchronise on the recorded events (the last 256 calls) and clear the accumulators.
- *   _phases_read : the calls laid out like the last one (same path): their count, the number
- *                  of phases and each phase's summed milliseconds and name (static strings):
- *                  direct protein path {annotate_kernel}; partitioned {chunking,
- *                  partition_kernel, probe_regions_kernel, vote_chunks_kernel,
- *                  annotate_list_kernel}; contigs {contigs_probe_kernel, scan_emit}.
+ *   _phases_read : the calls laid out like the last one (same entry point): their count, the
+ *                  number of phases and each phase's summed milliseconds and name (static
+ *                  strings): proteins {annotate_kernel}; contigs {contigs_probe_kernel,
+ *                  scan_emit}.
  *   _timing_read : kernel_ms = proteins: every phase / contigs: the probe; rest_ms = contigs:
  *                  scan + emit.                                                              */
 #define KMA_MAX_PHASES 8
@@ -233,13 +240,11 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                           uint32_t* out_tally, uint32_t n_fid);
 /* Device form: every pointer is device memory on the workspace's device (the table has a
- * replica there); `d_residues` is 8-byte aligned and readable for 32 bytes past offsets[n_seq]; n_residues =
- * offsets[n_seq] - offsets[0] (<= the workspace reservation); d_tally (n_fid u32) is
- * accumulated into, not cleared. Asynchronous on `stream`. Two forms, same results: the direct
- * path (one kernel: each window probes the table where it stands) and, for batches with >= 4
- * windows per table bucket, the region-partitioned path (windows sorted to table regions, each
- * region probed from one XCD's L2). KMA_PATH=direct|partitioned in the environment forces one
- * (read per call); KMA_REGION_BITS=4..16 sets the region size (default 15: 2 MiB).           */
+ * replica there); `d_residues` is 8-byte aligned and readable for 32 bytes past
+ * offsets[n_seq]; n_residues = offsets[n_seq] - offsets[0] (<= the workspace reservation);
+ * d_tally (n_fid u32) is accumulated into, not cleared. Asynchronous on `stream`: one kernel
+ * launch (annotate_kernel: each window probes the table where it stands, per-protein sets and
+ * the vote in LDS).                                                                           */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
                                  uint32_t n_seq, uint64_t n_residues, int min_hits,
@@ -346,8 +351,9 @@ int kma_hash_annotate(const uint8_t* genome_residues, const uint64_t* genome_off
  * isGood) and no buffered protein contains it. Output: (packed key, role) rows sorted by key
  * (the reference prints HashMap order: compare as sets); KMA_E_CAPACITY with *n_out = needed
  * if cap is too small; KMA_E_ALPHABET if a counted window holds a byte outside A-Z / '*'.
- * Roles < 2^24 - 1. Runs on the device: window packing, radix sort of key << 24 | role,
- * unique, one-role filter, select.                                                          */
+ * Roles < 2^24 - 1; K 1..12; < 2^31 residues. Runs on the device: window packing, radix sort
+ * of the (key, role) pairs by key, RoleCounter per key run (one role, no buffered protein),
+ * select.                                                                                    */
 int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const int32_t* roles,
                          uint32_t n_seq, int k, uint32_t flags, int device, uint64_t* out_keys,
                          uint32_t* out_roles, uint64_t cap, uint64_t* n_out);

@@ -46,7 +46,8 @@ int kma::minimizer_len(int k, uint64_t n_buckets) {
   if (f == 0) return 0;
   if (f == 6) return m6;
   if (f == 7) return m7;
-  return n_buckets <= kma::kMinimizer6Buckets ? m6 : m7;
+  const uint64_t lim = kma::wide_k(k) ? kma::kMinimizer6BucketsWide : kma::kMinimizer6Buckets;
+  return n_buckets <= lim ? m6 : m7;
 }
 
 namespace {
@@ -159,6 +160,17 @@ int check_k(int k) {
   return KMA_OK;
 }
 
+// Slot array geometry of a table of K-mers: narrow (K <= 8, kSlotsPerBucket u64 slots per
+// bucket) or wide (K 9..12, four 16-byte slots per 64-byte bucket; kma_internal.h).
+uint64_t bucket_bytes(int k) { return kma::wide_k(k) ? 64u : (uint64_t)kma::kBucketBytes; }
+uint64_t buckets_for_k(uint64_t n_keys, double load_factor, int k) {
+  if (load_factor <= 0) load_factor = 0.5;
+  const int spb = kma::slots_for_k(k);
+  const double slots = (double)(n_keys ? n_keys : 1) / load_factor;
+  const uint64_t nb = (uint64_t)((slots + spb - 1) / spb);
+  return nb < 1 ? 1 : nb;
+}
+
 // Pack rows [lo, hi) with the LUT; 0 for rows of the wrong length or with unencodable bytes.
 void pack_rows(const uint8_t* lut, const char* text, const uint64_t* off, uint64_t lo, uint64_t hi,
                int k, uint64_t* keys) {
@@ -236,24 +248,8 @@ std::vector<uint32_t> shard_bounds(const uint64_t* off, uint32_t n, int parts) {
 struct kma_workspace {
   int device = 0;
   int n_cu = 256;
-  uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue; the
-                               // partitioned path's records (u64 per residue) share it
+  uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
   uint64_t res_cap = 0;        // residues per call
-  // Partitioned protein path (kma_internal.h): results (u32 per residue), per-protein chunk
-  // flags / scan / direct-path list (seq_cap proteins), chunk tables (chunk_cap chunks) and the
-  // region offsets (u16 per chunk and region, for up to kMaxRegions regions).
-  uint32_t* d_pres = nullptr;
-  uint64_t* d_pflags = nullptr;
-  uint64_t* d_pexcl = nullptr;
-  uint32_t* d_plist = nullptr;
-  uint32_t* d_cfirst = nullptr;
-  uint32_t* d_cend = nullptr;
-  uint8_t* d_cfb = nullptr;
-  uint32_t* d_pcounts = nullptr;
-  uint16_t* d_runoff = nullptr;
-  void* d_ptemp = nullptr;
-  size_t ptemp_bytes = 0;
-  uint64_t seq_cap = 0, chunk_cap = 0;
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
   uint64_t* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
@@ -302,7 +298,10 @@ struct kma_table {
   uint64_t n_buckets = 0;
   uint8_t lut[256] = {};
   kma_table_info info = {};
+  // Replicas: appended by kma_table_replicate while host or device calls may run on the table,
+  // so they are read and appended under reps_mu; calls work on a copy (replicas() below).
   std::vector<Replica> reps;
+  mutable std::mutex reps_mu;
   std::mutex pool_mu;
   std::vector<HostCtx*> idle;  // host contexts not in use
 };
@@ -367,14 +366,28 @@ struct CtxGuard {
   kma_table* t;
   HostCtx* c;
   ~CtxGuard() {
-    if (c) release_ctx(t, c);
+    if (!c) return;
+    // A call that failed after queueing work returns early: let the context's copies and
+    // kernels drain before the next call reuses its pinned and device buffers.
+    (void)hipStreamSynchronize(c->copy);
+    (void)hipStreamSynchronize(c->stream);
+    release_ctx(t, c);
   }
 };
 
-const Replica* replica_on(const kma_table* t, int device) {
+// A copy of the table's replicas (safe against a concurrent kma_table_replicate).
+std::vector<Replica> replicas(const kma_table* t) {
+  std::lock_guard<std::mutex> g(t->reps_mu);
+  return t->reps;
+}
+bool replica_on(const kma_table* t, int device, Replica* out) {
+  std::lock_guard<std::mutex> g(t->reps_mu);
   for (const Replica& r : t->reps)
-    if (r.device == device) return &r;
-  return nullptr;
+    if (r.device == device) {
+      *out = r;
+      return true;
+    }
+  return false;
 }
 
 int add_replica(kma_table* t, int device, uint64_t* d_slots, bool owned) {
@@ -390,6 +403,7 @@ int add_replica(kma_table* t, int device, uint64_t* d_slots, bool owned) {
     if (r.d_lut) (void)hipFree(r.d_lut);
     return fail(KMA_E_DEVICE, "table LUT upload: %s", hipGetErrorString(e));
   }
+  std::lock_guard<std::mutex> g(t->reps_mu);
   t->reps.push_back(r);
   t->info.n_replicas = (int32_t)t->reps.size();
   return KMA_OK;
@@ -402,7 +416,8 @@ kma_table* new_table(int device, int k, int m, uint64_t n_buckets, const uint8_t
   t->n_buckets = n_buckets;
   std::memcpy(t->lut, lut, 256);
   t->info.n_buckets = n_buckets;
-  t->info.bytes = n_buckets * kma::kBucketBytes;
+  t->info.bytes = n_buckets * bucket_bytes(k);
+  t->info.slots_per_bucket = kma::slots_for_k(k);
   t->info.k = k;
   t->info.device = device;
   t->info.minimizer_len = m;
@@ -426,10 +441,10 @@ void free_table(kma_table* t) {
 int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m, uint32_t* d_winner,
                     const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, uint32_t* d_status,
                     hipStream_t s) {
-  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than %llu buckets",
-                                          (unsigned long long)kMaxBuckets);
-  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * kma::kBucketBytes, s));
-  KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::kSlotsPerBucket * sizeof(uint32_t), s));
+  if (n_buckets >= kMaxBuckets) return fail(KMA_E_INVALID, "%llu buckets or more",
+                                           (unsigned long long)kMaxBuckets);
+  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * bucket_bytes(k), s));
+  KMA_HIP(hipMemsetAsync(d_winner, 0, n_buckets * kma::slots_for_k(k) * sizeof(uint32_t), s));
   KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
   KMA_HIP(kma::launch_build_insert(d_slots, d_winner, (uint32_t)n_buckets, k, m, d_keys, n,
                                    d_status, s));
@@ -446,15 +461,15 @@ int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m, uint32_
 // minimizer one stays. KMA_MINIMIZER forces a layout.
 int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, int k,
                             int device, double lf, const uint8_t lut[256], kma_table** out) {
-  const uint64_t nb = kma_table_buckets_for(n, lf);
-  if (nb > kMaxBuckets)
+  const uint64_t nb = buckets_for_k(n, lf, k);
+  if (nb >= kMaxBuckets)
     return fail(KMA_E_INVALID, "table too large: %llu buckets", (unsigned long long)nb);
   DevBufs tmp;
   uint32_t *d_winner, *d_status;
-  KMA_HIP(tmp.alloc(&d_winner, nb * kma::kSlotsPerBucket * 4));
+  KMA_HIP(tmp.alloc(&d_winner, nb * kma::slots_for_k(k) * 4));
   KMA_HIP(tmp.alloc(&d_status, 16));
   auto build = [&](int m, uint64_t** slots, uint32_t st[4]) -> int {
-    KMA_HIP(hipMalloc(slots, nb * kma::kBucketBytes));
+    KMA_HIP(hipMalloc(slots, nb * bucket_bytes(k)));
     int rc = build_on_device(*slots, nb, k, m, d_winner, d_keys, d_fids, n, d_status, nullptr);
     if (rc == KMA_OK) {
       hipError_t e = hipMemcpy(st, d_status, 16, hipMemcpyDeviceToHost);
@@ -570,11 +585,14 @@ int kma_device_count(int* out_n) {
 }
 
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor) {
-  if (load_factor <= 0) load_factor = 0.5;
-  const double slots = (double)(n_keys ? n_keys : 1) / load_factor;
-  uint64_t nb = (uint64_t)((slots + kma::kSlotsPerBucket - 1) / kma::kSlotsPerBucket);
-  return nb < 1 ? 1 : nb;
+  return buckets_for_k(n_keys, load_factor, kma::kMaxNarrowK);
 }
+
+uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k) {
+  return buckets_for_k(n_keys, load_factor, k);
+}
+
+int kma_bucket_slots_for(int k) { return check_k(k) ? 0 : kma::slots_for_k(k); }
 
 int kma_table_layout_for(int k, uint64_t n_buckets) { return kma::minimizer_len(k, n_buckets); }
 
@@ -629,10 +647,10 @@ int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t
 }
 
 int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
-  if (!t || n_devices < 0 || (n_devices && !device_ids) || t->reps.empty())
+  if (!t || n_devices < 0 || (n_devices && !device_ids) || replicas(t).empty())
     return fail(KMA_E_INVALID, "null argument");
-  const Replica& src = t->reps[0];
-  const uint64_t bytes = t->n_buckets * kma::kBucketBytes;
+  const Replica src = replicas(t)[0];
+  const uint64_t bytes = t->n_buckets * bucket_bytes(t->k);
   for (int i = 0; i < n_devices; ++i) {
     const int dev = device_ids[i];
     int n_dev = 0;
@@ -679,8 +697,9 @@ int kma_table_create_replicated(const char* text, const uint64_t* offsets, const
 
 int kma_table_replicas(const kma_table* t, int* n, int* device_ids, int cap) {
   if (!t || !n) return fail(KMA_E_INVALID, "null argument");
-  *n = (int)t->reps.size();
-  for (int i = 0; i < *n && i < cap && device_ids; ++i) device_ids[i] = t->reps[i].device;
+  const std::vector<Replica> reps = replicas(t);
+  *n = (int)reps.size();
+  for (int i = 0; i < *n && i < cap && device_ids; ++i) device_ids[i] = reps[i].device;
   return KMA_OK;
 }
 
@@ -712,8 +731,8 @@ int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
 int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, int device,
                           kma_table** out) {
   if (!d_slots || !out || !n_buckets) return fail(KMA_E_INVALID, "null argument");
-  if (n_buckets > kMaxBuckets) return fail(KMA_E_INVALID, "more than %llu buckets",
-                                          (unsigned long long)kMaxBuckets);
+  if (n_buckets >= kMaxBuckets) return fail(KMA_E_INVALID, "%llu buckets or more",
+                                           (unsigned long long)kMaxBuckets);
   if (int rc = check_k(k)) return rc;
   const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout;
   if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
@@ -730,10 +749,10 @@ int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, 
 }
 
 int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes) {
-  if (!table || !d_slots || !bytes || table->reps.empty())
+  if (!table || !d_slots || !bytes || replicas(table).empty())
     return fail(KMA_E_INVALID, "null argument");
-  *d_slots = table->reps[0].d_slots;
-  *bytes = table->n_buckets * kma::kBucketBytes;
+  *d_slots = replicas(table)[0].d_slots;
+  *bytes = table->n_buckets * bucket_bytes(table->k);
   return KMA_OK;
 }
 
@@ -741,19 +760,9 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 
 namespace {
 void free_protein_scratch(kma_workspace* ws) {
-  for (void* p : {(void*)ws->d_gset, (void*)ws->d_pres, (void*)ws->d_pflags, (void*)ws->d_pexcl,
-                  (void*)ws->d_plist, (void*)ws->d_cfirst, (void*)ws->d_cend, (void*)ws->d_cfb,
-                  (void*)ws->d_pcounts, (void*)ws->d_runoff, ws->d_ptemp})
-    if (p) (void)hipFree(p);
+  if (ws->d_gset) (void)hipFree(ws->d_gset);
   ws->d_gset = nullptr;
-  ws->d_pres = nullptr;
-  ws->d_pflags = ws->d_pexcl = nullptr;
-  ws->d_plist = ws->d_cfirst = ws->d_cend = ws->d_pcounts = nullptr;
-  ws->d_cfb = nullptr;
-  ws->d_runoff = nullptr;
-  ws->d_ptemp = nullptr;
-  ws->ptemp_bytes = 0;
-  ws->res_cap = ws->seq_cap = ws->chunk_cap = 0;
+  ws->res_cap = 0;
 }
 
 void free_contig_scratch(kma_workspace* ws) {
@@ -824,8 +833,6 @@ struct PhaseClock {
 };
 
 const char* const kDirectPhases[] = {"annotate_kernel"};
-const char* const kPartPhases[] = {"chunking", "partition_kernel", "probe_regions_kernel",
-                                   "vote_chunks_kernel", "annotate_list_kernel"};
 const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
 // Proteins per annotate_kernel block: 4 (KMA_BLOCK_PROTEINS=1..8 overrides, read per call).
@@ -852,31 +859,6 @@ uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
   const char* e = getenv("KMA_DEFER");
   if (e && *e) return (uint32_t)std::max(0, std::min(64, atoi(e)));
   return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
-}
-
-// Region bits of the partitioned path (KMA_REGION_BITS=4..16 overrides, read per call).
-int region_bits() {
-  const char* e = getenv("KMA_REGION_BITS");
-  const int v = (e && *e) ? atoi(e) : 0;
-  return (v >= 4 && v <= 16) ? v : kma::kRegionBits;
-}
-
-// Which protein path a device call takes: 1 = partitioned (kma_internal.h), 0 = direct.
-// KMA_PATH=direct|partitioned forces it (read per call, so that tests run both in one
-// process); automatic: partitioned when the batch has >= 4 windows per table bucket (each
-// bucket line is then reused from L2 several times) and the table cuts into kMinRegions ..
-// kMaxRegions regions.
-int protein_path(const kma_table* t, const kma_workspace* ws, uint32_t n_seq, uint64_t n_res,
-                 int rb) {
-  const uint64_t regions = (t->n_buckets + (1ull << rb) - 1) >> rb;
-  const bool fits = regions <= (uint64_t)kma::kMaxRegions && n_seq <= ws->seq_cap &&
-                    kma::chunk_bound(n_res, n_seq) <= ws->chunk_cap && ws->d_pres != nullptr &&
-                    t->k <= 8;
-  const char* e = getenv("KMA_PATH");
-  if (e && !strcmp(e, "direct")) return 0;
-  if (e && !strcmp(e, "partitioned")) return fits ? 1 : 0;
-  (void)regions;
-  return 0;  // automatic: direct (measured faster at c4 and c5)
 }
 
 // The protein path on one replica (device buffers, asynchronous on s).
@@ -906,68 +888,18 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.block_proteins = block_proteins();
   a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
   a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
-  const int rb = region_bits();
-  if (!protein_path(t, ws, n_seq, n_residues, rb)) {
-    PhaseClock clk(ws, s, kDirectPhases, 1);
-    KMA_HIP(clk.mark());
-    KMA_HIP(kma::launch_annotate(a, s));
-    KMA_HIP(clk.mark());
-    return KMA_OK;
-  }
-  kma::PartArgs p{};
-  p.slots = r.d_slots;
-  p.n_buckets = (uint32_t)t->n_buckets;
-  p.lut = r.d_lut;
-  p.residues = d_residues;
-  p.offsets = d_offsets;
-  p.n_seq = n_seq;
-  p.k = t->k;
-  p.mlen = t->mlen;
-  p.region_bits = rb;
-  p.n_regions = (uint32_t)((t->n_buckets + (1ull << rb) - 1) >> rb);
-  p.min_hits = min_hits;
-  p.flags = flags;
-  p.chunk_flags = ws->d_pflags;
-  p.chunk_excl = ws->d_pexcl;
-  p.chunk_first = ws->d_cfirst;
-  p.chunk_end = ws->d_cend;
-  p.chunk_fb = ws->d_cfb;
-  p.counts = ws->d_pcounts;
-  p.list = ws->d_plist;
-  p.run_off = ws->d_runoff;
-  p.rec = reinterpret_cast<uint64_t*>(ws->d_gset);
-  p.res = ws->d_pres;
-  p.out_fid = d_fid;
-  p.out_count = d_count;
-  p.out_status = d_status;
-  p.tally = d_tally;
-  p.n_fid = d_tally ? n_fid : 0;
-  const int cu = ws->n_cu;
-  // P2: whole XCD groups, enough blocks that one holds <= kMaxRunsPerBlock chunks.
-  const uint64_t nb_min = (kma::chunk_bound(n_residues, n_seq) + kma::kMaxRunsPerBlock - 1) /
-                          kma::kMaxRunsPerBlock;
-  const uint64_t nb = std::max<uint64_t>(
-      nb_min, (uint64_t)std::max(1, cu / 8) * kma::partition_occupancy(t->k, t->mlen, 1));
-  PhaseClock clk(ws, s, kPartPhases, 5);
+  PhaseClock clk(ws, s, kDirectPhases, 1);
   KMA_HIP(clk.mark());
-  size_t tb = ws->ptemp_bytes;
-  KMA_HIP(kma::launch_chunking(p, ws->d_ptemp, &tb, s));
-  KMA_HIP(clk.mark());
-  KMA_HIP(kma::launch_partition(p, (unsigned)(cu * kma::partition_occupancy(t->k, t->mlen, 0)), s));
-  KMA_HIP(clk.mark());
-  KMA_HIP(kma::launch_probe_regions(p, (unsigned)(8 * nb), s));
-  KMA_HIP(clk.mark());
-  KMA_HIP(kma::launch_vote_chunks(p, (unsigned)(cu * kma::partition_occupancy(t->k, t->mlen, 2)), s));
-  KMA_HIP(clk.mark());
-  a.list = ws->d_plist;
-  a.list_n = ws->d_pcounts + 1;
-  KMA_HIP(kma::launch_annotate_list(a, (unsigned)(2 * cu), s));
+  KMA_HIP(kma::launch_annotate(a, s));
   KMA_HIP(clk.mark());
   return KMA_OK;
 }
 
 int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
   if (!t) return fail(KMA_E_INVALID, "null table");
+  if (kma::wide_k(t->k))
+    return fail(KMA_E_INVALID, "the protein path takes tables of K <= 8 (this table: K = %d)",
+                t->k);
   if (min_hits < 1) return fail(KMA_E_INVALID, "Min-hits must be positive.");
   if (flags & ~(KMA_F_END_EXCLUSIVE | KMA_F_MULTISET)) return fail(KMA_E_INVALID, "bad flags");
   return KMA_OK;
@@ -1141,33 +1073,12 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
     return fail(KMA_E_INVALID, "%llu residues in one call (limit 2^32 - 128)",
                 (unsigned long long)n_residues);
   if (n_seq >= (1ull << 31)) return fail(KMA_E_INVALID, "more than 2^31 proteins in one call");
-  if (ws->d_gset && n_residues <= ws->res_cap && n_seq <= ws->seq_cap) return KMA_OK;
+  if (ws->d_gset && n_residues <= ws->res_cap) return KMA_OK;
   DeviceScope ds(ws->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
-  n_residues = std::max<uint64_t>(n_residues, ws->res_cap);
-  n_seq = std::max<uint64_t>(n_seq, ws->seq_cap);
   free_protein_scratch(ws);
-  const uint64_t chunks = kma::chunk_bound(n_residues, n_seq);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
-  KMA_HIP(hipMalloc(&ws->d_pres, (n_residues + kResPad) * 4));
-  KMA_HIP(hipMalloc(&ws->d_pflags, (n_seq + 1) * 8));
-  KMA_HIP(hipMalloc(&ws->d_pexcl, (n_seq + 1) * 8));
-  KMA_HIP(hipMalloc(&ws->d_plist, (n_seq + 1) * 4));
-  KMA_HIP(hipMalloc(&ws->d_cfirst, chunks * 4));
-  KMA_HIP(hipMalloc(&ws->d_cend, chunks * 4));
-  KMA_HIP(hipMalloc(&ws->d_cfb, chunks));
-  KMA_HIP(hipMalloc(&ws->d_pcounts, 16));
-  KMA_HIP(hipMalloc(&ws->d_runoff, chunks * (kma::kMaxRegions + 1) * 2));
-
-  kma::PartArgs q{};
-  q.n_seq = (uint32_t)std::max<uint64_t>(n_seq, 1);
-  size_t tb = 0;
-  KMA_HIP(kma::launch_chunking(q, nullptr, &tb, nullptr));
-  KMA_HIP(hipMalloc(&ws->d_ptemp, tb ? tb : 1));
-  ws->ptemp_bytes = tb;
   ws->res_cap = n_residues;
-  ws->seq_cap = n_seq;
-  ws->chunk_cap = chunks;
   return KMA_OK;
 }
 
@@ -1250,9 +1161,10 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
                                  void* stream) {
   if (int rc = check_protein_call(t, min_hits, flags)) return rc;
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
-  const Replica* r = replica_on(t, ws->device);
-  if (!r) return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d",
-                      ws->device);
+  Replica rep;
+  if (!replica_on(t, ws->device, &rep))
+    return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d", ws->device);
+  const Replica* r = &rep;
   if (n_seq == 0) return KMA_OK;
   if (!d_residues || !d_offsets || !d_fid || !d_count || !d_status)
     return fail(KMA_E_INVALID, "null device buffer");
@@ -1279,11 +1191,12 @@ int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const ui
   for (uint32_t s = 0; s < n_seq; ++s)
     if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
   const bool tally = out_tally && n_fid;
-  const int nr = (int)std::min<uint64_t>(t->reps.size(), n_seq);
+  const std::vector<Replica> reps = replicas(t);
+  const int nr = (int)std::min<uint64_t>(reps.size(), n_seq);
   const std::vector<uint32_t> b = shard_bounds(offsets, n_seq, nr);
   std::vector<std::vector<uint32_t>> part(tally ? nr : 0, std::vector<uint32_t>(n_fid));
   const int rc = fan_out(nr, [&](int i) {
-    return protein_shard(t, t->reps[i], residues, offsets, b[i], b[i + 1], min_hits, flags,
+    return protein_shard(t, reps[i], residues, offsets, b[i], b[i + 1], min_hits, flags,
                          out_fid, out_count, out_status, tally ? part[i].data() : nullptr,
                          n_fid);
   });
@@ -1309,9 +1222,10 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
                                 uint64_t* d_n_hits, uint32_t* d_tally, uint32_t n_fid,
                                 void* stream) {
   if (!t || !ws) return fail(KMA_E_INVALID, "null table or workspace");
-  const Replica* r = replica_on(t, ws->device);
-  if (!r) return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d",
-                      ws->device);
+  Replica rep;
+  if (!replica_on(t, ws->device, &rep))
+    return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d", ws->device);
+  const Replica* r = &rep;
   const char* code = ncbi_code(genetic_code);
   if (!code) return fail(KMA_E_INVALID, "unsupported genetic code %d", genetic_code);
   if (!d_n_hits) return fail(KMA_E_INVALID, "null n_hits");
@@ -1389,7 +1303,7 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
       contig_args(t, r, c->ws, c->d_in.p, c->d_off.p, n, total, code, d_tally, n_fid);
   const uint64_t nb = contig_blocks(total);
   if (strict) {
-    const uint64_t n_slots = t->n_buckets * kma::kSlotsPerBucket;
+    const uint64_t n_slots = t->n_buckets * kma::slots_for_k(t->k);
     KMA_HIP(c->d_aux.reserve(n_slots));
     KMA_HIP(hipMemsetAsync(c->d_aux.p, 0, n_slots * 4, s));
     a.slot_count = c->d_aux.p;
@@ -1442,7 +1356,8 @@ int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offs
   if (offsets[n_contig] - offsets[0] >= (1ull << 39))
     return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
   const bool tally = out_tally && n_fid;
-  const int nr = strict ? 1 : (int)std::min<uint64_t>(t->reps.size(), n_contig);
+  const std::vector<Replica> reps = replicas(t);
+  const int nr = strict ? 1 : (int)std::min<uint64_t>(reps.size(), n_contig);
   const std::vector<uint32_t> b = shard_bounds(offsets, n_contig, nr);
   // Pass 1 counts (and tallies into copies: nothing is written on KMA_E_CAPACITY); pass 2
   // emits. A shard's hits are produced only if the whole call fits in cap.
@@ -1451,7 +1366,7 @@ int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offs
   for (int i = 0; i < (tally ? nr : 0); ++i)
     tal[i].assign(out_tally + (uint64_t)b[i] * n_fid, out_tally + (uint64_t)b[i + 1] * n_fid);
   int rc = fan_out(nr, [&](int i) {
-    return contig_shard(t, t->reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
+    return contig_shard(t, reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
                         nullptr, &nh[i], tally ? tal[i].data() : nullptr, n_fid);
   });
   if (rc != KMA_OK) return rc;
@@ -1467,7 +1382,7 @@ int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offs
   std::vector<std::vector<kma_hit>> hv(nr);
   rc = fan_out(nr, [&](int i) {
     if (nh[i] == 0) return KMA_OK;
-    return contig_shard(t, t->reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
+    return contig_shard(t, reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
                         &hv[i], &nh[i], nullptr, 0);
   });
   if (rc != KMA_OK) return rc;
@@ -1582,6 +1497,7 @@ int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const
   }
   const uint64_t base = offsets[0], total = offsets[n_seq] - base;
   if (total == 0) return KMA_OK;
+  if (total >= (1ull << 31)) return fail(KMA_E_INVALID, "more than 2^31 residues in one call");
   uint8_t lut[256];
   standard_lut(lut);
   std::vector<uint64_t> rel(offsets, offsets + n_seq + 1);
@@ -1591,15 +1507,19 @@ int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const
                                         hipGetErrorString(ds.err));
   DevBufs b;
   uint8_t *d_res, *d_lut, *d_flags;
-  uint64_t *d_off, *d_a, *d_b, *d_n;
+  uint64_t *d_off, *d_ka, *d_kb, *d_n;
   int32_t* d_roles;
-  uint32_t* d_alpha;
+  uint32_t *d_alpha, *d_ta, *d_tb, *d_head, *d_run;
   KMA_HIP(b.alloc(&d_res, total + 64));
   KMA_HIP(b.alloc(&d_off, (n_seq + 1) * 8ull));
   KMA_HIP(b.alloc(&d_roles, n_seq * 4ull));
   KMA_HIP(b.alloc(&d_lut, 256));
-  KMA_HIP(b.alloc(&d_a, total * 8));
-  KMA_HIP(b.alloc(&d_b, total * 8));
+  KMA_HIP(b.alloc(&d_ka, total * 8));
+  KMA_HIP(b.alloc(&d_kb, total * 8));
+  KMA_HIP(b.alloc(&d_ta, total * 4));
+  KMA_HIP(b.alloc(&d_tb, total * 4));
+  KMA_HIP(b.alloc(&d_head, total * 4));
+  KMA_HIP(b.alloc(&d_run, total * 4));
   KMA_HIP(b.alloc(&d_flags, total));
   KMA_HIP(b.alloc(&d_n, 16));
   KMA_HIP(b.alloc(&d_alpha, 4));
@@ -1610,46 +1530,39 @@ int kma_build_signatures(const uint8_t* residues, const uint64_t* offsets, const
   KMA_HIP(hipMemcpy(d_lut, lut, 256, hipMemcpyHostToDevice));
   KMA_HIP(hipMemset(d_alpha, 0, 4));
   KMA_HIP(kma::launch_build_windows(d_res, d_off, n_seq, d_roles, k,
-                                    (flags & KMA_F_END_EXCLUSIVE) ? 1 : 0, d_lut, d_a, d_alpha,
-                                    nullptr));
+                                    (flags & KMA_F_END_EXCLUSIVE) ? 1 : 0, d_lut, d_ka, d_ta,
+                                    d_alpha, nullptr));
+  // (key, role) pairs sorted by key; RoleCounter per key run; select the good runs' heads
   size_t t1 = 0, t2 = 0, t3 = 0;
-  const int bits = 24 + 5 * k;
-  KMA_HIP(kma::launch_sort_keys(nullptr, &t1, d_a, d_b, total, bits, nullptr));
-  KMA_HIP(kma::launch_unique(nullptr, &t2, d_b, d_a, d_n, total, nullptr));
-  KMA_HIP(kma::launch_select_flagged_keys(nullptr, &t3, d_a, d_flags, d_b, d_n + 1, total,
-                                          nullptr));
-  size_t tb = std::max(t1, std::max(t2, t3));
+  KMA_HIP(kma::launch_sort_pairs(nullptr, &t1, d_ka, d_kb, d_ta, d_tb, total, 5 * k, nullptr));
+  KMA_HIP(kma::launch_signature_flags(d_kb, d_tb, total, d_flags, d_head, d_run, nullptr, &t2,
+                                      nullptr));
+  KMA_HIP(kma::launch_select_flagged(nullptr, &t3, d_kb, d_tb, d_flags, d_ka, d_ta, d_n, total,
+                                     nullptr));
+  const size_t tb = std::max(t1, std::max(t2, t3));
   void* d_temp;
-  KMA_HIP(b.alloc(&d_temp, tb));
+  KMA_HIP(b.alloc(&d_temp, tb ? tb : 1));
   size_t t = tb;
-  KMA_HIP(kma::launch_sort_keys(d_temp, &t, d_a, d_b, total, bits, nullptr));  // a -> b
+  KMA_HIP(kma::launch_sort_pairs(d_temp, &t, d_ka, d_kb, d_ta, d_tb, total, 5 * k, nullptr));
   t = tb;
-  KMA_HIP(kma::launch_unique(d_temp, &t, d_b, d_a, d_n, total, nullptr));  // b -> a
-  uint64_t n_u = 0;
+  KMA_HIP(kma::launch_signature_flags(d_kb, d_tb, total, d_flags, d_head, d_run, d_temp, &t,
+                                      nullptr));
+  t = tb;
+  KMA_HIP(kma::launch_select_flagged(d_temp, &t, d_kb, d_tb, d_flags, d_ka, d_ta, d_n, total,
+                                     nullptr));
+  uint64_t n_sel = 0;
   uint32_t alpha = 0;
-  KMA_HIP(hipMemcpy(&n_u, d_n, 8, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(&n_sel, d_n, 8, hipMemcpyDeviceToHost));
   KMA_HIP(hipMemcpy(&alpha, d_alpha, 4, hipMemcpyDeviceToHost));
   if (alpha)
     return fail(KMA_E_ALPHABET, "a protein window holds a byte outside A-Z and '*'");
-  uint64_t n_sel = 0;
-  if (n_u) {
-    KMA_HIP(kma::launch_signature_flags(d_a, d_n, n_u, d_flags, nullptr));
-    t = tb;
-    KMA_HIP(kma::launch_select_flagged_keys(d_temp, &t, d_a, d_flags, d_b, d_n + 1, n_u,
-                                            nullptr));  // a -> b
-    KMA_HIP(hipMemcpy(&n_sel, d_n + 1, 8, hipMemcpyDeviceToHost));
-  }
   *n_out = n_sel;
   if (n_sel > cap || (n_sel && (!out_keys || !out_roles)))
     return fail(KMA_E_CAPACITY, "%llu signature kmers, capacity %llu",
                 (unsigned long long)n_sel, (unsigned long long)cap);
   if (n_sel == 0) return KMA_OK;
-  std::vector<uint64_t> rows(n_sel);
-  KMA_HIP(hipMemcpy(rows.data(), d_b, n_sel * 8, hipMemcpyDeviceToHost));
-  for (uint64_t i = 0; i < n_sel; ++i) {
-    out_keys[i] = rows[i] >> 24;
-    out_roles[i] = (uint32_t)(rows[i] & kma::kBuildNeg);
-  }
+  KMA_HIP(hipMemcpy(out_keys, d_ka, n_sel * 8, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(out_roles, d_ta, n_sel * 4, hipMemcpyDeviceToHost));
   return KMA_OK;
 }
 
@@ -1994,42 +1907,82 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
   }
   const uint64_t n_cand = last_off + last_cnt;
   KMA_HIP(b.alloc(&a.out_count, n_pt * 4ull));
+  uint64_t* best_bits;
+  uint32_t* best_proto;
+  KMA_HIP(b.alloc(&best_bits, n_gp * 8ull));
+  KMA_HIP(b.alloc(&best_proto, n_gp * 4ull));
   KMA_HIP(b.alloc(&a.best_bits, n_gp * 8ull));
   KMA_HIP(b.alloc(&a.best_proto, n_gp * 4ull));
   KMA_HIP(hipMemset(a.out_count, 0, n_pt * 4ull));
-  KMA_HIP(hipMemset(a.best_bits, 0, n_gp * 8ull));
-  KMA_HIP(hipMemset(a.best_proto, 0xFF, n_gp * 4ull));
+  for (uint64_t* q : {best_bits, a.best_bits}) KMA_HIP(hipMemset(q, 0, n_gp * 8ull));
+  for (uint32_t* q : {best_proto, a.best_proto}) KMA_HIP(hipMemset(q, 0xFF, n_gp * 4ull));
+  // Candidates are scored in slices of whole prototypes (file order) whose sort and run-length
+  // encoding stay below 2^31 elements (hipcub's int counts); a slice's best per protein
+  // replaces the running best only when strictly higher, so earlier prototypes keep ties.
+  // KMA_HASH_SLICE (tests) lowers the slice size.
+  uint64_t slice_cap = (1ull << 31) - 1;
+  if (const char* e = getenv("KMA_HASH_SLICE"))
+    slice_cap = std::max<uint64_t>(1, std::min<uint64_t>(slice_cap, strtoull(e, nullptr, 10)));
+  std::vector<uint64_t> cum(n_pt + 1, 0);
   if (n_cand) {
+    uint64_t* d_cum;
+    KMA_HIP(b.alloc(&d_cum, (n_pt + 1) * 8ull));
+    KMA_HIP(kma::launch_proto_cum(coff, a.ccount, p.off, n_pt, p.total, d_cum, nullptr));
+    KMA_HIP(hipMemcpy(cum.data(), d_cum, (n_pt + 1) * 8ull, hipMemcpyDeviceToHost));
+  }
+  std::vector<uint32_t> cut{0};  // slice boundaries in prototypes
+  for (uint32_t q = 0; q < n_pt; ++q) {
+    if (cum[q + 1] - cum[q] > (1ull << 31) - 1)
+      return fail(KMA_E_CAPACITY, "prototype %u has %llu candidates (limit 2^31 - 1)", q,
+                  (unsigned long long)(cum[q + 1] - cum[q]));
+    if (q > cut.back() && cum[q + 1] - cum[cut.back()] > slice_cap) cut.push_back(q);
+  }
+  cut.push_back(n_pt);
+  uint64_t max_slice = 0;
+  for (size_t i = 0; i + 1 < cut.size(); ++i)
+    max_slice = std::max(max_slice, cum[cut[i + 1]] - cum[cut[i]]);
+  if (max_slice) {
     uint64_t *cand, *csorted, *runs;
     uint32_t* run_len;
-    KMA_HIP(b.alloc(&cand, n_cand * 8));
-    KMA_HIP(b.alloc(&csorted, n_cand * 8));
-    KMA_HIP(b.alloc(&runs, n_cand * 8));
-    KMA_HIP(b.alloc(&run_len, n_cand * 4));
-    a.cand = cand;
-    KMA_HIP(kma::launch_cand_emit(a, nullptr));
+    KMA_HIP(b.alloc(&cand, max_slice * 8));
+    KMA_HIP(b.alloc(&csorted, max_slice * 8));
+    KMA_HIP(b.alloc(&runs, max_slice * 8));
+    KMA_HIP(b.alloc(&run_len, max_slice * 4));
     int pbits = 1;
     while (pbits < 32 && (1ull << pbits) < n_pt) ++pbits;
     size_t t2 = 0, t3 = 0;
-    KMA_HIP(kma::cub_sort_keys_u64(nullptr, &t2, cand, csorted, n_cand, 32 + pbits, nullptr));
-    KMA_HIP(kma::cub_rle_u64(nullptr, &t3, csorted, runs, run_len, d_n + 2, n_cand, nullptr));
+    KMA_HIP(kma::cub_sort_keys_u64(nullptr, &t2, cand, csorted, max_slice, 32 + pbits, nullptr));
+    KMA_HIP(kma::cub_rle_u64(nullptr, &t3, csorted, runs, run_len, d_n + 2, max_slice, nullptr));
     void* temp2;
     const size_t t23 = std::max(t2, t3);
     KMA_HIP(b.alloc(&temp2, t23 ? t23 : 1));
-    t2 = t23;
-    KMA_HIP(kma::cub_sort_keys_u64(temp2, &t2, cand, csorted, n_cand, 32 + pbits, nullptr));
-    t3 = t23;
-    KMA_HIP(kma::cub_rle_u64(temp2, &t3, csorted, runs, run_len, d_n + 2, n_cand, nullptr));
+    std::vector<uint64_t> hoff(n_pt + 1);
+    KMA_HIP(hipMemcpy(hoff.data(), p.off, (n_pt + 1) * 8ull, hipMemcpyDeviceToHost));
+    a.cand = cand;
     a.runs = runs;
     a.run_len = run_len;
     a.n_runs = d_n + 2;
-    KMA_HIP(kma::launch_score(a, n_cand, nullptr));
-    KMA_HIP(kma::launch_choose(a, n_cand, nullptr));
+    for (size_t i = 0; i + 1 < cut.size(); ++i) {
+      const uint64_t nc = cum[cut[i + 1]] - cum[cut[i]];
+      if (!nc) continue;
+      a.pos_lo = hoff[cut[i]] - hoff[0];
+      a.pos_hi = hoff[cut[i + 1]] - hoff[0];
+      a.cand_base = cum[cut[i]];
+      KMA_HIP(kma::launch_cand_emit(a, nullptr));
+      t2 = t23;
+      KMA_HIP(kma::cub_sort_keys_u64(temp2, &t2, cand, csorted, nc, 32 + pbits, nullptr));
+      t3 = t23;
+      KMA_HIP(kma::cub_rle_u64(temp2, &t3, csorted, runs, run_len, d_n + 2, nc, nullptr));
+      KMA_HIP(kma::launch_score(a, nc, nullptr));
+      KMA_HIP(kma::launch_choose(a, nc, nullptr));
+      KMA_HIP(kma::launch_merge_best(best_bits, best_proto, a.best_bits, a.best_proto, n_gp,
+                                     nullptr));
+    }
   }
   std::vector<uint64_t> bits(n_gp);
   std::vector<uint32_t> proto(n_gp);
-  KMA_HIP(hipMemcpy(bits.data(), a.best_bits, n_gp * 8ull, hipMemcpyDeviceToHost));
-  KMA_HIP(hipMemcpy(proto.data(), a.best_proto, n_gp * 4ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(bits.data(), best_bits, n_gp * 8ull, hipMemcpyDeviceToHost));
+  KMA_HIP(hipMemcpy(proto.data(), best_proto, n_gp * 4ull, hipMemcpyDeviceToHost));
   KMA_HIP(hipMemcpy(out_count, a.out_count, n_pt * 4ull, hipMemcpyDeviceToHost));
   for (uint32_t i = 0; i < n_gp; ++i) {
     if (proto[i] == 0xFFFFFFFFu) continue;

@@ -1,5 +1,4 @@
-// kma_device.h — device helpers shared by the protein-path kernels (kma_kernels.hip,
-// kma_partition.hip): wave reductions, window packing, bucket scans and the quad-cooperative
+// kma_device.h — device helpers shared by the probe kernels (kma_kernels.hip): wave reductions, window packing, bucket scans and the quad-cooperative
 // bucket match. Internal; not part of the ABI.
 #pragma once
 
@@ -188,6 +187,43 @@ __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], 
   return quad_or(w);
 }
 
+// Wide tables (K > 8, kma_internal.h): lane `part` of the quad holds slot `part` of the bucket
+// in v; same verdict word as match_part (fid + 1, slot from bit 24, bit 31 = overflow bit).
+__device__ __forceinline__ uint32_t match_wide(const uint4& v, uint32_t kl, uint32_t kh,
+                                               uint32_t part) {
+  const uint32_t m = (uint32_t)(v.x == kl) & (uint32_t)(v.y == kh);
+  uint32_t w = m * ((v.z & kFidMask) + 1u) | m * (part << kSlotShift);
+  w |= (uint32_t)(ovf_index_wide(kl) == part) & (v.z >> 23) & 1u ? 0x80000000u : 0u;
+  return quad_or(w);
+}
+
+// walk_chain for wide tables: whole 64-byte buckets of four 16-byte slots, one at a time.
+__device__ __forceinline__ bool walk_chain_wide(const uint64_t* __restrict__ slots,
+                                                uint32_t n_buckets, uint32_t b, uint64_t key,
+                                                uint32_t& fid, uint32_t& sid) {
+  const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+  const uint32_t home = b;
+  for (uint32_t steps = 1; steps < n_buckets; ++steps) {  // bounded
+    b = chain_bucket(home, steps, n_buckets);
+    const uint4* bp = reinterpret_cast<const uint4*>(slots) + (uint64_t)b * kWideSlots;
+    uint4 q[kWideSlots];
+#pragma unroll
+    for (int i = 0; i < kWideSlots; ++i) q[i] = bp[i];
+    bool empty = false;
+#pragma unroll
+    for (int i = 0; i < kWideSlots; ++i) {
+      if (q[i].x == klo && q[i].y == khi) {
+        fid = q[i].z & kFidMask;
+        sid = b * kWideSlots + i;
+        return true;
+      }
+      empty = empty || q[i].x == 0u;
+    }
+    if (empty) return false;
+  }
+  return false;
+}
+
 // kNone: a window that does not probe. The protein kernel packs the block's protein index
 // above the bucket index (buckets < 2^28).
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -202,7 +238,8 @@ __device__ __forceinline__ uint32_t set_slot(uint32_t key, uint32_t cap) {
 }  // namespace
 
 // Kernels are instantiated per (K, layout): the minimizer length is a template parameter so
-// that the m-mer loop unrolls; layouts are m = min(K, 6), min(K, 7) and 0 (flat).
+// that the m-mer loop unrolls; layouts are m = min(K, 6), min(K, 7) and 0 (flat). K = 9..12
+// are wide tables (16-byte slots); kernels that take only narrow tables reject them.
 template <int K, template <int, int> class Launch, typename... Args>
 inline hipError_t dispatch_m(int m, Args&&... args) {
   constexpr int M6 = K < 6 ? K : 6;
@@ -223,6 +260,10 @@ inline hipError_t dispatch_km(int k, int m, Args&&... args) {
     case 6: return dispatch_m<6, Launch>(m, args...);
     case 7: return dispatch_m<7, Launch>(m, args...);
     case 8: return dispatch_m<8, Launch>(m, args...);
+    case 9: return dispatch_m<9, Launch>(m, args...);  // wide tables (kma_internal.h)
+    case 10: return dispatch_m<10, Launch>(m, args...);
+    case 11: return dispatch_m<11, Launch>(m, args...);
+    case 12: return dispatch_m<12, Launch>(m, args...);
     default: return hipErrorInvalidValue;
   }
 }

@@ -24,15 +24,17 @@ struct HashArgs {
   uint32_t* ccount;
   uint32_t* cu;
   const uint64_t* coff;
-  uint64_t* cand;             // prototype << 32 | protein
+  uint64_t* cand;             // prototype << 32 | protein (the slice's, from cand_base)
+  uint64_t pos_lo, pos_hi;    // the slice: prototype positions [pos_lo, pos_hi)
+  uint64_t cand_base;         // coff[pos_lo]
   const uint64_t* runs;       // run-length encoded candidates
   const uint32_t* run_len;
   const uint64_t* n_runs;     // device
   // scoring
   double min_sim;
   uint32_t* out_count;        // per prototype: proteins with sim >= min_sim
-  uint64_t* best_bits;        // per protein: best similarity (double bits), 0 = none
-  uint32_t* best_proto;       // per protein: smallest prototype at the best similarity
+  uint64_t* best_bits;        // per protein: best similarity of the slice (double bits), 0 = none
+  uint32_t* best_proto;       // per protein: smallest prototype of the slice at that similarity
 };
 
 hipError_t launch_owner_first(const uint64_t* sorted, const uint64_t* off, uint32_t n,
@@ -43,6 +45,13 @@ hipError_t launch_set_end(uint32_t* ustart, const uint64_t* n_u, uint64_t n_pair
 hipError_t launch_cand_count(const HashArgs& a, hipStream_t s);
 hipError_t launch_cand_emit(const HashArgs& a, hipStream_t s);
 hipError_t launch_score(const HashArgs& a, uint64_t n_max, hipStream_t s);
+// cum[p] = candidates of prototypes before p (p <= n_proto; off: prototype position offsets).
+hipError_t launch_proto_cum(const uint64_t* coff, const uint32_t* ccount, const uint64_t* off,
+                            uint32_t n_proto, uint64_t n_pos, uint64_t* cum, hipStream_t s);
+// Slices of prototypes in file order: a slice's best replaces the running one only when strictly
+// higher (earlier prototypes win ties); the slice buffers are reset for the next slice.
+hipError_t launch_merge_best(uint64_t* best_bits, uint32_t* best_proto, uint64_t* slice_bits,
+                             uint32_t* slice_proto, uint32_t n, hipStream_t s);
 hipError_t launch_choose(const HashArgs& a, uint64_t n_max, hipStream_t s);
 hipError_t cub_select_flagged_u64(void* temp, size_t* tb, const uint64_t* in, const uint8_t* f,
                                   uint64_t* out, uint64_t* n_out, uint64_t n, hipStream_t s);

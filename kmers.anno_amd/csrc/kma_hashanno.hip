@@ -97,11 +97,13 @@ __global__ __launch_bounds__(256) void cand_count_kernel(HashArgs a) {
   }
 }
 
+// The slice's candidates: positions [pos_lo, pos_hi), written from cand_base.
 __global__ __launch_bounds__(256) void cand_emit_kernel(HashArgs a) {
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n_ppos; i += gridDim.x * 256ull) {
+  for (uint64_t i = a.pos_lo + blockIdx.x * 256ull + threadIdx.x; i < a.pos_hi;
+       i += gridDim.x * 256ull) {
     const uint32_t c = a.ccount[i];
     if (!c) continue;
-    const uint64_t o = a.coff[i], proto = a.powner[i];
+    const uint64_t o = a.coff[i] - a.cand_base, proto = a.powner[i];
     const uint32_t s = a.ustart[a.cu[i]];
     for (uint32_t j = 0; j < c; ++j) a.cand[o + j] = proto << 32 | a.gprot[s + j];
   }
@@ -138,7 +140,49 @@ __global__ __launch_bounds__(256) void choose_kernel(HashArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void proto_cum_kernel(const uint64_t* __restrict__ coff,
+                                                        const uint32_t* __restrict__ ccount,
+                                                        const uint64_t* __restrict__ off,
+                                                        uint32_t n_proto, uint64_t n_pos,
+                                                        uint64_t* __restrict__ cum) {
+  const uint64_t total = n_pos ? coff[n_pos - 1] + ccount[n_pos - 1] : 0;
+  const uint64_t o0 = off[0];
+  for (uint64_t p = blockIdx.x * 256ull + threadIdx.x; p <= n_proto; p += gridDim.x * 256ull) {
+    const uint64_t pos = off[p] - o0;
+    cum[p] = pos < n_pos ? coff[pos] : total;
+  }
+}
+
+__global__ __launch_bounds__(256) void merge_best_kernel(uint64_t* __restrict__ best_bits,
+                                                         uint32_t* __restrict__ best_proto,
+                                                         uint64_t* __restrict__ slice_bits,
+                                                         uint32_t* __restrict__ slice_proto,
+                                                         uint32_t n) {
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < n; g += gridDim.x * 256ull) {
+    const uint32_t sp = slice_proto[g];
+    if (sp != 0xFFFFFFFFu && (best_proto[g] == 0xFFFFFFFFu || slice_bits[g] > best_bits[g])) {
+      best_bits[g] = slice_bits[g];
+      best_proto[g] = sp;
+    }
+    slice_bits[g] = 0;
+    slice_proto[g] = 0xFFFFFFFFu;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_proto_cum(const uint64_t* coff, const uint32_t* ccount, const uint64_t* off,
+                            uint32_t n_proto, uint64_t n_pos, uint64_t* cum, hipStream_t s) {
+  hipLaunchKernelGGL(proto_cum_kernel, dim3(grid1((uint64_t)n_proto + 1)), dim3(256), 0, s, coff,
+                     ccount, off, n_proto, n_pos, cum);
+  return hipGetLastError();
+}
+hipError_t launch_merge_best(uint64_t* best_bits, uint32_t* best_proto, uint64_t* slice_bits,
+                             uint32_t* slice_proto, uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(merge_best_kernel, dim3(grid1(n)), dim3(256), 0, s, best_bits, best_proto,
+                     slice_bits, slice_proto, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_owner_first(const uint64_t* sorted, const uint64_t* off, uint32_t n,
                               uint32_t* owner, uint8_t* first, hipStream_t s) {
@@ -160,7 +204,7 @@ hipError_t launch_cand_count(const HashArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_cand_emit(const HashArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(cand_emit_kernel, dim3(grid1(a.n_ppos)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(cand_emit_kernel, dim3(grid1(a.pos_hi - a.pos_lo)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_score(const HashArgs& a, uint64_t n_max, hipStream_t s) {

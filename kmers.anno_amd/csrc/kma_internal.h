@@ -55,6 +55,23 @@ __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
   return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
 }
 
+// ---- wide tables (K = 9..12: 5K-bit keys up to 60 bits) ------------------------------------------
+// The projector's -K (KmerProcessor.java:86-88, KmerReference.setKmerSize) reaches 12; a 60-bit
+// key does not fit the 8-byte slot. Wide tables use 16-byte slots, four per 64-byte bucket, so a
+// probe is still one 64-byte line and each lane of a quad loads exactly one slot (one dwordx4):
+//   .x = key bits 0..31 (never 0: the last six residues' codes), .y = key bits 32..63,
+//   .z = overflow bit << 23 | fid (23 bits), .w = 0.
+// The overflow filter has one bit per slot (4 per bucket); chains, layouts and the stop rule are
+// those of the narrow table. Wide buckets are 64 bytes in every build.
+constexpr int kWideSlots = 4;
+constexpr int kWideSlotBits = 2;
+constexpr int kMaxNarrowK = 8;
+__host__ __device__ constexpr bool wide_k(int k) { return k > kMaxNarrowK; }
+__host__ __device__ constexpr int slots_for_k(int k) { return wide_k(k) ? kWideSlots : kSlotsPerBucket; }
+__host__ __device__ inline uint32_t ovf_index_wide(uint32_t klo) {
+  return (klo * 0x9E3779B1u) >> (32 - kWideSlotBits);
+}
+
 __host__ __device__ inline uint32_t mix32(uint32_t h) {  // murmur3 fmix32
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -164,6 +181,8 @@ __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32
 // KMA_MINIMIZER=0|6|7 in the environment forces a layout (read per call: tests run every layout
 // in one process). Defined in kma_abi.cpp.
 constexpr uint64_t kMinimizer6Buckets = kSlotsPerBucket == 16 ? (1ull << 24) : (1ull << 25);
+// Wide tables (4 slots per bucket): the same key count, i.e. twice the buckets.
+constexpr uint64_t kMinimizer6BucketsWide = 1ull << 26;
 int minimizer_len(int k, uint64_t n_buckets);
 // The table creators also build a minimizer-layout table flat when more than this fraction of
 // its keys were displaced past their home bucket, or a chain is longer than kMaxChain buckets,
@@ -226,75 +245,7 @@ struct ProteinArgs {
   // has fewer, so that short groups start after every long one.
   uint32_t defer_below;
   uint32_t n_groups;
-  // List form (annotate_list_kernel): the proteins list[0 .. *list_n), one per block step.
-  const uint32_t* list;
-  const uint32_t* list_n;
 };
-
-// ---- region-partitioned protein path (kma_partition.hip) ----------------------------------------
-// For batches with many windows per table bucket (c4, c5: 12-120), probing each window where it
-// stands requests one random 64-byte line per distinct minimizer and is capped by the chip's
-// random-request rate. The partitioned path instead moves the windows to the table:
-//   P1 partition_kernel   cuts the batch into chunks (whole proteins starting in one 32 Ki-residue
-//                         interval, <= 256 of them), computes every window's home bucket with
-//                         rolling 5-bit keys and minimizers, and writes one 8-byte record per
-//                         window (key | protein-in-chunk << 40 | bucket-in-region << 48), sorted
-//                         by table REGION (2^region_bits buckets) within the chunk;
-//   P2 probe_regions_kernel  XCD-aware: the blocks sharing an XCD (blockIdx % 8) sweep the
-//                         regions r = g, g + 8, ... together, each taking a fixed range of chunks,
-//                         so a region's lines are fetched into that XCD's L2 once and then served
-//                         from it; per record: one L2 bucket probe, per-protein dedupe of hits
-//                         (LDS set), a u32 result (protein-in-chunk << 24 | fid + 1, 0 = none);
-//   P3 vote_chunks_kernel per chunk: the results are contiguous; per-protein min / max fid and
-//                         distinct count in LDS, then the vote of annotate_kernel.
-// Proteins with more than kGiantWindows windows, and the proteins of a chunk with more than
-// kRunCap windows in one region, take annotate_list_kernel (the direct path) instead.
-constexpr int kChunkSpanBits = 15;
-constexpr int kChunkProteins = 256;          // protein-in-chunk: 8 bits of a result
-constexpr uint32_t kGiantWindows = 16384;
-constexpr int kChunkMaxSpan = (1 << kChunkSpanBits) + (int)kGiantWindows + 64;
-constexpr int kMaxRegions = 2048;
-constexpr int kMinRegions = 64;
-constexpr int kRegionBits = 15;              // 2 MiB of 64-byte buckets per region (default)
-constexpr int kRunCap = 1024;                // records of one chunk in one region
-constexpr int kProbeBatch = 1024;            // records per P2 step (4 per lane)
-constexpr int kPartSet = 2048;               // P2 dedupe set (u64 entries, hits of one step)
-constexpr int kMaxRunsPerBlock = 512;        // chunks per P2 block
-
-struct PartArgs {
-  const uint64_t* slots;
-  uint32_t n_buckets;
-  const uint8_t* lut;
-  const uint8_t* residues;
-  const uint64_t* offsets;
-  uint32_t n_seq;
-  int32_t k;
-  int32_t mlen;
-  int32_t region_bits;
-  uint32_t n_regions;
-  int32_t min_hits;
-  uint32_t flags;
-  uint64_t* chunk_flags;   // n_seq: giant << 32 | starts a chunk
-  uint64_t* chunk_excl;    // n_seq: exclusive scan of chunk_flags
-  uint32_t* chunk_first;   // chunk -> first protein
-  uint32_t* chunk_end;     // chunk -> one past its last protein
-  uint8_t* chunk_fb;       // chunk -> 1 if its proteins take the direct path
-  uint32_t* counts;        // [0] chunks, [1] direct-path proteins
-  uint32_t* list;          // direct-path proteins
-  uint16_t* run_off;       // [chunk][n_regions + 1]: exclusive record offsets by region
-  uint64_t* rec;           // records; chunk c's at its first residue position
-  uint32_t* res;           // results, same index as the records
-  int32_t* out_fid;
-  int32_t* out_count;
-  uint8_t* out_status;
-  uint32_t* tally;
-  uint32_t n_fid;
-};
-// Upper bound on the chunks of a batch (starts at protein multiples of kChunkProteins, after a
-// giant protein, or at a 2^kChunkSpanBits residue boundary).
-inline uint64_t chunk_bound(uint64_t n_residues, uint64_t n_seq) {
-  return (n_residues >> kChunkSpanBits) + n_residues / kGiantWindows + n_seq / kChunkProteins + 3;
-}
 
 struct ContigArgs {
   const uint64_t* slots;
@@ -357,16 +308,6 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
-// The direct path over a device list of proteins (a.list / a.list_n), `blocks` persistent blocks.
-hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream);
-// The partitioned path (kma_partition.hip): chunking (flags, scan, index), P1, P2, P3. temp:
-// the scan's scratch (temp == nullptr: size query into *temp_bytes).
-hipError_t launch_chunking(const PartArgs& a, void* temp, size_t* temp_bytes, hipStream_t stream);
-hipError_t launch_partition(const PartArgs& a, unsigned blocks, hipStream_t stream);
-hipError_t launch_probe_regions(const PartArgs& a, unsigned blocks, hipStream_t stream);
-hipError_t launch_vote_chunks(const PartArgs& a, unsigned blocks, hipStream_t stream);
-// Resident blocks per CU of each partitioned-path kernel (occupancy API; for grid sizing).
-int partition_occupancy(int k, int m, int which);
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
                               void* temp, size_t* temp_bytes, hipStream_t stream);
@@ -382,22 +323,18 @@ hipError_t launch_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* key
                              uint64_t n, int key_bits, hipStream_t stream);
 hipError_t launch_singleton_flags(const uint64_t* sorted_keys, uint64_t n, uint8_t* flags,
                                   hipStream_t stream);
-// Signature build (BuildKmerProcessor): composite = key << 24 | role (0xFFFFFF = buffered
-// protein) per window of ProteinKmers; sort; unique; keep keys with one role and no buffered
-// occurrence.
+// Signature build (BuildKmerProcessor): (key, role or kBuildNeg for a buffered protein) per
+// window of ProteinKmers (key 0: no window); radix sort of the pairs by key; per key run, good
+// iff one role and no buffered occurrence (RoleCounter); select.
 constexpr uint32_t kBuildNeg = 0xFFFFFFu;
 hipError_t launch_build_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq,
                                 const int32_t* roles, int k, int end_exclusive, const uint8_t* lut,
-                                uint64_t* out, uint32_t* alpha_flag, hipStream_t stream);
-hipError_t launch_sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                            uint64_t n, int bits, hipStream_t stream);
-hipError_t launch_unique(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                         uint64_t* n_out, uint64_t n, hipStream_t stream);
-hipError_t launch_signature_flags(const uint64_t* uniq, const uint64_t* n_uniq, uint64_t n_max,
-                                  uint8_t* flags, hipStream_t stream);
-hipError_t launch_select_flagged_keys(void* temp, size_t* temp_bytes, const uint64_t* in,
-                                      const uint8_t* flags, uint64_t* out, uint64_t* n_out,
-                                      uint64_t n, hipStream_t stream);
+                                uint64_t* keys, uint32_t* tags, uint32_t* alpha_flag,
+                                hipStream_t stream);
+// flags[i] = 1 for the first pair of every good key's run (temp == nullptr: size query).
+hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, uint64_t n,
+                                  uint8_t* flags, uint32_t* head_idx, uint32_t* run, void* temp,
+                                  size_t* temp_bytes, hipStream_t stream);
 hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
                                  const uint32_t* vals_in, const uint8_t* flags, uint64_t* keys_out,
                                  uint32_t* vals_out, uint64_t* n_out, uint64_t n,

@@ -35,29 +35,41 @@ namespace {
 // there. Finalize: write the winning row's fid into the slot; collect entry count, longest
 // chain and the number of keys displaced past their home bucket.
 // ---------------------------------------------------------------------------------------------
+// Wide tables (K > 8): the same with 16-byte slots (kma_internal.h): the claim is a 64-bit CAS
+// of the slot's key words (x | y << 32, 0 = empty), the overflow bit and fid live in .z.
+template <bool Wide>
 __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint32_t* winner,
                                                            uint32_t n_buckets, int k, int m,
                                                            const uint64_t* __restrict__ keys,
                                                            uint64_t n, uint32_t* status) {
+  constexpr int S = Wide ? kWideSlots : kSlotsPerBucket;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     if (key == 0) continue;
-    const uint64_t want = slot_make(key, 0);
+    const uint64_t want = Wide ? key : slot_make(key, 0);
     const uint32_t home = home_bucket(key, k, m, n_buckets);
     uint32_t b = home;
     bool done = false;
     for (uint32_t p = 0; p < n_buckets && !done; ++p) {
       b = chain_bucket(home, p, n_buckets);
-      for (int j = 0; j < kSlotsPerBucket; ++j) {
-        uint64_t* sp = slots + (uint64_t)b * kSlotsPerBucket + j;
+      for (int j = 0; j < S; ++j) {
+        const uint64_t si = (uint64_t)b * S + j;
+        uint64_t* sp = slots + (Wide ? 2 * si : si);
         uint64_t v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((uint32_t)v == 0u) {  // empty (possibly with its overflow bit set): claim it
-          const uint64_t old = atomicCAS((unsigned long long*)sp, (unsigned long long)v, v | want);
-          v = old == v ? (v | want) : old;
+        if (Wide) {
+          while (v == 0) {  // empty: claim it
+            const uint64_t old = atomicCAS((unsigned long long*)sp, 0ull, (unsigned long long)want);
+            v = old == 0 ? want : old;
+          }
+        } else {
+          while ((uint32_t)v == 0u) {  // empty (possibly with its overflow bit set): claim it
+            const uint64_t old = atomicCAS((unsigned long long*)sp, (unsigned long long)v, v | want);
+            v = old == v ? (v | want) : old;
+          }
         }
-        if (slot_key(v) == key) {
-          atomicMax(winner + (uint64_t)b * kSlotsPerBucket + j, (uint32_t)(i + 1));
+        if ((Wide ? v : slot_key(v)) == key) {
+          atomicMax(winner + si, (uint32_t)(i + 1));
           done = true;
           break;
         }
@@ -66,27 +78,39 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
     if (!done) {
       atomicOr(status, 1u);  // table full: cannot happen at load factor < 1
     } else if (b != home) {
-      uint32_t* hi = reinterpret_cast<uint32_t*>(
-                         slots + (uint64_t)home * kSlotsPerBucket + ovf_index((uint32_t)key)) + 1;
-      atomicOr(hi, kOvfBit);
+      uint32_t* ovf = Wide ? reinterpret_cast<uint32_t*>(
+                                 slots + 2 * ((uint64_t)home * S + ovf_index_wide((uint32_t)key)) + 1)
+                           : reinterpret_cast<uint32_t*>(
+                                 slots + (uint64_t)home * S + ovf_index((uint32_t)key)) + 1;
+      atomicOr(ovf, kOvfBit);
     }
   }
 }
 
+template <bool Wide>
 __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
                                                              const uint32_t* __restrict__ winner,
                                                              const uint32_t* __restrict__ fids,
                                                              uint32_t n_buckets, int k, int m,
                                                              uint32_t* stats) {
-  const uint64_t n_slots = (uint64_t)n_buckets * kSlotsPerBucket;
+  constexpr int S = Wide ? kWideSlots : kSlotsPerBucket;
+  const uint64_t n_slots = (uint64_t)n_buckets * S;
   uint32_t entries = 0, max_probe = 0, displaced = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_slots;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t w = winner[i];
     if (w == 0) continue;
-    const uint64_t v = slots[i];
-    slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
-    const uint32_t b = (uint32_t)(i / kSlotsPerBucket), h = home_bucket(slot_key(v), k, m, n_buckets);
+    uint64_t key;
+    if (Wide) {
+      key = slots[2 * i];
+      uint32_t* meta = reinterpret_cast<uint32_t*>(slots + 2 * i + 1);
+      *meta = *meta | (fids[w - 1] & kFidMask);  // keep the overflow bit
+    } else {
+      const uint64_t v = slots[i];
+      slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
+      key = slot_key(v);
+    }
+    const uint32_t b = (uint32_t)(i / S), h = home_bucket(key, k, m, n_buckets);
     const uint32_t d = chain_step(h, b, n_buckets) + 1u;
     entries++;
     displaced += d > 1u ? 1u : 0u;
@@ -446,20 +470,6 @@ namespace kma {
 namespace {
 #endif
 
-// The direct path for a device list of proteins (giant ones, and those of partitioned-path
-// chunks that crowd one region): one protein per block step, persistent blocks.
-template <int K, int M, int P>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void
-annotate_list_kernel(ProteinArgs a) {
-  __shared__ ProteinSmem<P> sm;
-  const uint32_t n = *a.list_n;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    annotate_block<K, M, P>(a, sm, a.list[i], 1u);
-    __syncthreads();  // the records are read before the next protein's are written
-  }
-}
-
-
 // ---------------------------------------------------------------------------------------------
 // 6-frame contig annotation. A block owns kContigTile consecutive forward positions x of the
 // concatenated contigs. Position x anchors two windows whose DNA span is [x, x + 3K):
@@ -518,6 +528,11 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
 
 template <int K, int M>
 __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
+  // K > 8: a wide table (16-byte slots, kma_internal.h): one slot per lane of the quad.
+  constexpr bool kWide = wide_k(K);
+  constexpr int kS = kWide ? kWideSlots : kSlotsPerBucket;   // slots per bucket
+  constexpr int kQ = kWide ? 4 : kBucketQuads;                // dwordx4 per bucket
+  constexpr int kH = kWide ? 1 : kBucketHalves;               // 64-byte pieces per bucket
   constexpr int kSpan = kContigTile + 3 * K;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   __shared__ uint8_t bases[kSpan];
@@ -622,7 +637,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     bk[h][0] = pv ? home_bucket(key[h][0], K, M, nb) : kNone;
     bk[h][1] = mv ? home_bucket(key[h][1], K, M, nb) : kNone;
   }
-  uint4 q[CP][2][4][kBucketHalves];  // every window's quad buckets: all dwordx4 in flight
+  uint4 q[CP][2][4][kH];  // every window's quad buckets: all dwordx4 in flight
 #pragma unroll
   for (int h = 0; h < CP; ++h)
 #pragma unroll
@@ -633,9 +648,9 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint4* bp = reinterpret_cast<const uint4*>(a.slots) + part +
-                          (uint64_t)(bb[r] == kNone ? 0u : bb[r]) * kBucketQuads;
+                          (uint64_t)(bb[r] == kNone ? 0u : bb[r]) * kQ;
 #pragma unroll
-        for (int hh = 0; hh < kBucketHalves; ++hh) q[h][j][r][hh] = bp[4 * hh];
+        for (int hh = 0; hh < kH; ++hh) q[h][j][r][hh] = bp[4 * hh];
       }
     }
   KMA_CLK(3);  // bucket loads issued
@@ -645,7 +660,8 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   for (int h = 0; h < CP; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const uint32_t klo = (uint32_t)key[h][j], khi = (uint32_t)(key[h][j] >> 32) << 24;
+      const uint32_t klo = (uint32_t)key[h][j];
+      const uint32_t khi = kWide ? (uint32_t)(key[h][j] >> 32) : (uint32_t)(key[h][j] >> 32) << 24;
       uint32_t word = 0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -653,15 +669,21 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
                           : rr == 2 ? quad_bcast<2>(klo) : quad_bcast<3>(klo);
         const uint32_t kh = rr == 0 ? quad_bcast<0>(khi) : rr == 1 ? quad_bcast<1>(khi)
                           : rr == 2 ? quad_bcast<2>(khi) : quad_bcast<3>(khi);
-        const uint32_t v = match_part(q[h][j][rr], kl, kh, part);
+        uint32_t v;
+        if constexpr (kWide) v = match_wide(q[h][j][rr][0], kl, kh, part);
+        else v = match_part(q[h][j][rr], kl, kh, part);
         word = part == rr ? v : word;
       }
       const uint32_t w = bk[h][j] != kNone ? word : 0u;
       hit[h][j] = (w & kWordFid) != 0u;
       fid[h][j] = (w & kWordFid) - 1u;
-      uint32_t sid = bk[h][j] * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask);
-      if (w == 0x80000000u)  // rare: the home bucket missed with the key's overflow bit set
-        hit[h][j] = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+      uint32_t sid = bk[h][j] * kS + ((w >> kSlotShift) & (kS - 1));
+      if (w == 0x80000000u) {  // rare: the home bucket missed with the key's overflow bit set
+        if constexpr (kWide)
+          hit[h][j] = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+        else
+          hit[h][j] = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+      }
       if (a.strict_pass && hit[h][j]) {  // KmerFactory.Strict: locations counted by slot id
         if (a.strict_pass == 1) atomicAdd(a.slot_count + sid, 1u);
         else hit[h][j] = a.slot_count[sid] == 1u;
@@ -747,18 +769,19 @@ __global__ __launch_bounds__(256) void singleton_flags_kernel(const uint64_t* __
   }
 }
 
-// Signature build (BuildKmerProcessor.java:137-223). One wave per protein: the windows of
-// ProteinKmers (i = 0..L-K, or i < L-K with end_exclusive) of interesting pegs (role >= 0) and
-// buffered proteins (role -1) become key << 24 | role (kBuildNeg for buffered); every other
-// position gets 0. A window with a byte the standard alphabet cannot encode raises alpha_flag
-// (the host refuses the batch rather than drop a kmer the reference would keep).
+// Signature build (BuildKmerProcessor.java:137-223). One wave per protein: every window of
+// ProteinKmers (i = 0..L-K, or i < L-K with end_exclusive) of an interesting peg (role >= 0) or
+// a buffered protein (role -1) becomes (key, role or kBuildNeg); every other position gets key 0.
+// A window with a byte the standard alphabet cannot encode raises alpha_flag (the host refuses
+// the batch rather than drop a kmer the reference would keep). Keys are up to 60 bits (K <= 12).
 __global__ __launch_bounds__(256) void build_windows_kernel(const uint8_t* __restrict__ residues,
                                                             const uint64_t* __restrict__ offsets,
                                                             uint32_t n_seq,
                                                             const int32_t* __restrict__ roles,
                                                             int k, int end_exclusive,
                                                             const uint8_t* __restrict__ lut_g,
-                                                            uint64_t* __restrict__ out,
+                                                            uint64_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ tags,
                                                             uint32_t* __restrict__ alpha_flag) {
   __shared__ uint8_t lut[256];
   lut[threadIdx.x] = lut_g[threadIdx.x];
@@ -771,7 +794,7 @@ __global__ __launch_bounds__(256) void build_windows_kernel(const uint8_t* __res
     const int32_t role = roles[s];
     const int64_t n_win = (int64_t)(hi - lo) - k + (end_exclusive ? 0 : 1);
     const bool counted = role >= -1;
-    const uint64_t tag = role >= 0 ? (uint64_t)role : (uint64_t)kBuildNeg;
+    const uint32_t tag = role >= 0 ? (uint32_t)role : kBuildNeg;
     bool bad = false;
     for (uint64_t p = lo + lane; p < hi; p += 64) {
       const int64_t i = (int64_t)(p - lo);
@@ -785,23 +808,41 @@ __global__ __launch_bounds__(256) void build_windows_kernel(const uint8_t* __res
           key = (key << 5) | c;
         }
         bad = bad || !ok;
-        v = ok ? (key << 24) | tag : 0;
+        v = ok ? key : 0;
       }
-      out[p - o0] = v;
+      keys[p - o0] = v;
+      tags[p - o0] = tag;
     }
     if (__ballot(bad) && lane == 0) atomicOr(alpha_flag, 1u);
   }
 }
 
-__global__ __launch_bounds__(256) void signature_flags_kernel(const uint64_t* __restrict__ u,
-                                                              const uint64_t* __restrict__ n_u,
-                                                              uint8_t* __restrict__ flags) {
-  const uint64_t n = *n_u;
+// RoleCounter over the (key, role) pairs sorted by key (RoleCounter.java:42-56: a kmer is good
+// iff every count hit its first role; BuildKmerProcessor.java:191-208 removes kmers of buffered
+// proteins). Pass 1: a run's first pair is flagged, and its index is the run id of every pair
+// of the run (max-scan of head indices). Pass 2: a pair whose role differs from its run's
+// first, or that comes from a buffered protein, clears the run's flag.
+__global__ __launch_bounds__(256) void sig_heads_kernel(const uint64_t* __restrict__ k, uint64_t n,
+                                                        uint8_t* __restrict__ flags,
+                                                        uint32_t* __restrict__ head_idx) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * 256) {
-    const uint64_t v = u[i], key = v >> 24;
-    flags[i] = key != 0 && (v & kBuildNeg) != kBuildNeg && (i == 0 || (u[i - 1] >> 24) != key) &&
-               (i + 1 == n || (u[i + 1] >> 24) != key);
+    const uint64_t v = k[i];
+    const bool head = v != 0 && (i == 0 || k[i - 1] != v);
+    flags[i] = head ? 1 : 0;
+    head_idx[i] = head ? (uint32_t)i : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restrict__ k,
+                                                        const uint32_t* __restrict__ tags,
+                                                        const uint32_t* __restrict__ run,
+                                                        uint64_t n, uint8_t* __restrict__ flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * 256) {
+    if (k[i] == 0) continue;
+    const uint32_t h = run[i], t = tags[i];
+    if (t == kBuildNeg || t != tags[h]) flags[h] = 0;  // every writer stores 0
   }
 }
 
@@ -842,23 +883,34 @@ static unsigned grid_for(uint64_t n, unsigned cap = 8192) {
 hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buckets, int k,
                                int m, const uint64_t* keys, uint64_t n, uint32_t* status,
                                hipStream_t stream) {
-  hipLaunchKernelGGL(build_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream, slots, winner,
-                     n_buckets, k, m, keys, n, status);
+  if (wide_k(k))
+    hipLaunchKernelGGL(build_insert_kernel<true>, dim3(grid_for(n)), dim3(256), 0, stream, slots,
+                       winner, n_buckets, k, m, keys, n, status);
+  else
+    hipLaunchKernelGGL(build_insert_kernel<false>, dim3(grid_for(n)), dim3(256), 0, stream, slots,
+                       winner, n_buckets, k, m, keys, n, status);
   return hipGetLastError();
 }
 
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream) {
-  hipLaunchKernelGGL(build_finalize_kernel,
-                     dim3(grid_for((uint64_t)n_buckets * kSlotsPerBucket)), dim3(256), 0, stream,
-                     slots, winner, fids, n_buckets, k, m, stats);
+  const dim3 g(grid_for((uint64_t)n_buckets * slots_for_k(k)));
+  if (wide_k(k))
+    hipLaunchKernelGGL(build_finalize_kernel<true>, g, dim3(256), 0, stream, slots, winner, fids,
+                       n_buckets, k, m, stats);
+  else
+    hipLaunchKernelGGL(build_finalize_kernel<false>, g, dim3(256), 0, stream, slots, winner, fids,
+                       n_buckets, k, m, stats);
   return hipGetLastError();
 }
 
 template <int K, int M>
 struct AnnotateLaunch {
   static hipError_t run(const ProteinArgs& a, hipStream_t stream) {
+    if constexpr (wide_k(K)) {  // the protein path packs windows of <= 8 residues (one u64)
+      return hipErrorInvalidValue;
+    } else {
     constexpr int P = kBlockProteins;
     const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= (uint32_t)P ? a.block_proteins : 4u;
     if (bp != a.block_proteins) return hipErrorInvalidValue;
@@ -867,25 +919,13 @@ struct AnnotateLaunch {
     hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(a.defer_below ? 2 * blocks : blocks),
                        dim3(256), 0, stream, a);
     return hipGetLastError();
+    }
   }
 };
 
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream) {
   if (a.n_seq == 0) return hipSuccess;
   return dispatch_km<AnnotateLaunch>(a.k, a.mlen, a, stream);
-}
-
-template <int K, int M>
-struct AnnotateListLaunch {
-  static hipError_t run(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
-    hipLaunchKernelGGL((annotate_list_kernel<K, M, kBlockProteins>), dim3(blocks), dim3(256), 0,
-                       stream, a);
-    return hipGetLastError();
-  }
-};
-
-hipError_t launch_annotate_list(const ProteinArgs& a, unsigned blocks, hipStream_t stream) {
-  return dispatch_km<AnnotateListLaunch>(a.k, a.mlen, a, blocks ? blocks : 1u, stream);
 }
 
 template <int K, int M>
@@ -955,34 +995,30 @@ hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t*
 
 hipError_t launch_build_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq,
                                 const int32_t* roles, int k, int end_exclusive, const uint8_t* lut,
-                                uint64_t* out, uint32_t* alpha_flag, hipStream_t stream) {
+                                uint64_t* keys, uint32_t* tags, uint32_t* alpha_flag,
+                                hipStream_t stream) {
   const unsigned g = (unsigned)std::min<uint64_t>(8192, ((uint64_t)n_seq + 3) / 4);
   hipLaunchKernelGGL(build_windows_kernel, dim3(g ? g : 1), dim3(256), 0, stream, residues,
-                     offsets, n_seq, roles, k, end_exclusive, lut, out, alpha_flag);
+                     offsets, n_seq, roles, k, end_exclusive, lut, keys, tags, alpha_flag);
   return hipGetLastError();
 }
 
-hipError_t launch_sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                            uint64_t n, int bits, hipStream_t stream) {
-  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, (int)n, 0, bits, stream);
-}
-
-hipError_t launch_unique(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                         uint64_t* n_out, uint64_t n, hipStream_t stream) {
-  return hipcub::DeviceSelect::Unique(temp, *temp_bytes, in, out, n_out, (int)n, stream);
-}
-
-hipError_t launch_signature_flags(const uint64_t* uniq, const uint64_t* n_uniq, uint64_t n_max,
-                                  uint8_t* flags, hipStream_t stream) {
-  hipLaunchKernelGGL(signature_flags_kernel, dim3(grid_for(n_max)), dim3(256), 0, stream, uniq,
-                     n_uniq, flags);
+hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, uint64_t n,
+                                  uint8_t* flags, uint32_t* head_idx, uint32_t* run, void* temp,
+                                  size_t* temp_bytes, hipStream_t stream) {
+  if (!temp)
+    return hipcub::DeviceScan::InclusiveScan(nullptr, *temp_bytes, head_idx, run, hipcub::Max(),
+                                             (int)n, stream);
+  hipLaunchKernelGGL(sig_heads_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, n, flags,
+                     head_idx);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::InclusiveScan(temp, *temp_bytes, head_idx, run, hipcub::Max(), (int)n,
+                                        stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sig_clear_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, tags, run,
+                     n, flags);
   return hipGetLastError();
-}
-
-hipError_t launch_select_flagged_keys(void* temp, size_t* temp_bytes, const uint64_t* in,
-                                      const uint8_t* flags, uint64_t* out, uint64_t* n_out,
-                                      uint64_t n, hipStream_t stream) {
-  return hipcub::DeviceSelect::Flagged(temp, *temp_bytes, in, flags, out, n_out, (int)n, stream);
 }
 
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {

@@ -20,7 +20,7 @@ OK = 0
 E_INVALID, E_DEVICE, E_NOMEM, E_CAPACITY, E_ALPHABET, E_TABLE_FULL = -1, -2, -3, -4, -5, -6
 STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN = 0, 1, 2, 3
 F_END_EXCLUSIVE, F_MULTISET = 0x1, 0x2
-MAX_K = 8
+MAX_K = 12  # K <= 8: narrow tables (8-byte slots); 9..12: wide tables (16-byte slots)
 
 # Every symbol include/kmeranno.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -35,7 +35,7 @@ EXPORTS = (
     "kma_table_create_replicated", "kma_table_replicate", "kma_table_replicas",
     "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
     "kma_workspace_reserve_batch", "kma_workspace_phases_read", "kma_propose_pegs",
-    "kma_hash_annotate",
+    "kma_hash_annotate", "kma_bucket_slots_for", "kma_table_buckets_for_k",
 )
 
 
@@ -50,7 +50,8 @@ class TableInfo(C.Structure):
                 ("n_buckets", C.c_uint64), ("bytes", C.c_uint64), ("k", C.c_int32),
                 ("device", C.c_int32), ("max_probe", C.c_uint32), ("n_extra_syms", C.c_uint32),
                 ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32),
-                ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32), ("reserved", C.c_int32)]
+                ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32),
+                ("slots_per_bucket", C.c_int32)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
@@ -86,6 +87,9 @@ def load(path: str | None = None):
         L.kma_table_destroy.argtypes = [_vp]
         L.kma_table_buckets_for.restype = _u64
         L.kma_table_buckets_for.argtypes = [_u64, C.c_double]
+        L.kma_table_buckets_for_k.restype = _u64
+        L.kma_table_buckets_for_k.argtypes = [_u64, C.c_double, _int]
+        L.kma_bucket_slots_for.argtypes = [_int]
         L.kma_table_build_device.argtypes = [_vp, _u64, _int, _int, _vp, _vp, _vp, _u64, _vp,
                                              _vp]
         L.kma_table_wrap_device.argtypes = [_vp, _u64, _int, _int, _int, C.POINTER(_vp)]
@@ -322,13 +326,14 @@ class Workspace:
             pass
 
 
-def buckets_for(n_keys: int, load_factor: float = 0.5) -> int:
-    return int(load().kma_table_buckets_for(n_keys, load_factor))
+def buckets_for(n_keys: int, load_factor: float = 0.5, k: int = 8) -> int:
+    return int(load().kma_table_buckets_for_k(n_keys, load_factor, k))
 
 
-def bucket_slots() -> int:
-    """u64 slots per bucket of this build (8: 64-byte buckets; 16: the 128-byte variant)."""
-    return int(load().kma_bucket_slots())
+def bucket_slots(k: int = 8) -> int:
+    """Slots per bucket of a table of k-mers: narrow (k <= 8) u64 slots of this build (8: 64-byte
+    buckets; 16: the 128-byte variant), wide (k 9..12) 4 slots of 16 bytes."""
+    return int(load().kma_bucket_slots_for(k))
 
 
 def layout_for(k: int, n_buckets: int) -> int:

@@ -144,19 +144,39 @@ def peg_connect(prots, contigs, gcode: int = 11, k: int = 8, strict: bool = Fals
     return out
 
 
+class RoleCounter:
+    """kmers/RoleCounter.java:14-78, literally: the role first associated with a kmer, and the
+    counts of hits in that role (good) and in any other (bad); good iff no bad hit."""
+
+    def __init__(self, role_id):
+        self.role_id = role_id      # RoleCounter(String roleId)  :31-35
+        self.good_count = 0
+        self.bad_count = 0
+
+    def count(self, role_hit) -> bool:  # :43-50
+        ret = self.role_id == role_hit
+        if ret:
+            self.good_count += 1
+        else:
+            self.bad_count += 1
+        return ret
+
+    def is_good(self) -> bool:  # :55-57
+        return self.bad_count == 0
+
+
 def build_signatures(prots, roles, k: int = 8, end_exclusive: bool = False):
     """BuildKmerProcessor.java:137-223 + RoleCounter: roles[i] >= 0 = the single good role of
     an interesting peg, -1 = a buffered protein, other = skipped. Returns {kmer: role}."""
-    first, bad = {}, set()
+    counters = {}
     for p, r in zip(prots, roles):
         if r < 0:
             continue
         for km in protein_kmers(p, k, end_exclusive, False):
-            if km not in first:
-                first[km] = r
-            elif first[km] != r:
-                bad.add(km)
-    keep = {km: r for km, r in first.items() if km not in bad}
+            # kmerMap.computeIfAbsent(kmer, k -> new RoleCounter(role)).count(role)  :165-175
+            counters.setdefault(km, RoleCounter(r)).count(r)
+    # kmerMap.values().removeIf(x -> ! x.isGood())  :182-190
+    keep = {km: c.role_id for km, c in counters.items() if c.is_good()}
     for p, r in zip(prots, roles):
         if r == -1:
             for km in protein_kmers(p, k, end_exclusive, False):

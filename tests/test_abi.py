@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 3
+    assert native_lib.kma_abi_version() == 4
     assert isinstance(native_lib.kma_last_error(), bytes)
 
 
@@ -36,6 +36,10 @@ def test_bucket_sizing_host_helper(native_lib):
     assert kmeranno.buckets_for(1000, 0.5) == 2000 // s
     assert kmeranno.buckets_for(10**8, 0.75) * s >= 10**8 / 0.75
     assert kmeranno.buckets_for(0, 0.5) == 1
+    # wide tables (K 9..12): four 16-byte slots per 64-byte bucket
+    assert kmeranno.bucket_slots(8) == s and kmeranno.bucket_slots(12) == 4
+    assert kmeranno.bucket_slots(13) == 0 and kmeranno.bucket_slots(0) == 0
+    assert kmeranno.buckets_for(1000, 0.5, k=10) == 500
 
 
 def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):

@@ -34,24 +34,48 @@ def _family_proteins(rng, n_fam=80, n=1500):
 
 
 @pytest.mark.parametrize("flags", [0, 1])
-def test_build_signatures_vs_oracle(kma, oracle_c, flags):
+@pytest.mark.parametrize("k", [8, 10, 12])
+def test_build_signatures_vs_oracle(kma, oracle_c, flags, k):
     """The discriminating (kmer, role) rows equal the oracle's, in key order without
-    duplicates; a window with a byte outside A-Z/'*' is refused (KMA_E_ALPHABET)."""
-    rng = np.random.default_rng(17 + flags)
+    duplicates, at K = 8 and the wide sizes (BuildKmerProcessor -K, :84-87); a window with a
+    byte outside A-Z/'*' is refused (KMA_E_ALPHABET)."""
+    rng = np.random.default_rng(17 + flags + k)
     prots, roles = _family_proteins(rng)
-    prots += ["", "ACDEFGH", "ACDEFGHI", "ACDEFGHIK"]
-    roles += [3, 3, 4, 5]
+    prots += ["", "ACDEFGH", "ACDEFGHI", "ACDEFGHIK", "ACDEFGHIKLMN", "ACDEFGHIKLMNP"]
+    roles += [3, 3, 4, 5, 6, 7]
     res, off = oracle_c.pack_strings(prots)
-    km, rl = oracle_c.build_signatures(res, off, roles, K, flags)
-    keys, groles = kma.build_signatures(res, off, roles, K, flags)
+    km, rl = oracle_c.build_signatures(res, off, roles, k, flags)
+    keys, groles = kma.build_signatures(res, off, roles, k, flags)
     from kmeranno import synth
-    got = {synth.unpack_key(x): int(r) for x, r in zip(keys.tolist(), groles)}
+    got = {synth.unpack_key(x, k): int(r) for x, r in zip(keys.tolist(), groles)}
     exp = {bytes(r).decode(): int(v) for r, v in zip(km, rl)}
     assert len(exp) > 10_000 and got == exp
     assert (np.diff(keys.astype(np.int64)) > 0).all()
     with pytest.raises(kma.KmerAnnoError) as e:
-        kma.build_signatures(*oracle_c.pack_strings(["ACDEFGHIKLmNP"]), [0], K)
+        kma.build_signatures(*oracle_c.pack_strings(["ACDEFGHIKLmNP"]), [0], k)
     assert e.value.code == kma.E_ALPHABET
+
+
+@pytest.mark.parametrize("k", [8, 10])
+def test_build_role_counter_RoleTests(kma, k):
+    """test/RoleTests.java:15-36 through kma_build_signatures: a kmer hit twice by roleA (good
+    count 2, bad 0) is kept for roleA; hit by roleB afterwards (bad count 1) it is dropped,
+    and so when roleB came first; a buffered protein removes it; a skipped peg does not."""
+    from kmeranno import synth
+    A, B = 0, 1
+    shared = "PPMKVLAGHW"[-k:]
+    prot = "QQ" + shared + "NN"
+    others = {A: "CCCCDEFGHIKLMNPQ", B: "WWWWYYYYVVVVTTTT"}
+    for roles, kept in (([A, A], True), ([A, A, B], False), ([B, A], False),
+                        ([A, -1], False), ([A, -2], True)):
+        prots = [prot] * len(roles) + [others[A], others[B]]
+        res, off = kma.pack_strings(prots)
+        keys, rl = kma.build_signatures(res, off, roles + [A, B], k)
+        got = {synth.unpack_key(x, k): int(r) for x, r in zip(keys.tolist(), rl)}
+        assert (shared in got) == kept, roles
+        if kept:
+            assert got[shared] == A
+        assert all(v == A for km, v in got.items() if km in others[A])
 
 
 def test_build_then_apply_roundtrip(kma, oracle_c):

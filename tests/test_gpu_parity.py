@@ -33,20 +33,12 @@ def layout(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["direct", "defer", "part"])
+@pytest.fixture(params=["direct", "defer"])
 def path(request, monkeypatch):
-    """Protein paths: the direct kernel with every group in block order (KMA_DEFER=0), the
-    direct kernel's two-pass grid deferring groups of fewer than 2 probe steps (forced on
-    every batch; automatic only for grids of 1-4 resident waves), and the region-partitioned
-    path (forced, with 64-bucket regions so that the small test tables still cut into hundreds
-    of regions; chunks that crowd one region fall back to the direct list kernel). KMA_PATH /
-    KMA_DEFER / KMA_REGION_BITS are read per call."""
-    if request.param in ("direct", "defer"):
-        monkeypatch.setenv("KMA_PATH", "direct")
-        monkeypatch.setenv("KMA_DEFER", "0" if request.param == "direct" else "2")
-    else:
-        monkeypatch.setenv("KMA_PATH", "partitioned")
-        monkeypatch.setenv("KMA_REGION_BITS", "6")
+    """Grids of the protein kernel: every group in block order (KMA_DEFER=0), and the two-pass
+    grid deferring groups of fewer than 2 probe steps (forced on every batch; automatic only
+    for grids of 1-4 resident waves). KMA_DEFER is read per call."""
+    monkeypatch.setenv("KMA_DEFER", "0" if request.param == "direct" else "2")
     return request.param
 
 
@@ -156,7 +148,6 @@ def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defe
     kmers = [synth.unpack_key(x) for x in wl.keys]
     ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
-    monkeypatch.setenv("KMA_PATH", "direct")
     monkeypatch.setenv("KMA_DEFER", defer)
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
         for bp in ("4", "1", "4", "1"):
@@ -343,64 +334,6 @@ def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c):
     assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
 
 
-@pytest.mark.timeout(600)
-def test_config5_size_sample_and_properties(kma, oracle_c, monkeypatch):
-    """BASELINE configs[4]: the 10^8-entry table (1.5 GiB, m = 6 layout since hashed chains) and
-    the 1M-protein batch. A random 20k-protein sample of the batch is bit-exact against the
-    oracle; the whole batch is checked by properties: a second call on shuffled-size shards
-    (device entry point on pointer offsets) gives identical outputs, the tally equals the
-    called-fid histogram, and copies called are called for their own function."""
-    torch = pytest.importorskip("torch")
-    from kmeranno import synth
-    n_seq, t_size, n_fid, seed = synth.CONFIGS["c5"]
-    sig = synth.make_table(t_size, n_fid, seed, K)
-    res, off, kinds, true_fid = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
-    print(f"c5 workload generated: {len(res)} residues", flush=True)
-    dev = torch.device("cuda", 0)
-    with _config_table(kma, sig) as t:
-        assert t.info.minimizer_len == 6 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
-        assert t.info.n_entries > 0.99 * t_size
-        monkeypatch.delenv("KMA_PATH", raising=False)  # automatic: the partitioned path here
-        monkeypatch.delenv("KMA_REGION_BITS", raising=False)
-        fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
-        # property 0: the direct path gives the same outputs on the whole batch
-        monkeypatch.setenv("KMA_PATH", "direct")
-        got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
-        for a, b in zip(got, (fid, cnt, st, tally)):
-            assert (a == b).all()
-        monkeypatch.delenv("KMA_PATH")
-        # property 1: the same batch cut into uneven shards through the device entry point
-        d_res = torch.from_numpy(res).to(dev)
-        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
-        d_fid = torch.empty(n_seq, dtype=torch.int32, device=dev)
-        d_cnt = torch.empty(n_seq, dtype=torch.int32, device=dev)
-        d_st = torch.empty(n_seq, dtype=torch.uint8, device=dev)
-        ws = kma.Workspace(0, int(off[-1]))
-        stream = torch.cuda.current_stream().cuda_stream
-        cuts = [0, 1, 7, 4096, 333_333, 500_001, 999_999, n_seq]
-        for lo, hi in zip(cuts[:-1], cuts[1:]):
-            kma.annotate_proteins_device(t, ws, d_res.data_ptr(), d_off.data_ptr() + 8 * lo,
-                                         hi - lo, int(off[hi] - off[lo]), 5, 0,
-                                         d_fid.data_ptr() + 4 * lo, d_cnt.data_ptr() + 4 * lo,
-                                         d_st.data_ptr() + lo, 0, 0, stream)
-        torch.cuda.synchronize()
-        assert (d_fid.cpu().numpy() == fid).all() and (d_cnt.cpu().numpy() == cnt).all()
-        assert (d_st.cpu().numpy() == st).all()
-        ws.close()
-    # property 2: tally = histogram of called fids; copies called carry their own function
-    assert (tally == np.bincount(fid[st == 1], minlength=n_fid)).all()
-    copies = (kinds == 0) & (st == 1)
-    assert copies.sum() > 0.2 * n_seq  # decoy hits make many copies AMBIGUOUS at 10^8
-    assert (fid[copies] == true_fid[copies]).mean() > 0.999
-    # sample vs the oracle
-    rng = np.random.default_rng(55)
-    idx = np.sort(rng.choice(n_seq, 20_000, replace=False))
-    sres, soff = take_proteins(res, off, idx)
-    ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, sres)
-    efid, ecnt, est = oracle_c.apply(ot, sres, soff, K, 5, 0)
-    assert (st[idx] == est).all() and (fid[idx] == efid).all() and (cnt[idx] == ecnt).all()
-
-
 def test_contigs_golden(kma, layout):
     z = np.load(os.path.join(GOLDEN, "contigs_gto.npz"))
     with kma.SignatureTable.from_rows([bytes(r).decode() for r in z["table_kmers"]],
@@ -533,20 +466,11 @@ def test_workspace_timing(kma):
         calls, kernel_ms, rest_ms = ws.timing_read()
         assert calls == 3 and kernel_ms > 0 and rest_ms >= 0
         assert ws.timing_read()[0] == 0
-        for forced, phases in (("direct", ["annotate_kernel"]),
-                               ("partitioned", ["chunking", "partition_kernel",
-                                                "probe_regions_kernel", "vote_chunks_kernel",
-                                                "annotate_list_kernel"])):
-            os.environ["KMA_PATH"] = forced
-            try:
-                for _ in range(2):
-                    kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res,
-                                                 5, 0, *[o.data_ptr() for o in outs], 0, 0,
-                                                 stream)
-            finally:
-                del os.environ["KMA_PATH"]
-            calls, ph = ws.phases_read()
-            assert calls == 2 and list(ph) == phases and all(v >= 0 for v in ph.values())
+        for _ in range(2):
+            kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
+                                         *[o.data_ptr() for o in outs], 0, 0, stream)
+        calls, ph = ws.phases_read()
+        assert calls == 2 and list(ph) == ["annotate_kernel"] and ph["annotate_kernel"] > 0
         with pytest.raises(kma.KmerAnnoError) as e:  # reservation too small
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res + 1, 5,
                                          0, *[o.data_ptr() for o in outs], 0, 0, stream)
