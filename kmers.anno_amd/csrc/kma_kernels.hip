@@ -217,7 +217,12 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs
   atomicMin(&sm.pmin[p], fid);
   atomicMax(&sm.pmax[p], fid);
   bool fresh = true;  // multiset: every hit counts
+#ifdef KMA_TUNE_NO_SET  // tuning builds only (cost bound of the distinct-key sets; wrong counts)
+  fresh = false;
+  if (false) {
+#else
   if (!multiset) {
+#endif
     const uint32_t base = sm.pset[p], cap = sm.pcap[p];
     fresh = base != kGlobalSet
                 ? lds_set_insert(sm.pool + base, cap, sid + 1u)
@@ -409,7 +414,11 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
         record_hit<P>(sm, a, span_lo, multiset, bk[j] >> kBucketBits, (w & kWordFid) - 1u,
                       (bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
       // rare: the home bucket missed with the key's overflow bit set -> deferred chain walk
+#ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
+      const bool pend = false;
+#else
       const bool pend = w == 0x80000000u;
+#endif
       const uint64_t m = __ballot(pend);
       if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + t;
       cn += (uint32_t)__popcll(m);

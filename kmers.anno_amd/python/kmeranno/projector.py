@@ -15,9 +15,16 @@ available). Restated choices, documented:
     (ATG, GTG, TTG) farthest upstream before the previous in-frame stop; no stop before the
     contig end, or no start, gives no proposal (PegProposal.create returns null). '-' strand
     mirrored on the reverse complement. Ambiguous bases never form start or stop codons.
-  - PegProposalList keeps one proposal per (contig, strand, end) — the intent of
-    PegProposal.equals / hashCode; the Java TreeSet's comparator is inconsistent with equals,
-    so its exact tie behaviour depends on tree shape and is not reproduced.
+  - PegProposalList is the reference's literally: a java.util.TreeSet ordered by
+    PegProposal.compareTo (PegProposal.java:85-98: contig id, then "equal" when end and strand
+    match, else left edge, then shorter first). That comparator is not consistent with equals
+    (same left and length on the other strand compare equal; two proposals with one end can
+    sit apart when the search path misses one), so which proposals survive depends on the
+    tree's shape: _TreeSet restates java.util.TreeMap's red-black put (search, attach,
+    fixAfterInsertion with its rotations) so the shape, the equal-key found by add, and the
+    in-order iteration are Java's for the same insertion order. merge() moves the kept
+    proposal's begin in place (Location.setBegin), as in Java. oracle/proposal_list.py is the
+    independent restatement the tests compare with.
 """
 from __future__ import annotations
 
@@ -38,6 +45,7 @@ class Location:
     strand: str
     left: int   # 1-based, inclusive
     right: int
+    contig_id: str = ""  # Location.getContigId (compareTo orders contigs by it)
 
     @property
     def length(self) -> int:
@@ -77,8 +85,8 @@ def extend(dna: str, loc: Location, gcode: int = 11) -> Location | None:
     if start < 0:
         return None
     if loc.strand == "+":
-        return Location(loc.contig, "+", start + 1, stop_end + 1)
-    return Location(loc.contig, "-", n - stop_end, n - start)
+        return Location(loc.contig, "+", start + 1, stop_end + 1, loc.contig_id)
+    return Location(loc.contig, "-", n - stop_end, n - start, loc.contig_id)
 
 
 @dataclass
@@ -103,16 +111,151 @@ class PegProposal:
             self.loc.right = other.loc.begin
         self.evidence = other.evidence
 
+    def compare_to(self, other: "PegProposal") -> int:  # PegProposal.compareTo :85-98
+        a, b = self.loc, other.loc
+        r = (a.contig_id > b.contig_id) - (a.contig_id < b.contig_id)  # String.compareTo sign
+        if r == 0 and (a.end != b.end or a.strand != b.strand):
+            r = a.left - b.left
+            if r == 0:
+                r = a.length - b.length  # shorter locations go first
+        return r
+
+
+class _Node:
+    __slots__ = ("key", "left", "right", "parent", "black")
+
+    def __init__(self, key, parent):
+        self.key, self.parent = key, parent
+        self.left = self.right = None
+        self.black = True  # new entries are BLACK until fixAfterInsertion colours them
+
+
+class _TreeSet:
+    """java.util.TreeSet over java.util.TreeMap (red-black, CLR), restated for add() and
+    iteration: add returns (True, new) or (False, the entry that compared equal on the search
+    path) — the one tailSet(x).first() then returns, since the tree has not changed."""
+
+    def __init__(self, cmp):
+        self.cmp, self.root, self.size = cmp, None, 0
+
+    def add(self, key):
+        t = self.root
+        if t is None:  # addEntryToEmptyMap
+            self.root = _Node(key, None)
+            self.size = 1
+            return True, key
+        while True:
+            parent = t
+            c = self.cmp(key, t.key)
+            if c < 0:
+                t = t.left
+            elif c > 0:
+                t = t.right
+            else:
+                return False, t.key  # the map keeps the old key
+            if t is None:
+                break
+        e = _Node(key, parent)
+        if c < 0:
+            parent.left = e
+        else:
+            parent.right = e
+        self._fix_after_insertion(e)
+        self.size += 1
+        return True, key
+
+    @staticmethod
+    def _black(x):
+        return x is None or x.black
+
+    def _rotate_left(self, p):
+        r = p.right
+        p.right = r.left
+        if r.left is not None:
+            r.left.parent = p
+        r.parent = p.parent
+        if p.parent is None:
+            self.root = r
+        elif p.parent.left is p:
+            p.parent.left = r
+        else:
+            p.parent.right = r
+        r.left, p.parent = p, r
+
+    def _rotate_right(self, p):
+        lft = p.left
+        p.left = lft.right
+        if lft.right is not None:
+            lft.right.parent = p
+        lft.parent = p.parent
+        if p.parent is None:
+            self.root = lft
+        elif p.parent.right is p:
+            p.parent.right = lft
+        else:
+            p.parent.left = lft
+        lft.right, p.parent = p, lft
+
+    def _fix_after_insertion(self, x):
+        x.black = False
+        while x is not None and x is not self.root and not x.parent.black:
+            p = x.parent
+            g = p.parent
+            if p is (g.left if g else None):
+                y = g.right if g else None
+                if not self._black(y):
+                    p.black, y.black, g.black = True, True, False
+                    x = g
+                else:
+                    if x is p.right:
+                        x = p
+                        self._rotate_left(x)
+                    x.parent.black = True
+                    gg = x.parent.parent
+                    if gg is not None:
+                        gg.black = False
+                        self._rotate_right(gg)
+            else:
+                y = g.left if g else None
+                if not self._black(y):
+                    p.black, y.black = True, True
+                    if g is not None:
+                        g.black = False
+                    x = g
+                else:
+                    if x is p.left:
+                        x = p
+                        self._rotate_right(x)
+                    x.parent.black = True
+                    gg = x.parent.parent
+                    if gg is not None:
+                        gg.black = False
+                        self._rotate_left(gg)
+        self.root.black = True
+
+    def __iter__(self):  # in order (successor walk)
+        stack, n = [], self.root
+        while stack or n is not None:
+            while n is not None:
+                stack.append(n)
+                n = n.left
+            n = stack.pop()
+            yield n.key
+            n = n.right
+
+    def __len__(self):
+        return self.size
+
 
 class PegProposalList:
-    """locations/PegProposalList.java:67-93 (one proposal per ORF end)."""
+    """locations/PegProposalList.java:67-93: the TreeSet of proposals (see module docstring)."""
 
     def __init__(self, contigs: list[str], min_strength: float, min_evidence: int,
                  gcode: int = 11):
         self.contigs, self.min_strength, self.min_evidence = contigs, min_strength, min_evidence
         self.gcode = gcode
         self.made = self.rejected = self.weak = self.small = self.merged = 0
-        self._by_end: dict[tuple, PegProposal] = {}
+        self._set = _TreeSet(lambda a, b: a.compare_to(b))
 
     def propose(self, loc: Location, function: str, evidence: int) -> PegProposal | None:
         self.made += 1
@@ -127,34 +270,35 @@ class PegProposalList:
         if evidence < self.min_evidence:
             self.small += 1
             return None
-        key = (real.contig, real.strand, real.end)
-        old = self._by_end.get(key)
-        if old is None:
-            self._by_end[key] = new
+        added, old = self._set.add(new)
+        if added:
             return new
-        if new.better_than(old):
+        if new.better_than(old):  # the duplicate: tailSet(new).first()
             old.merge(new)
             self.merged += 1
             return old
         return None
 
-    def __iter__(self):  # contig order: by contig, left edge, then shorter first
-        return iter(sorted(self._by_end.values(),
-                           key=lambda p: (p.loc.contig, p.loc.left, p.loc.length)))
+    def __iter__(self):  # the TreeSet's order
+        return iter(self._set)
 
     def __len__(self):
-        return len(self._by_end)
+        return len(self._set)
 
 
 def annotate_proposals(proposals, functions: list[str], contigs: list[str], genome_id: str,
-                       min_strength: float = 0.5, min_evidence: int = 10, gcode: int = 11):
+                       min_strength: float = 0.5, min_evidence: int = 10, gcode: int = 11,
+                       contig_ids: list[str] | None = None):
     """KmerProcessor.annotateGenome's tail (:250-284): the sweep's proposals (PROPOSAL_DTYPE, in
     list order; peg index -> functions[peg]) through PegProposalList with the DNA strength
     min_strength / 3 (:170), then makeFeature (:295-312): [(fid, function, Location, evidence,
-    strength)] in contig order."""
+    strength)] in the list's order. contig_ids: the contigs' ids (compareTo orders by them;
+    default: zero-padded indices, i.e. index order)."""
+    ids = contig_ids or [f"{i:010d}" for i in range(len(contigs))]
     plist = PegProposalList(contigs, min_strength / 3, min_evidence, gcode)
     for p in proposals:
-        loc = Location(int(p["contig"]), chr(p["strand"]), int(p["left"]), int(p["right"]))
+        c = int(p["contig"])
+        loc = Location(c, chr(p["strand"]), int(p["left"]), int(p["right"]), ids[c])
         plist.propose(loc, functions[int(p["peg"])], int(p["evidence"]))
     return [(f"fig|{genome_id}.peg.{i}", p.function, p.loc, p.evidence, p.strength)
             for i, p in enumerate(plist, start=1)], plist

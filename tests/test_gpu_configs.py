@@ -190,7 +190,7 @@ def test_config3_bench_size_vs_oracle(kma, oracle_c):
     ot = oracle_c.Table.from_buffer(rows.tobytes(), np.arange(len(rows) + 1, dtype=np.uint64) * K,
                                     wl.fids[keep].astype(np.int32))
     e = oracle_c.annotate_contigs(ot, wl.dna, wl.offsets, 11, K)
-    assert len(e[0]) > 1_000_000
+    assert len(e[0]) > 100_000
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
         hits, tally = kma.annotate_contigs(t, wl.dna, wl.offsets, 11, n_fid=n_fid)
         dev = torch.device("cuda", 0)
