@@ -16,10 +16,12 @@ Workloads (BASELINE.json configs; the default is c5, the north-star configuratio
   c3  6-frame pass (KmerReference.java:157-203) over a rank's 5 Mbp synthetic genome.
 
 Beside the timed steps, rank 0 of a 1-GPU run also reports
-  roofline      the kernel's algorithmic bytes / its hipEvent-timed duration against 8 TB/s,
-                its line-request rate against the random-64-B-gather ceiling measured live on a
-                buffer of the table's size (kma_gather_bench), and the PMC traffic per launch
-                from profiles/ (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, guide corrections);
+  roofline      the dominant kernel's HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE
+                passes of this build, committed under profiles/, calibrated per the guide) over
+                its hipEvent-timed duration against 8 TB/s (`achieved`, `frac`); beside it the
+                SURVEY §8(d) algorithmic equivalent (64 B per probed window + 1 B per residue,
+                `alg_equiv_GBps`) and the fabric line-request rate against the random-64-B
+                ceiling measured live on a buffer of the table's size (kma_gather_bench);
   e2e           the host entry point kma_annotate_proteins on the same batch from host memory
                 (H2D + kernel + D2H through pinned staging): the PCIe-inclusive rate;
   cpu_baseline  the C restatement of the reference loop (oracle/kma_oracle.c) on all the box's
@@ -56,8 +58,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 BYTES_PER_LOOKUP = 64  # one 64-byte bucket line per probed window
 MALL_BYTES = 256 << 20  # Infinity Cache: a table below it is served on-die (MI355X_MICROARCH.md)
 GATHER_BIN = os.path.join(ROOT, "kmers.anno_amd", "build", "kma_gather_bench")
-# Per-launch PMC traffic of the dominant kernels (scripts/gpu_traffic.sh + traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
+# Per-launch PMC traffic of the dominant kernels of this build (scripts/gpu_traffic.sh +
+# scripts/traffic_summary.py).
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
 METRIC = "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs roofline"
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
@@ -205,9 +208,8 @@ def pmc_traffic(workload: str, kernel: str):
 
 
 def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
-    """Signature table built on rank 0's GPU (size-derived layout; rebuilt flat if the
-    minimizer layout is crowded and flat halves the displaced keys — the library's own
-    creator rule), replicated over RCCL (xGMI) to the other ranks."""
+    """Signature table built on rank 0's GPU with the library creators' layout rule
+    (kmeranno.choose_layout), replicated over RCCL (xGMI) to the other ranks."""
     nb = kmeranno.buckets_for(t_size, load_factor)
     slots = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int64, device=dev)
     layout = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -216,6 +218,8 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
         status = torch.zeros(4, dtype=torch.int32, device=dev)
         keys = torch.from_numpy(keys_np.view(np.int64)).to(dev)
         fids = torch.from_numpy(fids_np.view(np.int32)).to(dev)
+
+        times = {}
 
         def build(m):
             tb, te = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -227,17 +231,12 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
             torch.cuda.synchronize()
             st = status.cpu().numpy().astype(np.int64)
             assert st[0] == 0, "table full"
-            return st, tb.elapsed_time(te)
+            times[m] = tb.elapsed_time(te)
+            return st
 
-        m = kmeranno.layout_for(K, nb)
-        st, ms = build(m)
-        forced = os.environ.get("KMA_MINIMIZER", "") in ("0", "6", "7")  # A/B runs: keep it
-        if m and not forced and (st[3] > 0.15 * st[1] or st[2] > 32):
-            sf, msf = build(0)
-            if 2 * sf[3] < st[3] or (st[2] > 32 and 2 * sf[2] < st[2]):
-                m, st, ms = 0, sf, msf
-            else:
-                st, ms = build(m)
+        # the library creators' rule (size rule, then m = 7 / flat rebuilds by measurement)
+        m, st = kmeranno.choose_layout(K, nb, build)
+        ms = times[m]
         layout.fill_(m)
         log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 8 * kmeranno.bucket_slots() / 2**20:.0f} MiB), "
             f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
@@ -291,71 +290,53 @@ def timed(step, ws, args, world, stream, dev, before=None, after=None):
 
 
 def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
-    """The dominant kernel's line: algorithmic bytes / duration against the 8 TB/s spec, and the
-    line-request rate against the live random-gather ceiling of a buffer of the table's size."""
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, reqs, src = pmc_traffic(workload, kernel.split(" (")[0])
+    """The dominant kernel's line. achieved = the HBM bytes it moves per launch (PMC counters
+    of this build, committed in profiles/) / its hipEvent-timed mean duration, against the
+    8 TB/s spec; when no counter summary names the kernel, the algorithmic bytes stand in (and
+    achieved_basis says so). The SURVEY §8(d) algorithmic figure (one 64-B line per probed
+    window + the input) is kept as alg_equiv_GBps: minimizer buckets let consecutive windows
+    share a line, so it exceeds the bytes actually moved and its ratio to the random-line
+    ceiling can pass 1. The request-rate view: fabric line requests per launch (PMC) per
+    second against the live random-64-B ceiling."""
+    name = kernel.split(" (")[0]
+    traffic, reqs, src = pmc_traffic(workload, name)
+    alg_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    if traffic:
+        achieved, basis = traffic / (kernel_ms * 1e-3) / 1e9, (
+            f"PMC bytes per launch ({src}) / hipEvent kernel time")
+    else:
+        achieved, basis = alg_gbps, "algorithmic bytes (no PMC summary for this kernel)"
     ceil = gather_ceiling(table_bytes) if live else None
     out = {"bound": "hbm" if table_bytes > MALL_BYTES else "infinity-cache",
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "achieved_basis": basis,
            "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "
                               "(MI355X_MICROARCH.md HBM section; Infinity-Cache hits included)")
            if src else None,
-           "kernel": kernel, "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
-           "alg_bytes_rule": kind, "windows_per_launch": windows,
-           "table_bytes": table_bytes}
+           "kernel": kernel, "kernel_ms": kernel_ms,
+           "alg_equiv_GBps": alg_gbps, "alg_bytes_per_launch": alg_bytes,
+           "alg_bytes_rule": kind, "windows_per_launch": windows, "table_bytes": table_bytes}
+    if reqs:
+        out["line_requests_per_launch"] = reqs
+        out["line_requests_per_window"] = reqs / windows
     if ceil:
         out["measured_random_64B_ceiling"] = {"lines_per_s": ceil["lines_per_s"],
                                               "GBps": ceil["GBps"], "buffer_MiB":
                                               ceil["buffer_MiB"], "inflight": ceil["inflight"]}
-        out["windows_per_s_frac_of_ceiling"] = windows / (kernel_ms * 1e-3) / ceil["lines_per_s"]
+        out["alg_windows_per_s_vs_ceiling"] = windows / (kernel_ms * 1e-3) / ceil["lines_per_s"]
         if reqs:
             rate = reqs / (kernel_ms * 1e-3)
-            out["line_requests_per_launch"] = reqs
             out["line_requests_per_s"] = rate
             out["requests_frac_of_ceiling"] = rate / ceil["lines_per_s"]
     return out
 
 
 def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
-    """Roofline of the protein path's dominant kernel (rank 0's shard; times are max over ranks).
-    Direct path (one kernel): one 64-B bucket line per window + 1 B per residue,
-    against the live random-64-B-request ceiling. Partitioned path: each phase's streamed bytes
-    per launch (algorithmic, from the record / result formats: 8-B records and 4-B results per
-    window; the table read once by the region sweep) against the 8 TB/s HBM spec; every phase's
-    rate is listed, the dominant one is the headline."""
-    if "annotate_kernel" in ph and len(ph) == 1:
-        return roofline("windows x 64 B + residues", workload,
-                        f"annotate_kernel<{K}, {m}, 8> (direct path: probe + sets + vote)",
-                        ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP + n_res, table_bytes,
-                        n_win, live=live)
-    alg = {"partition_kernel": (n_res + 8 * n_win, "residues + 8-B record per window"),
-           "probe_regions_kernel": (12 * n_win + table_bytes,
-                                    "8-B record + 4-B result per window + the table once"),
-           "vote_chunks_kernel": (4 * n_win, "4-B result per window")}
-    per = {k: {"ms": ph[k], "alg_bytes": b, "rule": r, "GBps": b / (ph[k] * 1e-3) / 1e9}
-           for k, (b, r) in alg.items() if ph.get(k)}
-    dom = max(per, key=lambda k: per[k]["ms"])
-    name = {"partition_kernel": f"partition_kernel<{K}, {m}>",
-            "probe_regions_kernel": f"probe_regions_kernel<{K}, {m}>",
-            "vote_chunks_kernel": "vote_chunks_kernel"}[dom]
-    traffic, reqs, src = pmc_traffic(workload, name)
-    out = {"bound": "hbm", "achieved": per[dom]["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": per[dom]["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
-           "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "
-                              "(MI355X_MICROARCH.md HBM section)") if src else None,
-           "kernel": name + " (partitioned path)", "kernel_ms": per[dom]["ms"],
-           "alg_bytes_per_launch": per[dom]["alg_bytes"], "alg_bytes_rule": per[dom]["rule"],
-           "windows_per_launch": n_win, "table_bytes": table_bytes, "phases": per}
-    if live:
-        ceil = gather_ceiling(table_bytes)
-        if ceil:
-            total = sum(ph.values())
-            out["measured_random_64B_ceiling"] = {k: ceil[k] for k in
-                                                  ("lines_per_s", "GBps", "buffer_MiB", "inflight")}
-            out["windows_per_s_vs_random_ceiling"] = n_win / (total * 1e-3) / ceil["lines_per_s"]
-    return out
+    """Roofline of the protein path (one kernel; rank 0's shard, times max over ranks)."""
+    return roofline("windows x 64 B + residues", workload,
+                    f"annotate_kernel<{K}, {m}, 8> (probe + sets + vote)",
+                    ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP + n_res, table_bytes, n_win,
+                    live=live)
 
 
 def bench_contigs(args, rank, world, dev, stream, sp):
@@ -383,7 +364,7 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                          0, 0, sp)
 
     elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev)
-    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["scan_emit"]
+    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["emit"]
     n_hits = int(d_nh.item())
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
@@ -402,7 +383,7 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                        "parallelism": f"genome-shard x{world}, table replicated (RCCL broadcast)"},
             "seqs_per_s": n_contig * args.steps * world / elapsed,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
+            "phases_ms": {"probe_and_scan": k_ms, "emit": rest_ms},
             # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 8 B per staged hit
             "roofline": roofline("probed windows x 64 B + bases + hits x 8 B", "c3",
                                  f"{kname} (6-frame translate + 2 probes per base)", k_ms,
@@ -523,7 +504,6 @@ def main():
             "seqs_per_s": seqs * args.steps / elapsed,
             "called_per_batch": called,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "protein_path": "partitioned" if "probe_regions_kernel" in ph else "direct",
             "phases_ms": ph,
         }
         out["roofline"] = protein_roofline(ph, args.workload, m, n_win, n_res, table.info.bytes,

@@ -254,8 +254,7 @@ struct kma_workspace {
   uint64_t* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
   uint64_t* d_cprefix = nullptr;
-  void* d_ctemp = nullptr;
-  size_t ctemp_bytes = 0;
+  uint32_t* d_cdone = nullptr;  // the probe grid's finished-block counter (0 between calls)
   uint64_t contig_cap = 0;  // bases
   // Per-phase timing (kma_workspace_timing): a ring of calls, each kMaxEv events (phase i runs
   // from event i to event i + 1) and its phase names.
@@ -453,12 +452,11 @@ int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m, uint32_
   return KMA_OK;
 }
 
-// Table from device-resident keys/fids on `device` (n rows; fids already checked). The layout
-// is the size-derived minimizer layout; when that one is crowded (more than kMaxDisplaced of
-// the keys past their home bucket, or a chain longer than kMaxChain: keys piling onto few
-// minimizers) the table is also built flat and the flat one kept if it halves the displaced
-// keys or the longest chain. At high load factors both layouts displace many keys and the
-// minimizer one stays. KMA_MINIMIZER forces a layout.
+// Table from device-resident keys/fids on `device` (n rows; fids already checked), laid out by
+// the size rule and then by measurement (kma_internal.h, kRetryDisplaced / kMaxDisplaced):
+// an m = 6 table with many displaced keys is rebuilt with m = 7 (kept if it displaces fewer),
+// a still crowded minimizer table is rebuilt flat (kept if that halves the displaced keys or
+// the longest chain). KMA_MINIMIZER forces a layout.
 int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, int k,
                             int device, double lf, const uint8_t lut[256], kma_table** out) {
   const uint64_t nb = buckets_for_k(n, lf, k);
@@ -486,22 +484,35 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
   uint64_t* d_slots = nullptr;
   uint32_t st[4] = {};
   if (int rc = build(m, &d_slots, st)) return rc;
-  const bool crowded = st[3] > kma::kMaxDisplaced * std::max<uint32_t>(st[1], 1) ||
-                       st[2] > kma::kMaxChain;
-  if (m != 0 && crowded && forced_layout() < 0) {
-    uint64_t* d_flat = nullptr;
-    uint32_t sf[4] = {};
-    if (int rc = build(0, &d_flat, sf)) {
+  auto displaced = [](const uint32_t s[4]) { return (double)s[3] / std::max<uint32_t>(s[1], 1); };
+  // Replace the current table (slots, stats, m) by a build with layout m2 when keep() says so.
+  auto try_layout = [&](int m2, bool (*keep)(const uint32_t*, const uint32_t*)) -> int {
+    uint64_t* d2 = nullptr;
+    uint32_t s2[4] = {};
+    if (int rc = build(m2, &d2, s2)) {
       (void)hipFree(d_slots);
       return rc;
     }
-    const bool better = 2ull * sf[3] < st[3] || (st[2] > kma::kMaxChain && 2 * sf[2] < st[2]);
-    (void)hipFree(better ? d_slots : d_flat);
+    const bool better = keep(st, s2);
+    (void)hipFree(better ? d_slots : d2);
     if (better) {
-      d_slots = d_flat;
-      std::memcpy(st, sf, sizeof st);
-      m = 0;
+      d_slots = d2;
+      std::memcpy(st, s2, sizeof st);
+      m = m2;
     }
+    return KMA_OK;
+  };
+  const int m6 = std::min(k, 6), m7 = std::min(k, 7);
+  if (forced_layout() < 0) {
+    if (m == m6 && m6 != m7 && displaced(st) > kma::kRetryDisplaced)
+      if (int rc = try_layout(m7, [](const uint32_t* a, const uint32_t* b) { return b[3] < a[3]; }))
+        return rc;
+    const bool crowded = displaced(st) > kma::kMaxDisplaced || st[2] > kma::kMaxChain;
+    if (m != 0 && crowded)
+      if (int rc = try_layout(0, [](const uint32_t* a, const uint32_t* b) {
+            return 2ull * b[3] < a[3] || (a[2] > kma::kMaxChain && 2 * b[2] < a[2]);
+          }))
+        return rc;
   }
   kma_table* t = new_table(device, k, m, nb, lut);
   if (int rc = add_replica(t, device, d_slots, true)) {
@@ -766,13 +777,13 @@ void free_protein_scratch(kma_workspace* ws) {
 }
 
 void free_contig_scratch(kma_workspace* ws) {
-  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix, ws->d_ctemp})
+  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix,
+                  (void*)ws->d_cdone})
     if (p) (void)hipFree(p);
   ws->d_cstage = nullptr;
   ws->d_ccounts = nullptr;
   ws->d_cprefix = nullptr;
-  ws->d_ctemp = nullptr;
-  ws->ctemp_bytes = 0;
+  ws->d_cdone = nullptr;
   ws->contig_cap = 0;
 }
 
@@ -801,6 +812,7 @@ kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace*
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
   a.prefix = ws->d_cprefix;
+  a.done = ws->d_cdone;
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
@@ -833,7 +845,7 @@ struct PhaseClock {
 };
 
 const char* const kDirectPhases[] = {"annotate_kernel"};
-const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
+const char* const kContigPhases[] = {"contigs_probe_kernel", "emit"};
 
 // Proteins per annotate_kernel block: 4 (KMA_BLOCK_PROTEINS=1..8 overrides, read per call).
 // Measured on MI355X (profiles/r02f_block_proteins.log): c2 65.1 / 65.5 / 65.6 / 73.9 us and c5
@@ -1033,13 +1045,11 @@ int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   free_contig_scratch(ws);
   const uint64_t nb = contig_blocks(n_bases);
-  size_t tb = 0;
-  KMA_HIP(kma::launch_contig_scan(nullptr, nullptr, nb, nullptr, &tb, nullptr));
   KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * 8));
   KMA_HIP(hipMalloc(&ws->d_ccounts, nb * 4));
   KMA_HIP(hipMalloc(&ws->d_cprefix, nb * 8));
-  KMA_HIP(hipMalloc(&ws->d_ctemp, tb ? tb : 1));
-  ws->ctemp_bytes = tb;
+  KMA_HIP(hipMalloc(&ws->d_cdone, 4));
+  KMA_HIP(hipMemset(ws->d_cdone, 0, 4));
   ws->contig_cap = nb * kma::kContigTile;
   return KMA_OK;
 }
@@ -1136,7 +1146,7 @@ int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kern
   const char* names[KMA_MAX_PHASES];
   int np = 0;
   if (int rc = kma_workspace_phases_read(ws, n_calls, &np, ms, names)) return rc;
-  // contigs: (probe, scan + emit); proteins: the whole path (every phase), nothing after it
+  // contigs: (probe + block-count scan, emit); proteins: the whole path (every phase), nothing after it
   const bool contigs = np > 0 && names[0] == kContigPhases[0];
   *kernel_ms = 0;
   *rest_ms = 0;
@@ -1247,8 +1257,6 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
   const uint64_t nb = contig_blocks(n_bases);
   KMA_HIP(kma::launch_contigs_probe(a, nb, s));
   KMA_HIP(clk.mark());
-  size_t tb = ws->ctemp_bytes;
-  KMA_HIP(kma::launch_contig_scan(ws->d_ccounts, ws->d_cprefix, nb, ws->d_ctemp, &tb, s));
   const int rc = enqueue_contig_emit(a, d_hits, cap, d_n_hits, s);
   if (rc == KMA_OK) KMA_HIP(clk.mark());
   return rc;
@@ -1312,8 +1320,6 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
     a.strict_pass = 2;  // keep keys with exactly one location
   }
   KMA_HIP(kma::launch_contigs_probe(a, nb, s));
-  size_t stb = c->ws->ctemp_bytes;
-  KMA_HIP(kma::launch_contig_scan(c->ws->d_ccounts, c->ws->d_cprefix, nb, c->ws->d_ctemp, &stb, s));
   if (!out_hits) {  // pass 1: count (and tally)
     if (int rc = enqueue_contig_emit(a, nullptr, 0, d_n, s)) return rc;
     KMA_HIP(c->h_out.reserve(16 + tb));

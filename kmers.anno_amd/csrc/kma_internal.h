@@ -170,24 +170,27 @@ __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32
 // Layout (minimizer length m, 0 = flat) of a table of n_buckets buckets for K-mers. Keys
 // sharing a minimizer share a bucket, so the m-mer space must stay large against the table,
 // while consecutive windows share their minimizer (and a request) with probability
-// 1 - 2/(K - m + 2): 1/2 for m = 6, 1/3 for m = 7. Simulated home-bucket loads of uniform
-// keys at load factor 0.5: 8-slot buckets leave 1.8% of 1e7 keys and 12% of
-// 1e8 keys past their home bucket at m = 6, 1.0% / 2.5% at m = 7; 16-slot buckets 0.25% / 4.2%
-// at m = 6. With paired homes and hashed chains (above) m = 6's displaced keys cost short walks:
-// at c5 (10^8 keys, 2^24.6 buckets) m = 6 displaces 7.7% (chain 10) and takes 4.28 ms against
-// m = 7's 4.50-4.54 (2.4% displaced; two runs each, profiles/r02t_final/layout_ab.log): its 12%
-// fewer line requests win. So m = 6 up to kMinimizer6Buckets buckets (134M keys at load factor
-// 0.5; 20^6 = 64M 6-mers then cover ~2 minimizers per bucket pair), else 7 (m <= K).
-// KMA_MINIMIZER=0|6|7 in the environment forces a layout (read per call: tests run every layout
-// in one process). Defined in kma_abi.cpp.
+// 1 - 2/(K - m + 2): 1/2 for m = 6, 1/3 for m = 7. The size rule: m = 6 up to
+// kMinimizer6Buckets buckets (134M keys at load factor 0.5), else 7 (m <= K); KMA_MINIMIZER=
+// 0|6|7 in the environment forces a layout (read per call: tests run every layout in one
+// process). Defined in kma_abi.cpp.
 constexpr uint64_t kMinimizer6Buckets = kSlotsPerBucket == 16 ? (1ull << 24) : (1ull << 25);
 // Wide tables (4 slots per bucket): the same key count, i.e. twice the buckets.
 constexpr uint64_t kMinimizer6BucketsWide = 1ull << 26;
 int minimizer_len(int k, uint64_t n_buckets);
-// The table creators also build a minimizer-layout table flat when more than this fraction of
-// its keys were displaced past their home bucket, or a chain is longer than kMaxChain buckets,
-// and keep the flat one if it halves either (kma_abi.cpp; uniform keys at load factor 0.5
-// displace 2-4% under m = 6/7 and ~1% flat; keys sharing minimizers, nearly all).
+// The creators then measure the table they built (kma_abi.cpp create_from_device_keys): every
+// displaced key costs a dependent round trip when it is looked up, and false filter hits cost
+// the misses the same. Measured at c5 (10^8 keys, paired homes, hashed chains; round 3 sweep,
+// profiles/r03_layout/): m = 6 / m = 7 / flat take 4.12 / 4.11 / 5.57 ms at load factor 0.5
+// (7.7 / 2.4 / 0.9% displaced), 5.82 / 5.00 / 5.95 ms at 0.75 (17.1 / 9.4 / 6.1%) and
+// 10.0 / 7.74 / 7.72 ms at 0.9 (24.5 / 16.8 / 13.1%): m = 6's 12% fewer line requests pay off
+// only while few keys are displaced. So:
+//   1. an m = 6 table with more than kRetryDisplaced of its keys displaced is also built with
+//      m = 7, and the one with fewer displaced keys kept;
+//   2. a minimizer table still crowded (more than kMaxDisplaced displaced, or a chain longer
+//      than kMaxChain buckets: keys piling onto few minimizers) is also built flat, and the flat
+//      one kept if it halves the displaced keys or the longest chain.
+constexpr double kRetryDisplaced = 0.10;
 constexpr double kMaxDisplaced = 0.15;
 constexpr uint32_t kMaxChain = 32;
 
@@ -214,6 +217,9 @@ constexpr uint32_t kMaxChain = 32;
 constexpr int kProbeWin = KMA_PROBE_WIN;
 constexpr int kBlockProteins = KMA_BLOCK_PROTEINS;
 constexpr int kSetPool = KMA_SET_POOL;
+#ifndef KMA_LANE_PERM
+#define KMA_LANE_PERM 0
+#endif
 #ifndef KMA_CHAIN_Q
 #define KMA_CHAIN_Q 384
 #endif
@@ -258,7 +264,9 @@ struct ContigArgs {
   int32_t mlen;
   uint64_t* staging;           // n_blocks x kContigTile*2 packed hits (relative position)
   uint32_t* block_counts;      // n_blocks
-  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (emit pass)
+  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (the probe's last
+                               // block writes it; the emit pass reads it)
+  uint32_t* done;              // blocks finished (0 between calls; the last block resets it)
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order
@@ -309,8 +317,6 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
-hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n,
-                              void* temp, size_t* temp_bytes, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 // Peg-kmer singleton table (KmerReference.countPegKmers + CountMap.getSingletons): every
 // window i < L-K without 'X' of every peg -> (key or 0, peg index) per residue position; sort;

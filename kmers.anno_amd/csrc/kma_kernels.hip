@@ -251,6 +251,15 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   constexpr int U = kProbeWin;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
+  // The lane's window within each 256-window slice. KMA_LANE_PERM: quad q's member p takes
+  // window 16 p + q of its wave, so that load instruction r (member r of every quad) reads the
+  // buckets of 16 consecutive windows — windows that share a minimizer then share a line
+  // inside one instruction.
+#if KMA_LANE_PERM
+  const uint32_t tw = (uint32_t)(wave * 64 + 16 * (lane & 3) + (lane >> 2));
+#else
+  const uint32_t tw = (uint32_t)t;
+#endif
   // wave 0: the proteins' offsets (issued first); every wave: the span start (scalar)
   const uint64_t beg_raw = wave == 0 && lane <= (int)np ? a.offsets[p0 + lane] : 0u;
   const uint64_t o0 = a.offsets[0];
@@ -267,7 +276,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     const uint64_t lim = a.n_residues - span_lo;
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = j * 256u + t;
+      const uint32_t x = j * 256u + tw;
       ww[j] = window_words(res, (x < lim ? x : 0u) + mis);
     }
   }
@@ -294,14 +303,30 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       sm.pcnt[lane] = 0u;
     }
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {  // greedy: LDS pool in protein order, workspace memory past it
+    if (lane == 0) {  // LDS pool for the sets; workspace memory for those that do not fit
+      uint32_t sum = 0;
+      for (int p = 0; p < P; ++p) sum += sm.pcap[p];
       uint32_t top = 0;
-      for (int p = 0; p < P; ++p) {
-        const uint32_t cap = sm.pcap[p];
-        const bool fits = top + cap <= (uint32_t)kSetPool;
-        sm.pset[p] = fits ? top : kGlobalSet;
-        if (!fits) sm.pcap[p] = 2u * sm.pwin[p];  // <= 2 entries per residue of its region
-        top += fits ? cap : 0u;
+      if (sum <= (uint32_t)kSetPool) {  // the usual case: every set in LDS, in protein order
+        for (int p = 0; p < P; ++p) {
+          sm.pset[p] = top;
+          top += sm.pcap[p];
+        }
+      } else {
+        // First fit by decreasing size (fewer windows left to workspace sets than protein
+        // order: 1.9% vs 2.4% of c5's windows in a simulation of its length distribution).
+        uint32_t done = 0;
+        for (int it = 0; it < P; ++it) {
+          int best = -1;
+          for (int p = 0; p < P; ++p)
+            if (!(done >> p & 1u) && (best < 0 || sm.pcap[p] > sm.pcap[best])) best = p;
+          done |= 1u << best;
+          const uint32_t cap = sm.pcap[best];
+          const bool fits = top + cap <= (uint32_t)kSetPool;
+          sm.pset[best] = fits ? top : kGlobalSet;
+          if (!fits) sm.pcap[best] = 2u * sm.pwin[best];  // <= 2 entries per residue
+          top += fits ? cap : 0u;
+        }
       }
       sm.chain_q[0][0] = top;  // pool entries in use (read before the queues are)
     }
@@ -353,7 +378,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     uint32_t klo[U], khi[U], bk[U];  // bk: protein << kBucketBits | home bucket, or kNone
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = x0 + j * 256u + t;
+      const uint32_t x = x0 + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
       uint32_t pbp = pb[0], pwp = pw[0];
 #pragma unroll
@@ -389,7 +414,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     // flight, vmcnt counts in order).
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = x0 + stride + j * 256u + t;
+      const uint32_t x = x0 + stride + j * 256u + tw;
       ww[j] = window_words(res, (x < span ? x : 0u) + mis);
     }
     uint32_t word[U];
@@ -420,7 +445,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const bool pend = w == 0x80000000u;
 #endif
       const uint64_t m = __ballot(pend);
-      if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + t;
+      if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + tw;
       cn += (uint32_t)__popcll(m);
     }
     if (cn > (uint32_t)(kChainQ - 64 * U)) chain_flush();
@@ -512,7 +537,8 @@ __device__ __forceinline__ uint32_t base2(uint8_t c) {  // T,C,A,G -> 0..3; othe
 // loads of the protein path (both probes' 8 dwordx4 of a lane in flight before any compare,
 // DPP quad match); the tile's contigs are found once (two wave-parallel searches) and their
 // offsets cached in LDS, so a position's contig costs no global loads. Hits are compacted per
-// block in canonical order (position, '+' before '-'); a scan + emit pass orders the blocks.
+// block in canonical order (position, '+' before '-'); the grid's last block scans the block
+// counts and an emit pass writes every block's hits at its offset.
 constexpr int kOffCache = 64;
 
 // contig_of by a whole wave, 64 candidates per dependent load: the largest c < n with
@@ -533,6 +559,32 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
     lo = nlo;
   }
   return lo;
+}
+
+// Exclusive prefix of n block counts by one block of 256 threads (the probe grid's last block):
+// thread t sums a contiguous chunk (agent-scope loads: the counts were written by blocks on
+// other XCDs), a block scan of the 256 sums, then each thread writes its chunk's prefixes.
+__device__ __forceinline__ void scan_block_counts(const uint32_t* counts, uint64_t* prefix,
+                                                  uint32_t n) {
+  __shared__ uint64_t part[256];
+  const uint32_t t = threadIdx.x, per = (n + 255) / 256;
+  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
+  uint64_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i)
+    sum += __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan of the sums
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - sum;  // exclusive
+  for (uint32_t i = lo; i < hi; ++i) {
+    prefix[i] = run;
+    run += __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int K, int M>
@@ -602,16 +654,24 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   __syncthreads();
   KMA_CLK(2);  // translated
 
-  // Each lane owns positions t + 256 h (h < kContigPos): both windows of every one of them are
-  // probed with all their dwordx4 in flight before any compare.
+  // Each lane owns positions tp + 256 h (h < kContigPos): both windows of every one of them are
+  // probed with all their dwordx4 in flight before any compare. KMA_LANE_PERM: quad q's member
+  // p takes position 16 p + q of its wave, so that one load instruction covers 16 consecutive
+  // positions (same-frame windows 3 apart share minimizers, hence lines); the results go back
+  // to position order through LDS before the compaction.
   constexpr int CP = kContigPos;
+#if KMA_LANE_PERM
+  const uint32_t tp = (uint32_t)(wave * 64 + 16 * (lane & 3) + (lane >> 2));
+#else
+  const uint32_t tp = (uint32_t)t;
+#endif
   uint32_t contig[CP];
   int64_t xs[CP], lens[CP];
   uint64_t key[CP][2];
   uint32_t bk[CP][2];
 #pragma unroll
   for (int h = 0; h < CP; ++h) {
-    const uint32_t tt = t + 256u * h;
+    const uint32_t tt = tp + 256u * h;
     const uint64_t g = base + r0 + tt;
     contig[h] = c_lo;
     int64_t x = 0, len = 0;
@@ -703,6 +763,24 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   (void)xs;
   (void)lens;
   KMA_CLK(4);  // matched (chain walks done)
+#if KMA_LANE_PERM
+  {  // back to position order: lane t takes position t's verdicts
+    __shared__ uint32_t xv[CP][2][256];
+#pragma unroll
+    for (int h = 0; h < CP; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xv[h][j][tp] = hit[h][j] ? fid[h][j] + 1u : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < CP; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t v = xv[h][j][t];
+        hit[h][j] = v != 0u;
+        fid[h][j] = v - 1u;
+      }
+  }
+#endif
   // Block-local compaction in canonical order (position, '+' before '-'): positions of the
   // first 256 before those of the next.
   uint64_t bp[CP], bm[CP];
@@ -726,7 +804,20 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     if (hit[h][0]) st[o++] = (r << 25) | fid[h][0];               // strand bit 24 = 0: '+'
     if (hit[h][1]) st[o] = (r << 25) | (1ull << 24) | fid[h][1];  // '-'
   }
-  if (t == 0) a.block_counts[blockIdx.x] = total;
+  // The last block to finish scans the block counts (the emit pass's offsets): no scan
+  // kernels between probe and emit (they were ~10 us of a ~115 us c3 step).
+  __shared__ uint32_t last;
+  if (t == 0) {
+    a.block_counts[blockIdx.x] = total;
+    __threadfence();  // the count is visible device-wide before the ticket
+    last = atomicAdd(a.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    scan_block_counts(a.block_counts, const_cast<uint64_t*>(a.prefix), gridDim.x);
+    if (t == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   KMA_CLK(5);
   KMA_CLK_HW();
 }
@@ -948,11 +1039,6 @@ struct ContigLaunch {
 
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
   return dispatch_km<ContigLaunch>(a.k, a.mlen, a, n_blocks, stream);
-}
-
-hipError_t launch_contig_scan(const uint32_t* counts, uint64_t* prefix, uint64_t n, void* temp,
-                              size_t* temp_bytes, hipStream_t stream) {
-  return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, counts, prefix, (int)n, stream);
 }
 
 hipError_t launch_peg_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_peg,

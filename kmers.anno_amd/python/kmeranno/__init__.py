@@ -341,6 +341,40 @@ def layout_for(k: int, n_buckets: int) -> int:
     return int(load().kma_table_layout_for(k, n_buckets))
 
 
+# The creators' layout rule by measurement (kma_internal.h kRetryDisplaced / kMaxDisplaced /
+# kMaxChain; kma_abi.cpp create_from_device_keys).
+RETRY_DISPLACED, MAX_DISPLACED, MAX_CHAIN = 0.10, 0.15, 32
+
+
+def choose_layout(k: int, n_buckets: int, build):
+    """The library creators' layout choice for hosts that build tables on the device
+    themselves (kma_table_build_device into their own buffer, e.g. one RCCL broadcasts):
+    build(m) builds the table with layout m into the caller's buffer and returns its status
+    {full, entries, longest chain, displaced}. Returns (m, status); the kept layout is the one
+    built last. KMA_MINIMIZER forces the size rule's answer."""
+    m = layout_for(k, n_buckets)
+    st = build(m)
+    if os.environ.get("KMA_MINIMIZER", "") in ("0", "6", "7"):
+        return m, st
+
+    def disp(s):
+        return s[3] / max(s[1], 1)
+    m6, m7 = min(k, 6), min(k, 7)
+    if m == m6 and m6 != m7 and disp(st) > RETRY_DISPLACED:
+        s2 = build(m7)
+        if s2[3] < st[3]:
+            m, st = m7, s2
+        else:
+            st = build(m)
+    if m != 0 and (disp(st) > MAX_DISPLACED or st[2] > MAX_CHAIN):
+        s2 = build(0)
+        if 2 * s2[3] < st[3] or (st[2] > MAX_CHAIN and 2 * s2[2] < st[2]):
+            m, st = 0, s2
+        else:
+            st = build(m)
+    return m, st
+
+
 def build_device(d_slots: int, n_buckets: int, d_winner: int, d_keys: int, d_fids: int, n: int,
                  d_status: int, stream: int = 0, k: int = 8, layout: int = -1):
     """Device-resident table build; d_status (4 x u32) <- {full, entries, longest chain,

@@ -67,3 +67,27 @@ def test_table_layout_host_helper(native_lib, monkeypatch):
     assert kmeranno.layout_for(8, 1000) == 0
     monkeypatch.setenv("KMA_MINIMIZER", "7")
     assert kmeranno.layout_for(8, 1000) == 7
+
+
+def test_choose_layout_rule():
+    """kmeranno.choose_layout mirrors the creators' rule (kma_abi.cpp create_from_device_keys)
+    on the round-3 c5 sweep's build statistics {full, entries, longest chain, displaced}: m = 6
+    kept at load factor 0.5, rebuilt m = 7 at 0.75 and 0.9 (flat halves neither), flat for keys
+    piling onto few minimizers; the kept layout is built last."""
+    import kmeranno
+    n = 99_821_868
+    sweep = {  # load factor -> layout -> status
+        0.5: {6: [0, n, 10, int(0.0770 * n)], 7: [0, n, 7, int(0.0239 * n)], 0: [0, n, 6, int(0.0086 * n)]},
+        0.75: {6: [0, n, 24, int(0.1706 * n)], 7: [0, n, 19, int(0.0936 * n)], 0: [0, n, 17, int(0.0607 * n)]},
+        0.9: {6: [0, n, 47, int(0.2449 * n)], 7: [0, n, 39, int(0.1675 * n)], 0: [0, n, 38, int(0.1309 * n)]},
+        "adv": {6: [0, 1506982, 290, 1490000], 7: [0, 1506982, 145, 1012000], 0: [0, 1506982, 5, 13000]},
+    }
+    want = {0.5: 6, 0.75: 7, 0.9: 7, "adv": 0}
+    for case, st in sweep.items():
+        built = []
+
+        def build(m):
+            built.append(m)
+            return st[m]
+        m, s = kmeranno.choose_layout(8, 25_000_000, build)
+        assert m == want[case] and built[-1] == m and s == st[m], (case, built)

@@ -99,3 +99,34 @@ def test_kma_apply_errors(kma_bin, apply_inputs, tmp_path):
     assert r.returncode == 2
     r = subprocess.run([kma_bin, "frobnicate"], capture_output=True, text=True)
     assert r.returncode == 1 and "Invalid command frobnicate." in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [8, 10])
+def test_kma_contigs_report(kma_bin, oracle_c, small_gto, apply_inputs, tmp_path, k):
+    """`kma contigs` (6-frame kmers of every genome's contigs probed against a kmer database
+    whose last row sets K, as ApplyKmerProcessor.java:108 / KmerProcessor -K do) at K = 8 and
+    K = 10 (a wide table): every line equals the oracle's hit (KmerReference.java:157-203)."""
+    d, _, _, _ = apply_inputs
+    contigs = [c["dna"] for c in small_gto["contigs"]]
+    dna, off = oracle_c.pack_strings(contigs)
+    km, _, _, _, _ = oracle_c.contig_kmers(dna, off, 11, k)
+    rng = np.random.default_rng(k)
+    kmers = [bytes(r).decode() for r in km[rng.choice(len(km), 5000, replace=False)]]
+    roles = [f"R{i % 37}" for i in range(len(kmers))]
+    with open(tmp_path / "db.tbl", "w") as f:
+        f.writelines(f"{a}\t{b}\n" for a, b in zip(kmers, roles))
+    ids = {}
+    for r in roles:
+        ids.setdefault(r, len(ids))
+    inv = {v: r for r, v in ids.items()}
+    ct, lf, sd, fr, fid = oracle_c.annotate_contigs(
+        oracle_c.Table(kmers, [ids[r] for r in roles]), dna, off, 11, k)
+    gid, cids = small_gto["id"], [c["id"] for c in small_gto["contigs"]]
+    exp = ["genome_id\tcontig_id\tstrand\tleft\tright\tframe\trole"] + [
+        f"{gid}\t{cids[c]}\t{chr(s)}\t{l}\t{l + 3 * k - 1}\t{f}\t{inv[int(x)]}"
+        for c, l, s, f, x in zip(ct, lf, sd, fr, fid)]
+    out = subprocess.run([kma_bin, "contigs", str(tmp_path / "db.tbl"), str(d / "gtos")],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == exp and len(exp) > 5000

@@ -110,3 +110,23 @@ def test_hash_annotate_rejects_bad_input(kma):
         kma.hash_annotate(np.frombuffer(b"ACDEFGHIKL", np.uint8), np.array([0, 10], np.uint64),
                           np.frombuffer(b"ACDEFGHIKL", np.uint8), np.array([0, 10], np.uint64),
                           min_sim=1.0)
+
+
+@pytest.mark.parametrize("slice_cand", ["1", "700", "5000"])
+def test_hash_scores_in_prototype_slices(kma, oracle_c, small_gto, monkeypatch, slice_cand):
+    """Candidates are sorted and run-length encoded in slices of whole prototypes (each below
+    hipcub's 2^31 element limit; KMA_HASH_SLICE lowers the slice size here): a slice's best
+    similarity replaces the running best only when strictly higher, so ties still go to the
+    earlier prototype (exact copies placed in different slices) and the result equals the
+    one-slice call and the oracle."""
+    rng = np.random.default_rng(21)
+    prots = [f["protein_translation"] for f in small_gto["features"]
+             if f.get("protein_translation")][:300]
+    protos = [_mut(rng, p, rng.uniform(0.1, 0.4)) for p in prots]
+    protos = protos[:150] + prots[:10] + protos[150:] + prots[:10]  # ties across slices
+    ref = _both(kma, oracle_c, prots, protos, 8, 0.0125)
+    monkeypatch.setenv("KMA_HASH_SLICE", slice_cand)
+    got = _both(kma, oracle_c, prots, protos, 8, 0.0125)
+    for a, b in zip(got, ref):
+        assert (a == b).all()
+    assert (got[0][:10] == np.arange(150, 160)).all() and (got[1][:10] == 1.0).all()

@@ -131,7 +131,10 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags):
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, flags)
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
         assert t.info.n_entries == ot.size
-        assert t.info.minimizer_len == {"auto": 6, "7": 7, "0": 0}[layout]
+        if layout != "auto":
+            assert t.info.minimizer_len == int(layout)
+        elif lf == 0.5:
+            assert t.info.minimizer_len == 6  # size rule, few displaced keys
         if lf == 0.9:
             assert t.info.max_probe >= 2 and t.info.n_displaced > 0
         fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, flags)
