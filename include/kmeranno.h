@@ -91,11 +91,12 @@ extern "C" {
  *   so key equality is exactly the String.equals of the reference's HashMap lookup.
  * Tables of K <= 8 ("narrow") keep the key's 40 bits, an overflow-filter bit and the fid in one
  * 8-byte slot (kma_bucket_slots() per bucket); tables of K = 9..12 ("wide": the projector's
- * -K, KmerProcessor.java:86-88) use 16-byte slots, four per 64-byte bucket. fid < 2^23.
+ * -K, KmerProcessor.java:86-88) use 16-byte slots, four per 64-byte bucket. fid < 2^22 (two
+ * bits of each slot's upper word form the bucket's overflow filter; ABI 3 allowed 2^23).
  * The protein path (kma_annotate_proteins*) takes narrow tables: apply's ProteinKmers keeps
  * K = 8 whatever the table holds (ApplyKmerProcessor.java:108 sets KmerReference's K only). */
 #define KMA_MAX_K 12
-#define KMA_MAX_FID ((1u << 23) - 1u)
+#define KMA_MAX_FID ((1u << 22) - 1u)
 
 
 typedef struct kma_table kma_table;         /* opaque: a signature table resident on one GPU */
@@ -190,7 +191,8 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
  *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7); builds on
  *                           `stream`; d_status (4 u32) receives {table full, entries, longest
  *                           chain, displaced keys} (a caller may rebuild with layout 0 when
- *                           displaced keys are many); fids are masked to 23 bits.
+ *                           displaced keys are many); fids are masked to 22 bits; keys that
+ *                           are 0 or not K-mer keys (>= 2^(5K)) are not stored.
  *   kma_table_wrap_device : adopt an already-built slot array of that layout (not owned).    */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
 uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k);
@@ -283,7 +285,7 @@ int kma_annotate_contigs_device(const kma_table* table, kma_workspace* ws, const
  * Built on the device (window packing, radix sort, singleton select, table build). Windows with
  * bytes outside A-Z / '*' never equal a translated contig kmer and are left out.
  * *n_windows (optional) receives the number of counted windows; table info n_entries the
- * singletons. n_peg < 2^23.
+ * singletons. n_peg <= 2^22.
  * kma_connect_pegs: every location of a singleton in the new genome's 6-frame contig kmer map
  * connected to its peg (framer.connect(pegId, loc)), i.e. hits with fid = peg index in the
  * canonical order of kma_annotate_contigs. strict != 0 applies KmerFactory.Strict

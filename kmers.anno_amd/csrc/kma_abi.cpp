@@ -535,7 +535,7 @@ int create_from_keys(const std::vector<uint64_t>& keys, const uint32_t* fids, ui
   if (lf <= 0) lf = 0.5;
   if (lf > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", lf);
   for (uint64_t r = 0; r < n; ++r)
-    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^23-1",
+    if (fids[r] > KMA_MAX_FID) return fail(KMA_E_INVALID, "fid %u of row %llu exceeds 2^22-1",
                                             fids[r], (unsigned long long)r);
   DeviceScope ds(device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d): %s", device,
@@ -1426,7 +1426,7 @@ int kma_peg_table_create(const uint8_t* residues, const uint64_t* offsets, uint3
   if (int rc = check_k(k)) return rc;
   if (load_factor <= 0) load_factor = 0.5;
   if (load_factor > 0.95) return fail(KMA_E_INVALID, "load factor %.3f > 0.95", load_factor);
-  if (n_peg > KMA_MAX_FID + 1u) return fail(KMA_E_INVALID, "more than 2^23 pegs");
+  if (n_peg > KMA_MAX_FID + 1u) return fail(KMA_E_INVALID, "more than 2^22 pegs");
   if (n_peg && (!residues || !offsets)) return fail(KMA_E_INVALID, "null argument");
   for (uint32_t s = 0; s < n_peg; ++s)
     if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);

@@ -92,8 +92,8 @@ __device__ __forceinline__ void scan_half(const uint4 (&q)[4], int half, uint64_
   }
 }
 
-// Walk the overflow chain after home bucket `b` (the key missed there and its overflow bit is
-// set): stop at the key or at the first bucket with an empty slot. Returns true on a hit, with
+// Walk the overflow chain after home bucket `b` (the key missed there and its filter positions
+// are set): stop at the key or at the first bucket with an empty slot. Returns true on a hit, with
 // the key's fid and slot id (bucket * slots + slot: the key's identity in this table). The
 // buckets can be loaded kWalkGroup at a time (all their dwordx4 in flight, then scanned in chain
 // order): ceil(n / kWalkGroup) dependent round trips for n buckets. Measured at c5 LF 0.9 (linear
@@ -152,24 +152,13 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 // One quad's verdict on a bucket it loaded cooperatively: lane `part` holds slots 2part and
 // 2part + 1 of each 64-byte half h of the bucket in v[h] (slots 8h + 2part, 8h + 2part + 1)
 // for key (kl, kh): fid + 1 of the matching slot in bits 0..23 (0 = not in this bucket), the
-// slot's index in the bucket from bit 24, and bit 31 = the key's overflow bit (chain walk
-// needed if there is no match). Keys are unique in a table, so at most one lane matches and OR
+// slot's index in the bucket from bit 24, and bit 31 - h set when the key's filter position h
+// is set (with no match and every position set, the chain must be walked: kWalkWord). Keys are unique in a table, so at most one lane matches and OR
 // is the reduction. Every lane of the quad must call it (DPP). Branch-free on purpose: a
 // short-circuit here lets the compiler split the 16-byte loads into a lazily loaded tail
 // behind a branch and a vmcnt(0).
 __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
                                                uint32_t kh, uint32_t part) {
-  if constexpr (kBucketHalves == 1) {  // 64-byte buckets (fewest registers)
-    const uint4 x = v[0];
-    const uint32_t m0 = (uint32_t)(x.x == kl) & (uint32_t)((x.y & kKeyHiMask) == kh);
-    const uint32_t m1 = (uint32_t)(x.z == kl) & (uint32_t)((x.w & kKeyHiMask) == kh);
-    uint32_t w = (m0 * ((x.y & kFidMask) + 1u)) | (m1 * ((x.w & kFidMask) + 1u));
-    w |= (m0 | m1) * ((2u * part + m1) << kSlotShift);  // slot within the bucket
-    const uint32_t ob = ovf_index(kl);
-    const uint32_t hi = (ob & 1u) ? x.w : x.y;
-    w |= (uint32_t)((ob >> 1) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
-    return quad_or(w);
-  }
   uint32_t w = 0;
 #pragma unroll
   for (int h = 0; h < kBucketHalves; ++h) {
@@ -178,22 +167,34 @@ __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], 
     w |= (m0 * ((v[h].y & kFidMask) + 1u)) | (m1 * ((v[h].w & kFidMask) + 1u));
     w |= (m0 | m1) * ((8u * h + 2u * part + m1) << kSlotShift);  // slot within the bucket
   }
-  const uint32_t ob = ovf_index(kl);  // slot 8h + 2p + (0|1) carries the key's filter bit
-  uint32_t hi = 0;
+  // filter position i: slot i / kFilterBits = 8 hh + 2 p + which, held by quad lane p
 #pragma unroll
-  for (int h = 0; h < kBucketHalves; ++h)
-    hi = (ob >> 3) == (uint32_t)h ? ((ob & 1u) ? v[h].w : v[h].y) : hi;
-  w |= (uint32_t)(((ob >> 1) & 3u) == part) & (hi >> 23) & 1u ? 0x80000000u : 0u;
+  for (int f = 0; f < kFilterBits; ++f) {
+    const uint32_t pos = filter_pos<kSlotsPerBucket>(kl, f), slot = pos / kFilterBits;
+    const uint32_t which = slot & 1u, lp = (slot >> 1) & 3u, hh = slot >> 3;
+    uint32_t hi = 0;
+#pragma unroll
+    for (int h = 0; h < kBucketHalves; ++h)
+      hi = hh == (uint32_t)h ? (which ? v[h].w : v[h].y) : hi;
+    const uint32_t b = (uint32_t)(lp == part) & (hi >> (kFidBits + pos % kFilterBits)) & 1u;
+    w |= b << (31 - f);
+  }
   return quad_or(w);
 }
 
 // Wide tables (K > 8, kma_internal.h): lane `part` of the quad holds slot `part` of the bucket
-// in v; same verdict word as match_part (fid + 1, slot from bit 24, bit 31 = overflow bit).
+// in v; same verdict word as match_part (fid + 1, slot from bit 24, filter positions set from
+// bit 31 down).
 __device__ __forceinline__ uint32_t match_wide(const uint4& v, uint32_t kl, uint32_t kh,
                                                uint32_t part) {
   const uint32_t m = (uint32_t)(v.x == kl) & (uint32_t)(v.y == kh);
   uint32_t w = m * ((v.z & kFidMask) + 1u) | m * (part << kSlotShift);
-  w |= (uint32_t)(ovf_index_wide(kl) == part) & (v.z >> 23) & 1u ? 0x80000000u : 0u;
+#pragma unroll
+  for (int f = 0; f < kFilterBits; ++f) {
+    const uint32_t pos = filter_pos<kWideSlots>(kl, f);
+    w |= ((uint32_t)(pos / kFilterBits == part) & (v.z >> (kFidBits + pos % kFilterBits)) & 1u)
+         << (31 - f);
+  }
   return quad_or(w);
 }
 

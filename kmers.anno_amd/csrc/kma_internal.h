@@ -13,13 +13,14 @@ namespace kma {
 // n_buckets buckets of kSlotsPerBucket slots of one u64 (8 slots = 64 bytes, the default; 16 =
 // 128 bytes, the KMA_BUCKET_SLOTS=16 build):
 //   low dword  = key bits 0..31            (never 0 for a valid key: codes are 1..31)
-//   high dword = key bits 32..39 << 24 | overflow bit << 23 | fid (23 bits)
+//   high dword = key bits 32..39 << 24 | filter bits << 22 | fid (22 bits)
 // A slot whose low dword is 0 is empty. A key lives in its home bucket or, if that was full,
-// in the next buckets of its probe chain (chain_bucket below: hashed steps by default). The overflow bits of a bucket (one
-// per slot, independent of the slot's key) form a filter of the keys homed there that live
-// further down the chain: overflow bit ovf_index(key) of the home bucket is set for each. A
-// lookup that misses its home bucket walks the chain only if its bit is set (then it stops at
-// the key or at a bucket with an empty slot). Every compare is a 32-bit operation.
+// in the next buckets of its probe chain (chain_bucket below: hashed steps by default). The
+// filter bits of a bucket (kFilterBits per slot, independent of the slot's key) form a Bloom
+// filter of the keys homed there that live further down the chain: each such key sets the
+// kFilterBits positions filter_pos(key, 0 ..) of its home bucket. A lookup that misses its home
+// bucket walks the chain only if all its positions are set (then it stops at the key or at a
+// bucket with an empty slot). Every compare is a 32-bit operation.
 // Bucket width: the chip serves random 128-byte lines at the same request rate as 64-byte ones
 // (kma_gather_bench quad2 vs quad: 5.43e10 lines/s both, profiles/r02_gather_shapes_b.jsonl),
 // but a 128-byte probe doubles the load instructions and the registers per window in flight:
@@ -33,9 +34,21 @@ static_assert(kSlotsPerBucket == 8 || kSlotsPerBucket == 16, "64- or 128-byte bu
 constexpr int kBucketBytes = kSlotsPerBucket * 8;
 constexpr int kBucketHalves = kBucketBytes / 64;  // 64-byte pieces a quad loads per bucket
 constexpr int kSlotBits = kSlotsPerBucket == 16 ? 4 : 3;
-constexpr uint32_t kFidMask = (1u << 23) - 1;
-constexpr uint32_t kOvfBit = 1u << 23;         // in the high dword
+// Filter bits per slot, each displaced key setting that many positions of its home bucket (two
+// of 16 at 8 slots): a miss walks a chain only when both its positions are set. Round 2 kept one
+// bit per slot (fid in 23 bits); at c5's m = 6 layout (7.7% of keys displaced) a miss found its
+// bit set in ~4% of home buckets, each a dependent round trip.
+#ifndef KMA_FILTER_BITS
+#define KMA_FILTER_BITS 2
+#endif
+constexpr int kFilterBits = KMA_FILTER_BITS;
+static_assert(kFilterBits == 1 || kFilterBits == 2, "one or two filter bits per slot");
+constexpr uint32_t kFidBits = 24 - kFilterBits;  // fid width (KMA_MAX_FID: 22 bits)
+constexpr uint32_t kFidMask = (1u << kFidBits) - 1;
 constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
+// The probe's verdict word when the home bucket misses and every filter position is set: the
+// key may live further down the chain (bit 31 - h = position h set).
+constexpr uint32_t kWalkWord = kFilterBits == 2 ? 0xC0000000u : 0x80000000u;
 // The probe's per-window verdict: fid + 1 in bits 0..23, slot in bucket at kSlotShift,
 // bit 31 = the key's overflow bit in its home bucket.
 constexpr uint32_t kWordFid = (1u << 24) - 1;
@@ -47,9 +60,14 @@ constexpr uint64_t kMaxBuckets = 1ull << (32 - kSlotBits);
 __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
   return ((uint64_t)((uint32_t)(key >> 32) << 24 | (fid & kFidMask)) << 32) | (uint32_t)key;
 }
-// Which slot of the home bucket carries the key's overflow bit (from the key's low dword).
-__host__ __device__ inline uint32_t ovf_index(uint32_t klo) {
-  return (klo * 0x9E3779B1u) >> (32 - kSlotBits);
+// Filter position h (0 .. kFilterBits - 1) of a key in a bucket of S slots (from the key's low
+// dword): position i lives in slot i / kFilterBits, at bit kFidBits + i % kFilterBits of the
+// slot's high dword (narrow) or .z (wide).
+template <int S>
+__host__ __device__ inline uint32_t filter_pos(uint32_t klo, int h) {
+  constexpr int bits = (S * kFilterBits == 32) ? 5 : (S * kFilterBits == 16) ? 4
+                     : (S * kFilterBits == 8) ? 3 : 2;
+  return ((klo * (h ? 0x85EBCA77u : 0x9E3779B1u)) + (h ? 0x165667B1u : 0u)) >> (32 - bits);
 }
 __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
   return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
@@ -60,17 +78,14 @@ __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
 // key does not fit the 8-byte slot. Wide tables use 16-byte slots, four per 64-byte bucket, so a
 // probe is still one 64-byte line and each lane of a quad loads exactly one slot (one dwordx4):
 //   .x = key bits 0..31 (never 0: the last six residues' codes), .y = key bits 32..63,
-//   .z = overflow bit << 23 | fid (23 bits), .w = 0.
-// The overflow filter has one bit per slot (4 per bucket); chains, layouts and the stop rule are
-// those of the narrow table. Wide buckets are 64 bytes in every build.
+//   .z = filter bits << 22 | fid (22 bits), .w = 0.
+// The filter has kFilterBits per slot; chains, layouts and the stop rule are those of the
+// narrow table. Wide buckets are 64 bytes in every build.
 constexpr int kWideSlots = 4;
 constexpr int kWideSlotBits = 2;
 constexpr int kMaxNarrowK = 8;
 __host__ __device__ constexpr bool wide_k(int k) { return k > kMaxNarrowK; }
 __host__ __device__ constexpr int slots_for_k(int k) { return wide_k(k) ? kWideSlots : kSlotsPerBucket; }
-__host__ __device__ inline uint32_t ovf_index_wide(uint32_t klo) {
-  return (klo * 0x9E3779B1u) >> (32 - kWideSlotBits);
-}
 
 __host__ __device__ inline uint32_t mix32(uint32_t h) {  // murmur3 fmix32
   h ^= h >> 16;
@@ -217,8 +232,11 @@ constexpr uint32_t kMaxChain = 32;
 constexpr int kProbeWin = KMA_PROBE_WIN;
 constexpr int kBlockProteins = KMA_BLOCK_PROTEINS;
 constexpr int kSetPool = KMA_SET_POOL;
+// Lane permutation of the probe loops (kma_kernels.hip): one load instruction covers 16
+// consecutive windows, so windows sharing a minimizer share a line inside the instruction.
+// c5 3.96 vs 4.03 ms (profiles/r03_ab/).
 #ifndef KMA_LANE_PERM
-#define KMA_LANE_PERM 0
+#define KMA_LANE_PERM 1
 #endif
 #ifndef KMA_CHAIN_Q
 #define KMA_CHAIN_Q 384

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
-    if (key == 0) continue;
+    if (key == 0 || (key >> (5 * k)) != 0) continue;  // no key / not a K-mer key: never stored
     const uint64_t want = Wide ? key : slot_make(key, 0);
     const uint32_t home = home_bucket(key, k, m, n_buckets);
     uint32_t b = home;
@@ -77,12 +77,14 @@ __global__ __launch_bounds__(256) void build_insert_kernel(uint64_t* slots, uint
     }
     if (!done) {
       atomicOr(status, 1u);  // table full: cannot happen at load factor < 1
-    } else if (b != home) {
-      uint32_t* ovf = Wide ? reinterpret_cast<uint32_t*>(
-                                 slots + 2 * ((uint64_t)home * S + ovf_index_wide((uint32_t)key)) + 1)
-                           : reinterpret_cast<uint32_t*>(
-                                 slots + (uint64_t)home * S + ovf_index((uint32_t)key)) + 1;
-      atomicOr(ovf, kOvfBit);
+    } else if (b != home) {  // displaced: set the key's filter positions in its home bucket
+      for (int f = 0; f < kFilterBits; ++f) {
+        const uint32_t pos = filter_pos<S>((uint32_t)key, f);
+        const uint64_t si = (uint64_t)home * S + pos / kFilterBits;
+        uint32_t* meta = Wide ? reinterpret_cast<uint32_t*>(slots + 2 * si + 1)   // .z
+                              : reinterpret_cast<uint32_t*>(slots + si) + 1;      // high dword
+        atomicOr(meta, 1u << (kFidBits + pos % kFilterBits));
+      }
     }
   }
 }
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
     if (Wide) {
       key = slots[2 * i];
       uint32_t* meta = reinterpret_cast<uint32_t*>(slots + 2 * i + 1);
-      *meta = *meta | (fids[w - 1] & kFidMask);  // keep the overflow bit
+      *meta = *meta | (fids[w - 1] & kFidMask);  // keep the filter bits
     } else {
       const uint64_t v = slots[i];
       slots[i] = v | ((uint64_t)(fids[w - 1] & kFidMask) << 32);
@@ -438,11 +440,11 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       if (w & kWordFid)
         record_hit<P>(sm, a, span_lo, multiset, bk[j] >> kBucketBits, (w & kWordFid) - 1u,
                       (bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
-      // rare: the home bucket missed with the key's overflow bit set -> deferred chain walk
+      // rare: the home bucket missed and the key's filter positions are set -> deferred walk
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
       const bool pend = false;
 #else
-      const bool pend = w == 0x80000000u;
+      const bool pend = w == kWalkWord;
 #endif
       const uint64_t m = __ballot(pend);
       if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + tw;
@@ -561,17 +563,26 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
   return lo;
 }
 
-// Exclusive prefix of n block counts by one block of 256 threads (the probe grid's last block):
-// thread t sums a contiguous chunk (agent-scope loads: the counts were written by blocks on
-// other XCDs), a block scan of the 256 sums, then each thread writes its chunk's prefixes.
+// Exclusive prefix of n block counts by one block of 256 threads (the probe grid's last block,
+// after an agent-scope acquire fence that pairs with the other blocks' release fences through
+// the `done` counter): thread t sums a contiguous chunk of a multiple of 4 counts with 16-byte
+// loads (all in flight together), a block scan of the 256 sums, then each thread writes its
+// chunk's prefixes (the chunk is cache-hot by then).
 __device__ __forceinline__ void scan_block_counts(const uint32_t* counts, uint64_t* prefix,
                                                   uint32_t n) {
   __shared__ uint64_t part[256];
-  const uint32_t t = threadIdx.x, per = (n + 255) / 256;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = ((n + 255) / 256 + 3) & ~3u;
   const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
   uint64_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i)
-    sum += __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint4* c4 = reinterpret_cast<const uint4*>(counts);  // hipMalloc: 16-byte aligned
+  const uint32_t whole = lo + ((hi - lo) & ~3u);
+#pragma unroll 8
+  for (uint32_t i = lo; i < whole; i += 4) {
+    const uint4 v = c4[i / 4];
+    sum += (uint64_t)v.x + v.y + v.z + v.w;
+  }
+  for (uint32_t i = whole; i < hi; ++i) sum += counts[i];
   part[t] = sum;
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan of the sums
@@ -583,7 +594,7 @@ __device__ __forceinline__ void scan_block_counts(const uint32_t* counts, uint64
   uint64_t run = part[t] - sum;  // exclusive
   for (uint32_t i = lo; i < hi; ++i) {
     prefix[i] = run;
-    run += __hip_atomic_load(counts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    run += counts[i];
   }
 }
 
@@ -747,7 +758,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
       hit[h][j] = (w & kWordFid) != 0u;
       fid[h][j] = (w & kWordFid) - 1u;
       uint32_t sid = bk[h][j] * kS + ((w >> kSlotShift) & (kS - 1));
-      if (w == 0x80000000u) {  // rare: the home bucket missed with the key's overflow bit set
+      if (w == kWalkWord) {  // rare: the home bucket missed and the key's filter positions are set
         if constexpr (kWide)
           hit[h][j] = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
         else

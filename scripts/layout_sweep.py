@@ -155,7 +155,7 @@ def adversarial_workload():
         elif pos == 1:
             v = (a0 << np.uint64(35)) | (core << np.uint64(5)) | a1
         else:
-            v = (a0 << np.uint64(40)) | (a1 << np.uint64(35)) | core
+            v = (a0 << np.uint64(35)) | (a1 << np.uint64(30)) | core
         ks.append(v.reshape(-1))
     keys = np.unique(np.concatenate(ks))
     fids = (np.arange(len(keys)) % 5000).astype(np.uint32)
