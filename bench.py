@@ -364,7 +364,7 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                          0, 0, sp)
 
     elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev)
-    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["emit"]
+    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["scan_emit"]
     n_hits = int(d_nh.item())
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
@@ -383,7 +383,7 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                        "parallelism": f"genome-shard x{world}, table replicated (RCCL broadcast)"},
             "seqs_per_s": n_contig * args.steps * world / elapsed,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"probe_and_scan": k_ms, "emit": rest_ms},
+            "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
             # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 8 B per staged hit
             "roofline": roofline("probed windows x 64 B + bases + hits x 8 B", "c3",
                                  f"{kname} (6-frame translate + 2 probes per base)", k_ms,

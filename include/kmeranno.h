@@ -219,10 +219,10 @@ int kma_workspace_destroy(kma_workspace* ws);
  * synchronise on the recorded events (the last 256 calls) and clear the accumulators.
  *   _phases_read : the calls laid out like the last one (same entry point): their count, the
  *                  number of phases and each phase's summed milliseconds and name (static
- *                  strings): proteins {annotate_kernel}; contigs {contigs_probe_kernel (the
- *                  probe and, in its last block, the block-count scan), emit}.
+ *                  strings): proteins {annotate_kernel}; contigs {contigs_probe_kernel,
+ *                  scan_emit}.
  *   _timing_read : kernel_ms = proteins: every phase / contigs: the probe; rest_ms = contigs:
- *                  the emit pass.                                                            */
+ *                  the block-count scan and the emit pass.                                   */
 #define KMA_MAX_PHASES 8
 int kma_workspace_timing(kma_workspace* ws, int enable);
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,

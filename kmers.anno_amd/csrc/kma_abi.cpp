@@ -254,7 +254,6 @@ struct kma_workspace {
   uint64_t* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
   uint64_t* d_cprefix = nullptr;
-  uint32_t* d_cdone = nullptr;  // the probe grid's finished-block counter (0 between calls)
   uint64_t contig_cap = 0;  // bases
   // Per-phase timing (kma_workspace_timing): a ring of calls, each kMaxEv events (phase i runs
   // from event i to event i + 1) and its phase names.
@@ -777,13 +776,11 @@ void free_protein_scratch(kma_workspace* ws) {
 }
 
 void free_contig_scratch(kma_workspace* ws) {
-  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix,
-                  (void*)ws->d_cdone})
+  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix})
     if (p) (void)hipFree(p);
   ws->d_cstage = nullptr;
   ws->d_ccounts = nullptr;
   ws->d_cprefix = nullptr;
-  ws->d_cdone = nullptr;
   ws->contig_cap = 0;
 }
 
@@ -812,15 +809,16 @@ kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace*
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
   a.prefix = ws->d_cprefix;
-  a.done = ws->d_cdone;
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
   return a;
 }
 
+// Scan of the probe's block counts + canonical-order emission (after the probe on s).
 int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
                         hipStream_t s) {
+  KMA_HIP(kma::launch_contig_scan(a, contig_blocks(a.total_bases), s));
   a.out = d_hits;
   a.cap = d_hits ? cap : 0;
   a.n_hits = d_n_hits;
@@ -845,7 +843,7 @@ struct PhaseClock {
 };
 
 const char* const kDirectPhases[] = {"annotate_kernel"};
-const char* const kContigPhases[] = {"contigs_probe_kernel", "emit"};
+const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
 // Proteins per annotate_kernel block: 4 (KMA_BLOCK_PROTEINS=1..8 overrides, read per call).
 // Measured on MI355X (profiles/r02f_block_proteins.log): c2 65.1 / 65.5 / 65.6 / 73.9 us and c5
@@ -1048,8 +1046,6 @@ int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * 8));
   KMA_HIP(hipMalloc(&ws->d_ccounts, nb * 4));
   KMA_HIP(hipMalloc(&ws->d_cprefix, nb * 8));
-  KMA_HIP(hipMalloc(&ws->d_cdone, 4));
-  KMA_HIP(hipMemset(ws->d_cdone, 0, 4));
   ws->contig_cap = nb * kma::kContigTile;
   return KMA_OK;
 }
@@ -1146,7 +1142,7 @@ int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kern
   const char* names[KMA_MAX_PHASES];
   int np = 0;
   if (int rc = kma_workspace_phases_read(ws, n_calls, &np, ms, names)) return rc;
-  // contigs: (probe + block-count scan, emit); proteins: the whole path (every phase), nothing after it
+  // contigs: (probe, scan + emit); proteins: the whole path (every phase), nothing after it
   const bool contigs = np > 0 && names[0] == kContigPhases[0];
   *kernel_ms = 0;
   *rest_ms = 0;

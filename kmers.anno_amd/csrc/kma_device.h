@@ -151,50 +151,41 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 
 // One quad's verdict on a bucket it loaded cooperatively: lane `part` holds slots 2part and
 // 2part + 1 of each 64-byte half h of the bucket in v[h] (slots 8h + 2part, 8h + 2part + 1)
-// for key (kl, kh): fid + 1 of the matching slot in bits 0..23 (0 = not in this bucket), the
-// slot's index in the bucket from bit 24, and bit 31 - h set when the key's filter position h
-// is set (with no match and every position set, the chain must be walked: kWalkWord). Keys are unique in a table, so at most one lane matches and OR
-// is the reduction. Every lane of the quad must call it (DPP). Branch-free on purpose: a
-// short-circuit here lets the compiler split the 16-byte loads into a lazily loaded tail
-// behind a branch and a vmcnt(0).
+// for key (kl, kh) with filter mask `need` (filter_need of the key, the same in every lane of
+// the quad): the verdict word of kma_internal.h (fid + 1, slot, kAbsent). Lane `part` holds
+// the filter positions of its two slots (position i in slot i / kFilterBits). Keys are unique
+// in a table, so at most one lane matches and OR is the reduction. Every lane of the quad must
+// call it (DPP). Branch-free on purpose: a short-circuit here lets the compiler split the
+// 16-byte loads into a lazily loaded tail behind a branch and a vmcnt(0).
 __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
-                                               uint32_t kh, uint32_t part) {
-  uint32_t w = 0;
+                                               uint32_t kh, uint32_t need, uint32_t part) {
+  constexpr uint32_t FB = kFilterBits, PM = (1u << (2 * FB)) - 1;  // positions per lane, half
+  uint32_t w = 0, missing = 0;
 #pragma unroll
   for (int h = 0; h < kBucketHalves; ++h) {
     const uint32_t m0 = (uint32_t)(v[h].x == kl) & (uint32_t)((v[h].y & kKeyHiMask) == kh);
     const uint32_t m1 = (uint32_t)(v[h].z == kl) & (uint32_t)((v[h].w & kKeyHiMask) == kh);
     w |= (m0 * ((v[h].y & kFidMask) + 1u)) | (m1 * ((v[h].w & kFidMask) + 1u));
     w |= (m0 | m1) * ((8u * h + 2u * part + m1) << kSlotShift);  // slot within the bucket
+    // the lane's positions: slot 8h + 2part (bits of .y), slot 8h + 2part + 1 (bits of .w)
+    const uint32_t held = ((v[h].y >> kFidBits) & ((1u << FB) - 1u)) |
+                          (((v[h].w >> kFidBits) & ((1u << FB) - 1u)) << FB);
+    const uint32_t want = (need >> (2u * FB * (4u * h + part))) & PM;
+    missing |= want & ~held;
   }
-  // filter position i: slot i / kFilterBits = 8 hh + 2 p + which, held by quad lane p
-#pragma unroll
-  for (int f = 0; f < kFilterBits; ++f) {
-    const uint32_t pos = filter_pos<kSlotsPerBucket>(kl, f), slot = pos / kFilterBits;
-    const uint32_t which = slot & 1u, lp = (slot >> 1) & 3u, hh = slot >> 3;
-    uint32_t hi = 0;
-#pragma unroll
-    for (int h = 0; h < kBucketHalves; ++h)
-      hi = hh == (uint32_t)h ? (which ? v[h].w : v[h].y) : hi;
-    const uint32_t b = (uint32_t)(lp == part) & (hi >> (kFidBits + pos % kFilterBits)) & 1u;
-    w |= b << (31 - f);
-  }
+  w |= missing ? kAbsent : 0u;
   return quad_or(w);
 }
 
 // Wide tables (K > 8, kma_internal.h): lane `part` of the quad holds slot `part` of the bucket
-// in v; same verdict word as match_part (fid + 1, slot from bit 24, filter positions set from
-// bit 31 down).
+// in v (and its filter positions 2part .. in .z); same verdict word as match_part.
 __device__ __forceinline__ uint32_t match_wide(const uint4& v, uint32_t kl, uint32_t kh,
-                                               uint32_t part) {
+                                               uint32_t need, uint32_t part) {
   const uint32_t m = (uint32_t)(v.x == kl) & (uint32_t)(v.y == kh);
   uint32_t w = m * ((v.z & kFidMask) + 1u) | m * (part << kSlotShift);
-#pragma unroll
-  for (int f = 0; f < kFilterBits; ++f) {
-    const uint32_t pos = filter_pos<kWideSlots>(kl, f);
-    w |= ((uint32_t)(pos / kFilterBits == part) & (v.z >> (kFidBits + pos % kFilterBits)) & 1u)
-         << (31 - f);
-  }
+  const uint32_t held = (v.z >> kFidBits) & ((1u << kFilterBits) - 1u);
+  const uint32_t want = (need >> (kFilterBits * part)) & ((1u << kFilterBits) - 1u);
+  w |= (want & ~held) ? kAbsent : 0u;
   return quad_or(w);
 }
 

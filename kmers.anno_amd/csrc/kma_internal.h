@@ -46,9 +46,11 @@ static_assert(kFilterBits == 1 || kFilterBits == 2, "one or two filter bits per 
 constexpr uint32_t kFidBits = 24 - kFilterBits;  // fid width (KMA_MAX_FID: 22 bits)
 constexpr uint32_t kFidMask = (1u << kFidBits) - 1;
 constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
-// The probe's verdict word when the home bucket misses and every filter position is set: the
-// key may live further down the chain (bit 31 - h = position h set).
-constexpr uint32_t kWalkWord = kFilterBits == 2 ? 0xC0000000u : 0x80000000u;
+// The probe's verdict word (match_part / match_wide): fid + 1 in bits 0..23 (0 = no match),
+// the slot in the bucket from bit 24, and kAbsent (bit 31) when a filter position of the key is
+// clear in its home bucket — the key is not further down the chain. A probed window whose word
+// is 0 missed its home bucket with every filter position set: it walks the chain.
+constexpr uint32_t kAbsent = 0x80000000u;
 // The probe's per-window verdict: fid + 1 in bits 0..23, slot in bucket at kSlotShift,
 // bit 31 = the key's overflow bit in its home bucket.
 constexpr uint32_t kWordFid = (1u << 24) - 1;
@@ -68,6 +70,14 @@ __host__ __device__ inline uint32_t filter_pos(uint32_t klo, int h) {
   constexpr int bits = (S * kFilterBits == 32) ? 5 : (S * kFilterBits == 16) ? 4
                      : (S * kFilterBits == 8) ? 3 : 2;
   return ((klo * (h ? 0x85EBCA77u : 0x9E3779B1u)) + (h ? 0x165667B1u : 0u)) >> (32 - bits);
+}
+// The key's filter positions as a mask over the bucket's S * kFilterBits positions (computed
+// once per window by its lane and broadcast to the quad that probes it).
+template <int S>
+__host__ __device__ inline uint32_t filter_need(uint32_t klo) {
+  uint32_t m = 0;
+  for (int h = 0; h < kFilterBits; ++h) m |= 1u << filter_pos<S>(klo, h);
+  return m;
 }
 __host__ __device__ inline uint64_t slot_key(uint64_t slot) {
   return ((uint64_t)(uint32_t)(slot >> 56) << 32) | (uint32_t)slot;
@@ -282,9 +292,7 @@ struct ContigArgs {
   int32_t mlen;
   uint64_t* staging;           // n_blocks x kContigTile*2 packed hits (relative position)
   uint32_t* block_counts;      // n_blocks
-  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (the probe's last
-                               // block writes it; the emit pass reads it)
-  uint32_t* done;              // blocks finished (0 between calls; the last block resets it)
+  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (emit pass)
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order
@@ -335,6 +343,7 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
+hipError_t launch_contig_scan(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 // Peg-kmer singleton table (KmerReference.countPegKmers + CountMap.getSingletons): every
 // window i < L-K without 'X' of every peg -> (key or 0, peg index) per residue position; sort;

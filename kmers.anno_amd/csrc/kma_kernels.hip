@@ -378,6 +378,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   // flight, so a wave's only exposed latency per step is the bucket gather.
   for (uint32_t x0 = 0; x0 < span; x0 += stride) {
     uint32_t klo[U], khi[U], bk[U];  // bk: protein << kBucketBits | home bucket, or kNone
+    uint32_t need[U];                // the key's filter positions
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint32_t x = x0 + j * 256u + tw;
@@ -393,6 +394,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
                       x < span && x - pbp < pwp;
       klo[j] = (uint32_t)key;
       khi[j] = (uint32_t)(key >> 32) << 24;
+      need[j] = filter_need<kSlotsPerBucket>(klo[j]);
       bk[j] = ok ? (p << kBucketBits | home_bucket(key, K, M, nb)) : kNone;
     }
     // Cooperative loads: the quad's four buckets, 64 bytes at a time (lane `part` reads bytes
@@ -429,7 +431,9 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
                           : r == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
         const uint32_t kh = r == 0 ? quad_bcast<0>(khi[j]) : r == 1 ? quad_bcast<1>(khi[j])
                           : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
-        const uint32_t v = match_part(q[j][r], kl, kh, part);
+        const uint32_t nd = r == 0 ? quad_bcast<0>(need[j]) : r == 1 ? quad_bcast<1>(need[j])
+                          : r == 2 ? quad_bcast<2>(need[j]) : quad_bcast<3>(need[j]);
+        const uint32_t v = match_part(q[j][r], kl, kh, nd, part);
         word[j] = part == r ? v : word[j];
       }
     }
@@ -444,7 +448,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
       const bool pend = false;
 #else
-      const bool pend = w == kWalkWord;
+      const bool pend = probed && w == 0u;
 #endif
       const uint64_t m = __ballot(pend);
       if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + tw;
@@ -540,7 +544,7 @@ __device__ __forceinline__ uint32_t base2(uint8_t c) {  // T,C,A,G -> 0..3; othe
 // DPP quad match); the tile's contigs are found once (two wave-parallel searches) and their
 // offsets cached in LDS, so a position's contig costs no global loads. Hits are compacted per
 // block in canonical order (position, '+' before '-'); the grid's last block scans the block
-// counts and an emit pass writes every block's hits at its offset.
+// counts (one-block scan kernel) and an emit pass writes every block's hits at its offset.
 constexpr int kOffCache = 64;
 
 // contig_of by a whole wave, 64 candidates per dependent load: the largest c < n with
@@ -561,41 +565,6 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
     lo = nlo;
   }
   return lo;
-}
-
-// Exclusive prefix of n block counts by one block of 256 threads (the probe grid's last block,
-// after an agent-scope acquire fence that pairs with the other blocks' release fences through
-// the `done` counter): thread t sums a contiguous chunk of a multiple of 4 counts with 16-byte
-// loads (all in flight together), a block scan of the 256 sums, then each thread writes its
-// chunk's prefixes (the chunk is cache-hot by then).
-__device__ __forceinline__ void scan_block_counts(const uint32_t* counts, uint64_t* prefix,
-                                                  uint32_t n) {
-  __shared__ uint64_t part[256];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = ((n + 255) / 256 + 3) & ~3u;
-  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
-  uint64_t sum = 0;
-  const uint4* c4 = reinterpret_cast<const uint4*>(counts);  // hipMalloc: 16-byte aligned
-  const uint32_t whole = lo + ((hi - lo) & ~3u);
-#pragma unroll 8
-  for (uint32_t i = lo; i < whole; i += 4) {
-    const uint4 v = c4[i / 4];
-    sum += (uint64_t)v.x + v.y + v.z + v.w;
-  }
-  for (uint32_t i = whole; i < hi; ++i) sum += counts[i];
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan of the sums
-    const uint64_t v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint64_t run = part[t] - sum;  // exclusive
-  for (uint32_t i = lo; i < hi; ++i) {
-    prefix[i] = run;
-    run += counts[i];
-  }
 }
 
 template <int K, int M>
@@ -742,6 +711,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     for (int j = 0; j < 2; ++j) {
       const uint32_t klo = (uint32_t)key[h][j];
       const uint32_t khi = kWide ? (uint32_t)(key[h][j] >> 32) : (uint32_t)(key[h][j] >> 32) << 24;
+      const uint32_t need = filter_need<kS>(klo);
       uint32_t word = 0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -749,16 +719,18 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
                           : rr == 2 ? quad_bcast<2>(klo) : quad_bcast<3>(klo);
         const uint32_t kh = rr == 0 ? quad_bcast<0>(khi) : rr == 1 ? quad_bcast<1>(khi)
                           : rr == 2 ? quad_bcast<2>(khi) : quad_bcast<3>(khi);
+        const uint32_t nd = rr == 0 ? quad_bcast<0>(need) : rr == 1 ? quad_bcast<1>(need)
+                          : rr == 2 ? quad_bcast<2>(need) : quad_bcast<3>(need);
         uint32_t v;
-        if constexpr (kWide) v = match_wide(q[h][j][rr][0], kl, kh, part);
-        else v = match_part(q[h][j][rr], kl, kh, part);
+        if constexpr (kWide) v = match_wide(q[h][j][rr][0], kl, kh, nd, part);
+        else v = match_part(q[h][j][rr], kl, kh, nd, part);
         word = part == rr ? v : word;
       }
       const uint32_t w = bk[h][j] != kNone ? word : 0u;
       hit[h][j] = (w & kWordFid) != 0u;
       fid[h][j] = (w & kWordFid) - 1u;
       uint32_t sid = bk[h][j] * kS + ((w >> kSlotShift) & (kS - 1));
-      if (w == kWalkWord) {  // rare: the home bucket missed and the key's filter positions are set
+      if (bk[h][j] != kNone && w == 0u) {  // rare: home missed, every filter position set
         if constexpr (kWide)
           hit[h][j] = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
         else
@@ -815,20 +787,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     if (hit[h][0]) st[o++] = (r << 25) | fid[h][0];               // strand bit 24 = 0: '+'
     if (hit[h][1]) st[o] = (r << 25) | (1ull << 24) | fid[h][1];  // '-'
   }
-  // The last block to finish scans the block counts (the emit pass's offsets): no scan
-  // kernels between probe and emit (they were ~10 us of a ~115 us c3 step).
-  __shared__ uint32_t last;
-  if (t == 0) {
-    a.block_counts[blockIdx.x] = total;
-    __threadfence();  // the count is visible device-wide before the ticket
-    last = atomicAdd(a.done, 1u) == gridDim.x - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (last) {
-    __threadfence();
-    scan_block_counts(a.block_counts, const_cast<uint64_t*>(a.prefix), gridDim.x);
-    if (t == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (t == 0) a.block_counts[blockIdx.x] = total;
   KMA_CLK(5);
   KMA_CLK_HW();
 }
@@ -954,6 +913,43 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
     if (k[i] == 0) continue;
     const uint32_t h = run[i], t = tags[i];
     if (t == kBuildNeg || t != tags[h]) flags[h] = 0;  // every writer stores 0
+  }
+}
+
+// Exclusive prefix of the probe grid's n block counts, one block of 1024 threads (between probe
+// and emit; round 2 used hipcub's two-kernel scan, ~10 us; a ticket counter letting the probe's
+// last block scan measured 0.6 ms: 20k atomics on one address serialize). Thread t sums a
+// contiguous chunk of a multiple of 4 counts with 16-byte loads, a block scan of the sums, then
+// each thread writes its chunk's prefixes.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void contig_scan_kernel(const uint32_t* __restrict__ counts,
+                                                                   uint64_t* __restrict__ prefix,
+                                                                   uint32_t n) {
+  __shared__ uint64_t part[kScanThreads];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = ((n + kScanThreads - 1) / kScanThreads + 3) & ~3u;
+  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
+  const uint32_t whole = lo + ((hi - lo) & ~3u);
+  const uint4* c4 = reinterpret_cast<const uint4*>(counts);  // hipMalloc: 16-byte aligned
+  uint64_t sum = 0;
+#pragma unroll 4
+  for (uint32_t i = lo; i < whole; i += 4) {
+    const uint4 v = c4[i / 4];
+    sum += (uint64_t)v.x + v.y + v.z + v.w;
+  }
+  for (uint32_t i = whole; i < hi; ++i) sum += counts[i];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < kScanThreads; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - sum;
+  for (uint32_t i = lo; i < hi; ++i) {
+    prefix[i] = run;
+    run += counts[i];
   }
 }
 
@@ -1124,6 +1120,12 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(sig_clear_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, tags, run,
                      n, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_contig_scan(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  hipLaunchKernelGGL(contig_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, a.block_counts,
+                     const_cast<uint64_t*>(a.prefix), (uint32_t)n_blocks);
   return hipGetLastError();
 }
 
