@@ -248,6 +248,10 @@ constexpr int kSetPool = KMA_SET_POOL;
 #ifndef KMA_LANE_PERM
 #define KMA_LANE_PERM 1
 #endif
+// Two-stage software pipeline of the protein kernel's probe loop (kma_kernels.hip).
+#ifndef KMA_PIPE
+#define KMA_PIPE 0
+#endif
 #ifndef KMA_CHAIN_Q
 #define KMA_CHAIN_Q 384
 #endif

@@ -374,14 +374,15 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     __builtin_amdgcn_wave_barrier();
     cn = 0;
   };
-  // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
-  // flight, so a wave's only exposed latency per step is the bucket gather.
-  for (uint32_t x0 = 0; x0 < span; x0 += stride) {
-    uint32_t klo[U], khi[U], bk[U];  // bk: protein << kBucketBits | home bucket, or kNone
-    uint32_t need[U];                // the key's filter positions
+  // A step's windows: packed keys, filter masks and home buckets (bk: protein << kBucketBits |
+  // home bucket, or kNone for a window that does not probe), from the residues in ww.
+  struct Prep {
+    uint32_t klo[U], khi[U], need[U], bk[U];
+  };
+  auto prep = [&](uint32_t xs, Prep& o) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = x0 + j * 256u + tw;
+      const uint32_t x = xs + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
       uint32_t pbp = pb[0], pwp = pw[0];
 #pragma unroll
@@ -392,19 +393,20 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       uint64_t key;
       const bool ok = pack_window<K>(lut, funnel(ww[j].lo, ww[j].hi, ww[j].sh), key) &&
                       x < span && x - pbp < pwp;
-      klo[j] = (uint32_t)key;
-      khi[j] = (uint32_t)(key >> 32) << 24;
-      need[j] = filter_need<kSlotsPerBucket>(klo[j]);
-      bk[j] = ok ? (p << kBucketBits | home_bucket(key, K, M, nb)) : kNone;
+      o.klo[j] = (uint32_t)key;
+      o.khi[j] = (uint32_t)(key >> 32) << 24;
+      o.need[j] = filter_need<kSlotsPerBucket>(o.klo[j]);
+      o.bk[j] = ok ? (p << kBucketBits | home_bucket(key, K, M, nb)) : kNone;
     }
-    // Cooperative loads: the quad's four buckets, 64 bytes at a time (lane `part` reads bytes
-    // [16 part, 16 part + 16) of each 64-byte half), all dwordx4 of the lane in flight before
-    // any compare. A window that does not probe reads bucket 0 (result discarded).
-    uint4 q[U][4][kBucketHalves];
+  };
+  // Cooperative loads: the quad's four buckets, 64 bytes at a time (lane `part` reads bytes
+  // [16 part, 16 part + 16) of each 64-byte half), all dwordx4 of the lane in flight before any
+  // compare. A window that does not probe reads bucket 0 (result discarded).
+  auto gather = [&](const Prep& c, uint4 (&q)[U][4][kBucketHalves]) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t b0 = quad_bcast<0>(bk[j]), b1 = quad_bcast<1>(bk[j]);
-      const uint32_t b2 = quad_bcast<2>(bk[j]), b3 = quad_bcast<3>(bk[j]);
+      const uint32_t b0 = quad_bcast<0>(c.bk[j]), b1 = quad_bcast<1>(c.bk[j]);
+      const uint32_t b2 = quad_bcast<2>(c.bk[j]), b3 = quad_bcast<3>(c.bk[j]);
       const uint32_t bb[4] = {b0, b1, b2, b3};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -414,36 +416,39 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
         for (int h = 0; h < kBucketHalves; ++h) q[j][r][h] = bp[4 * h];
       }
     }
-    // Next step's residues (issued after the bucket loads: waiting for those leaves these in
-    // flight, vmcnt counts in order).
+  };
+  auto load_residues = [&](uint32_t xs) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = x0 + stride + j * 256u + tw;
+      const uint32_t x = xs + j * 256u + tw;
       ww[j] = window_words(res, (x < span ? x : 0u) + mis);
     }
+  };
+  // Compare the quad's buckets, record hits, queue chain walks.
+  auto settle = [&](uint32_t x0, const Prep& c, const uint4 (&q)[U][4][kBucketHalves]) {
     uint32_t word[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       word[j] = 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t kl = r == 0 ? quad_bcast<0>(klo[j]) : r == 1 ? quad_bcast<1>(klo[j])
-                          : r == 2 ? quad_bcast<2>(klo[j]) : quad_bcast<3>(klo[j]);
-        const uint32_t kh = r == 0 ? quad_bcast<0>(khi[j]) : r == 1 ? quad_bcast<1>(khi[j])
-                          : r == 2 ? quad_bcast<2>(khi[j]) : quad_bcast<3>(khi[j]);
-        const uint32_t nd = r == 0 ? quad_bcast<0>(need[j]) : r == 1 ? quad_bcast<1>(need[j])
-                          : r == 2 ? quad_bcast<2>(need[j]) : quad_bcast<3>(need[j]);
+        const uint32_t kl = r == 0 ? quad_bcast<0>(c.klo[j]) : r == 1 ? quad_bcast<1>(c.klo[j])
+                          : r == 2 ? quad_bcast<2>(c.klo[j]) : quad_bcast<3>(c.klo[j]);
+        const uint32_t kh = r == 0 ? quad_bcast<0>(c.khi[j]) : r == 1 ? quad_bcast<1>(c.khi[j])
+                          : r == 2 ? quad_bcast<2>(c.khi[j]) : quad_bcast<3>(c.khi[j]);
+        const uint32_t nd = r == 0 ? quad_bcast<0>(c.need[j]) : r == 1 ? quad_bcast<1>(c.need[j])
+                          : r == 2 ? quad_bcast<2>(c.need[j]) : quad_bcast<3>(c.need[j]);
         const uint32_t v = match_part(q[j][r], kl, kh, nd, part);
         word[j] = part == r ? v : word[j];
       }
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const bool probed = bk[j] != kNone;
+      const bool probed = c.bk[j] != kNone;
       const uint32_t w = probed ? word[j] : 0u;
       if (w & kWordFid)
-        record_hit<P>(sm, a, span_lo, multiset, bk[j] >> kBucketBits, (w & kWordFid) - 1u,
-                      (bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
+        record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, (w & kWordFid) - 1u,
+                      (c.bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
       // rare: the home bucket missed and the key's filter positions are set -> deferred walk
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
       const bool pend = false;
@@ -455,8 +460,39 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       cn += (uint32_t)__popcll(m);
     }
     if (cn > (uint32_t)(kChainQ - 64 * U)) chain_flush();
+  };
+#if KMA_PIPE
+  // Two-stage software pipeline: step i + 1's windows are packed and hashed while step i's
+  // buckets are in flight (its residues were loaded one step earlier), so the exposed time per
+  // step is the gather plus the compare only.
+  Prep cur;
+  prep(0u, cur);
+  load_residues(stride);
+  for (uint32_t x0 = 0; x0 < span; x0 += stride) {
+    uint4 q[U][4][kBucketHalves];
+    gather(cur, q);
+    Prep nxt;
+    prep(x0 + stride, nxt);
+    load_residues(x0 + 2 * stride);
+    settle(x0, cur, q);
+    cur = nxt;
     if (x0 == 0) KMA_CLK(2);
   }
+#else
+  // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
+  // flight, so a wave's only exposed latency per step is the bucket gather.
+  for (uint32_t x0 = 0; x0 < span; x0 += stride) {
+    Prep cur;
+    prep(x0, cur);
+    uint4 q[U][4][kBucketHalves];
+    gather(cur, q);
+    // next step's residues (issued after the bucket loads: waiting for those leaves these in
+    // flight, vmcnt counts in order)
+    load_residues(x0 + stride);
+    settle(x0, cur, q);
+    if (x0 == 0) KMA_CLK(2);
+  }
+#endif
   KMA_CLK(3);
   KMA_CLK_SET(7, (span + stride - 1) / stride);
   if (cn) chain_flush();
@@ -918,38 +954,50 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
 
 // Exclusive prefix of the probe grid's n block counts, one block of 1024 threads (between probe
 // and emit; round 2 used hipcub's two-kernel scan, ~10 us; a ticket counter letting the probe's
-// last block scan measured 0.6 ms: 20k atomics on one address serialize). Thread t sums a
-// contiguous chunk of a multiple of 4 counts with 16-byte loads, a block scan of the sums, then
-// each thread writes its chunk's prefixes.
+// last block scan measured 0.6 ms: 20k atomics on one address serialize). Tiles of 16 counts
+// per thread: four 16-byte loads into registers, a block scan of the thread sums with the
+// running carry, the 16 prefixes written from registers.
 constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 16;
 __global__ __launch_bounds__(kScanThreads) void contig_scan_kernel(const uint32_t* __restrict__ counts,
                                                                    uint64_t* __restrict__ prefix,
                                                                    uint32_t n) {
   __shared__ uint64_t part[kScanThreads];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = ((n + kScanThreads - 1) / kScanThreads + 3) & ~3u;
-  const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
-  const uint32_t whole = lo + ((hi - lo) & ~3u);
-  const uint4* c4 = reinterpret_cast<const uint4*>(counts);  // hipMalloc: 16-byte aligned
-  uint64_t sum = 0;
-#pragma unroll 4
-  for (uint32_t i = lo; i < whole; i += 4) {
-    const uint4 v = c4[i / 4];
-    sum += (uint64_t)v.x + v.y + v.z + v.w;
-  }
-  for (uint32_t i = whole; i < hi; ++i) sum += counts[i];
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < kScanThreads; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint64_t v = t >= d ? part[t - d] : 0;
+  uint64_t carry = 0;
+  for (uint32_t base = 0; base < n; base += kScanThreads * kScanPer) {
+    const uint32_t lo = base + t * kScanPer;
+    uint32_t c[kScanPer];
+    if (lo + kScanPer <= n) {
+      const uint4* c4 = reinterpret_cast<const uint4*>(counts + lo);  // 64-byte aligned
+#pragma unroll
+      for (int i = 0; i < kScanPer / 4; ++i) {
+        const uint4 v = c4[i];
+        c[4 * i] = v.x, c[4 * i + 1] = v.y, c[4 * i + 2] = v.z, c[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kScanPer; ++i) c[i] = lo + i < n ? counts[lo + i] : 0u;
+    }
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) sum += c[i];
+    part[t] = sum;
     __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint64_t run = part[t] - sum;
-  for (uint32_t i = lo; i < hi; ++i) {
-    prefix[i] = run;
-    run += counts[i];
+    for (uint32_t d = 1; d < kScanThreads; d <<= 1) {  // inclusive Hillis-Steele scan
+      const uint64_t v = t >= d ? part[t - d] : 0;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+    }
+    uint64_t run = carry + part[t] - sum;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      if (lo + i < n) prefix[lo + i] = run;
+      run += c[i];
+    }
+    carry += part[kScanThreads - 1];
+    __syncthreads();  // part is rewritten by the next tile
   }
 }
 
