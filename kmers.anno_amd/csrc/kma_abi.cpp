@@ -808,14 +808,14 @@ kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace*
   a.mlen = t->mlen;
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
-  a.prefix = ws->d_cprefix;
+  a.group_sum = ws->d_cprefix;
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
   return a;
 }
 
-// Scan of the probe's block counts + canonical-order emission (after the probe on s).
+// Group sums of the probe's block counts + canonical-order emission (after the probe on s).
 int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
                         hipStream_t s) {
   KMA_HIP(kma::launch_contig_scan(a, contig_blocks(a.total_bases), s));

@@ -248,10 +248,6 @@ constexpr int kSetPool = KMA_SET_POOL;
 #ifndef KMA_LANE_PERM
 #define KMA_LANE_PERM 1
 #endif
-// Two-stage software pipeline of the protein kernel's probe loop (kma_kernels.hip).
-#ifndef KMA_PIPE
-#define KMA_PIPE 0
-#endif
 #ifndef KMA_CHAIN_Q
 #define KMA_CHAIN_Q 384
 #endif
@@ -296,7 +292,7 @@ struct ContigArgs {
   int32_t mlen;
   uint64_t* staging;           // n_blocks x kContigTile*2 packed hits (relative position)
   uint32_t* block_counts;      // n_blocks
-  const uint64_t* prefix;      // n_blocks: exclusive scan of block_counts (emit pass)
+  uint64_t* group_sum;         // ceil(n_blocks / 256): sums of 256 block counts (emit offsets)
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order

@@ -461,26 +461,10 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     }
     if (cn > (uint32_t)(kChainQ - 64 * U)) chain_flush();
   };
-#if KMA_PIPE
-  // Two-stage software pipeline: step i + 1's windows are packed and hashed while step i's
-  // buckets are in flight (its residues were loaded one step earlier), so the exposed time per
-  // step is the gather plus the compare only.
-  Prep cur;
-  prep(0u, cur);
-  load_residues(stride);
-  for (uint32_t x0 = 0; x0 < span; x0 += stride) {
-    uint4 q[U][4][kBucketHalves];
-    gather(cur, q);
-    Prep nxt;
-    prep(x0 + stride, nxt);
-    load_residues(x0 + 2 * stride);
-    settle(x0, cur, q);
-    cur = nxt;
-    if (x0 == 0) KMA_CLK(2);
-  }
-#else
   // Software pipeline: the residues of step i + 1 are loaded while step i's buckets are in
-  // flight, so a wave's only exposed latency per step is the bucket gather.
+  // flight, so a wave's only exposed latency per step is the bucket gather. (A two-stage
+  // pipeline packing step i + 1 under step i's gather measured 6.51 vs 4.48 ms at c5,
+  // profiles/r03_ab/r03h_steps.log.)
   for (uint32_t x0 = 0; x0 < span; x0 += stride) {
     Prep cur;
     prep(x0, cur);
@@ -492,7 +476,6 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     settle(x0, cur, q);
     if (x0 == 0) KMA_CLK(2);
   }
-#endif
   KMA_CLK(3);
   KMA_CLK_SET(7, (span + stride - 1) / stride);
   if (cn) chain_flush();
@@ -579,8 +562,8 @@ __device__ __forceinline__ uint32_t base2(uint8_t c) {  // T,C,A,G -> 0..3; othe
 // loads of the protein path (both probes' 8 dwordx4 of a lane in flight before any compare,
 // DPP quad match); the tile's contigs are found once (two wave-parallel searches) and their
 // offsets cached in LDS, so a position's contig costs no global loads. Hits are compacted per
-// block in canonical order (position, '+' before '-'); the grid's last block scans the block
-// counts (one-block scan kernel) and an emit pass writes every block's hits at its offset.
+// block in canonical order (position, '+' before '-'); group sums of the block counts and an emit
+// pass (each block computes its offset from them) write every block's hits in order.
 constexpr int kOffCache = 64;
 
 // contig_of by a whole wave, 64 candidates per dependent load: the largest c < n with
@@ -952,60 +935,46 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
   }
 }
 
-// Exclusive prefix of the probe grid's n block counts, one block of 1024 threads (between probe
-// and emit; round 2 used hipcub's two-kernel scan, ~10 us; a ticket counter letting the probe's
-// last block scan measured 0.6 ms: 20k atomics on one address serialize). Tiles of 16 counts
-// per thread: four 16-byte loads into registers, a block scan of the thread sums with the
-// running carry, the 16 prefixes written from registers.
-constexpr int kScanThreads = 1024;
-constexpr int kScanPer = 16;
-__global__ __launch_bounds__(kScanThreads) void contig_scan_kernel(const uint32_t* __restrict__ counts,
-                                                                   uint64_t* __restrict__ prefix,
-                                                                   uint32_t n) {
-  __shared__ uint64_t part[kScanThreads];
-  const uint32_t t = threadIdx.x;
-  uint64_t carry = 0;
-  for (uint32_t base = 0; base < n; base += kScanThreads * kScanPer) {
-    const uint32_t lo = base + t * kScanPer;
-    uint32_t c[kScanPer];
-    if (lo + kScanPer <= n) {
-      const uint4* c4 = reinterpret_cast<const uint4*>(counts + lo);  // 64-byte aligned
+// The emit pass's offsets, in two levels: group_sum_kernel sums the probe's block counts in
+// groups of kScanGroup blocks (one workgroup per group, fully parallel); an emit block adds the
+// sums of the groups before its own and the counts before it in its group (one wave, a few
+// loads per lane). Measured alternatives (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us;
+// a ticket letting the probe's last block scan, 0.6 ms (20k atomics on one address
+// serialize); a one-block scan kernel, ~18 us (a single CU's dependent round trips).
+constexpr uint32_t kScanGroup = 256;
+__global__ __launch_bounds__(256) void group_sum_kernel(const uint32_t* __restrict__ counts,
+                                                        uint64_t* __restrict__ group_sum,
+                                                        uint32_t n) {
+  __shared__ uint32_t ws[kWavesPerBlock];
+  const uint32_t i = blockIdx.x * kScanGroup + threadIdx.x;
+  const uint32_t v = wave_sum(i < n ? counts[i] : 0u);  // <= 512 hits per block: fits u32
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) group_sum[blockIdx.x] = (uint64_t)ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Exclusive prefix of block b's count (wave 0 of the emit block; wave-uniform result).
+__device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b) {
+  const uint32_t lane = threadIdx.x & 63, g = b / kScanGroup;
+  uint64_t s = 0;
+  for (uint32_t i = lane; i < g; i += 64) s += a.group_sum[i];
+  for (uint32_t i = g * kScanGroup + lane; i < b; i += 64) s += a.block_counts[i];
 #pragma unroll
-      for (int i = 0; i < kScanPer / 4; ++i) {
-        const uint4 v = c4[i];
-        c[4 * i] = v.x, c[4 * i + 1] = v.y, c[4 * i + 2] = v.z, c[4 * i + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < kScanPer; ++i) c[i] = lo + i < n ? counts[lo + i] : 0u;
-    }
-    uint64_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) sum += c[i];
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < kScanThreads; d <<= 1) {  // inclusive Hillis-Steele scan
-      const uint64_t v = t >= d ? part[t - d] : 0;
-      __syncthreads();
-      part[t] += v;
-      __syncthreads();
-    }
-    uint64_t run = carry + part[t] - sum;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-      if (lo + i < n) prefix[lo + i] = run;
-      run += c[i];
-    }
-    carry += part[kScanThreads - 1];
-    __syncthreads();  // part is rewritten by the next tile
-  }
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  return s;
 }
 
 // Emit pass: block b's staged hits go to out[prefix[b] ..], those past `cap` are dropped; the
 // last block publishes the total (the caller compares it with cap).
 __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a) {
+  __shared__ uint64_t off;
   const uint32_t n = a.block_counts[blockIdx.x];
-  const uint64_t p0 = a.prefix[blockIdx.x];
+  if (threadIdx.x < 64) {
+    const uint64_t o = emit_offset(a, blockIdx.x);
+    if (threadIdx.x == 0) off = o;
+  }
+  __syncthreads();
+  const uint64_t p0 = off;
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *a.n_hits = p0 + n;
   const uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
   const uint64_t base = a.offsets[0];
@@ -1172,8 +1141,8 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
 }
 
 hipError_t launch_contig_scan(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
-  hipLaunchKernelGGL(contig_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, a.block_counts,
-                     const_cast<uint64_t*>(a.prefix), (uint32_t)n_blocks);
+  hipLaunchKernelGGL(group_sum_kernel, dim3((unsigned)((n_blocks + kScanGroup - 1) / kScanGroup)),
+                     dim3(256), 0, stream, a.block_counts, a.group_sum, (uint32_t)n_blocks);
   return hipGetLastError();
 }
 
