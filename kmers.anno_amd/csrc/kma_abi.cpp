@@ -845,14 +845,19 @@ struct PhaseClock {
 const char* const kDirectPhases[] = {"annotate_kernel"};
 const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
-// Proteins per annotate_kernel block: 4 (KMA_BLOCK_PROTEINS=1..8 overrides, read per call).
-// Measured on MI355X (profiles/r02f_block_proteins.log): c2 65.1 / 65.5 / 65.6 / 73.9 us and c5
-// 4.53 / 4.53 / 4.66 / 4.86 ms for the automatic tail-minimising choice / 4 / 6 / 8 per block:
-// the partial last wave of blocks at c2 is not what bounds it, so the simple 4 stays.
-uint32_t block_proteins() {
+// Proteins per annotate_kernel block (KMA_BLOCK_PROTEINS=1..8 overrides, read per call): 6 for
+// batches of more than 4 resident waves of such blocks, else 4. A block's fixed costs (the
+// offsets and first residues round trips, the final chain walks, the vote) are amortized over
+// more probe steps with more proteins, while a batch of few waves of blocks ends with a longer
+// tail. Measured on MI355X (profiles/r03_ab/r03m, r03n): c5 3.94 / 3.77 / 3.88 ms at 4 / 6 / 8
+// (3.87 / 3.72 / 3.84 with queued keys), c2 51 vs 66 us at 4 vs 6. (Round 2, before the walk
+// queue and the scratch fix: c5 4.53 / 4.66 / 4.86 ms at 4 / 6 / 8, r02f_block_proteins.log.)
+uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq) {
   const char* e = getenv("KMA_BLOCK_PROTEINS");
   const int f = (e && *e) ? atoi(e) : 0;
-  return (f >= 1 && f <= kma::kBlockProteins) ? (uint32_t)f : 4u;
+  if (f >= 1 && f <= kma::kBlockProteins) return (uint32_t)f;
+  const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
+  return (uint64_t)n_seq / 6 > 4 * slots ? 6u : 4u;
 }
 
 // Deferral of short groups (annotate_kernel's two-pass grid), in probe steps: groups below it
@@ -865,7 +870,7 @@ uint32_t block_proteins() {
 // even, 100k (14) 3% slower, c4 / c5 7% / 3% slower when forced. KMA_DEFER=0 disables it,
 // KMA_DEFER=<steps> forces it on any batch (read per call).
 uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
-  const uint64_t slots = 7ull * (uint64_t)std::max(ws->n_cu, 1);
+  const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
   const char* e = getenv("KMA_DEFER");
   if (e && *e) return (uint32_t)std::max(0, std::min(64, atoi(e)));
   return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
@@ -895,7 +900,7 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
-  a.block_proteins = block_proteins();
+  a.block_proteins = block_proteins(ws, n_seq);
   a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
   a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
   PhaseClock clk(ws, s, kDirectPhases, 1);

@@ -201,15 +201,22 @@ __device__ __forceinline__ bool walk_chain_wide(const uint64_t* __restrict__ slo
     uint4 q[kWideSlots];
 #pragma unroll
     for (int i = 0; i < kWideSlots; ++i) q[i] = bp[i];
-    bool empty = false;
+    // selects, not an early return per slot: that one is compiled into a dynamically indexed
+    // copy of q in scratch memory
+    bool empty = false, found = false;
+    uint32_t z = 0, at = 0;
 #pragma unroll
     for (int i = 0; i < kWideSlots; ++i) {
-      if (q[i].x == klo && q[i].y == khi) {
-        fid = q[i].z & kFidMask;
-        sid = b * kWideSlots + i;
-        return true;
-      }
+      const bool m = q[i].x == klo && q[i].y == khi;
+      z = m ? q[i].z : z;
+      at = m ? (uint32_t)i : at;
+      found = found || m;
       empty = empty || q[i].x == 0u;
+    }
+    if (found) {
+      fid = z & kFidMask;
+      sid = b * kWideSlots + at;
+      return true;
     }
     if (empty) return false;
   }

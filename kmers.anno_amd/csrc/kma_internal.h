@@ -249,11 +249,18 @@ constexpr int kSetPool = KMA_SET_POOL;
 #define KMA_LANE_PERM 1
 #endif
 #ifndef KMA_CHAIN_Q
-#define KMA_CHAIN_Q 384
+#define KMA_CHAIN_Q 192
 #endif
-constexpr int kChainQ = KMA_CHAIN_Q;  // deferred overflow-chain walks per wave (u32 positions)
+constexpr int kChainQ = KMA_CHAIN_Q;  // deferred chain walks per wave (8 bytes: key, protein)
+// a step adds at most 64 kProbeWin entries to a wave's queue after a flush check
+static_assert(kChainQ >= 64 * (kProbeWin + 1), "chain queue below two steps of windows");
 constexpr uint32_t kGlobalSet = 0xFFFFFFFFu;  // pset[] marker: the set lives in workspace memory
 constexpr int kWavesPerBlock = 4;
+// annotate_kernel blocks resident per CU (= waves per SIMD): its LDS and VGPR budget.
+#ifndef KMA_PROTEIN_OCC
+#define KMA_PROTEIN_OCC 7
+#endif
+constexpr int kProteinOcc = KMA_PROTEIN_OCC;
 
 struct ProteinArgs {
   const uint64_t* slots;

@@ -173,11 +173,28 @@ __device__ uint64_t g_block_clk[8 * 65536];
 #define KMA_CLK_HW() ((void)0)
 #endif
 
-// Per-block protein records (LDS). The layout keeps 7 blocks per CU resident (<= 23,405 B).
+#ifdef KMA_TUNE_COUNT
+// Tuning builds only (make variant VNAME=count VFLAGS=-DKMA_TUNE_COUNT): wave-level event
+// counts of the protein launches since the last reset (kma_debug_walk_stats): 0 chain flushes,
+// 1 queued walks, 2 probed windows, 3 home-bucket hits, 4 walk hits, 5 walk hits in the
+// chain's first bucket.
+__device__ unsigned long long g_walk_stats[8];
+#define KMA_COUNT(i, v)                                                                    \
+  do {                                                                                     \
+    const unsigned long long kma_v_ = (unsigned long long)(v); /* wave-wide, all lanes */  \
+    if ((threadIdx.x & 63) == 0)                                                           \
+      __hip_atomic_fetch_add(&g_walk_stats[i], kma_v_, __ATOMIC_RELAXED,                   \
+                             __HIP_MEMORY_SCOPE_AGENT);                                    \
+  } while (0)
+#else
+#define KMA_COUNT(i, v) ((void)0)
+#endif
+
+// Per-block protein records (LDS). The layout keeps kProteinOcc blocks per CU resident.
 template <int P>
 struct ProteinSmem {
   __attribute__((aligned(16))) uint32_t pool[kSetPool];  // LDS sets: slot id + 1, 0 = empty
-  uint32_t chain_q[kWavesPerBlock][kChainQ];  // deferred chain walks: position - span start
+  uint32_t chain_q[kWavesPerBlock][2 * kChainQ];  // deferred chain walks: packed key, protein
   uint32_t pbeg[P + 1];  // protein starts relative to the span start; [np..P] = span end
   uint32_t pwin[P];      // windows of the protein (ProteinKmers: L - K + 1, or L - K)
   uint32_t pset[P];      // set base in `pool`, or kGlobalSet
@@ -186,8 +203,8 @@ struct ProteinSmem {
   uint32_t skip;                       // two-pass grid: the group belongs to the other pass
   uint8_t lut[256];
 };
-static_assert(sizeof(ProteinSmem<kBlockProteins>) <= 163840 / 7,
-              "protein-path LDS must leave 7 blocks per CU");
+static_assert(sizeof(ProteinSmem<kBlockProteins>) <= 163840 / kProteinOcc,
+              "protein-path LDS must leave kProteinOcc blocks per CU");
 
 // Insert slot id + 1 in a set of `cap` u32 entries; true if it was not there.
 __device__ __forceinline__ bool lds_set_insert(uint32_t* set, uint32_t cap, uint32_t key) {
@@ -233,8 +250,8 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs
   if (fresh) atomicAdd(&sm.pcnt[p], 1u);
 }
 
-// Which of the block's proteins holds span position x, and whether x starts one of its
-// windows (pb / pw: the block-uniform starts and window counts, in registers).
+// Which of the block's proteins holds span position x (pb: the block-uniform starts, in
+// scalar registers).
 template <int P>
 __device__ __forceinline__ uint32_t protein_at(const uint32_t (&pb)[P + 1], uint32_t x) {
   uint32_t p = 0;
@@ -242,47 +259,89 @@ __device__ __forceinline__ uint32_t protein_at(const uint32_t (&pb)[P + 1], uint
   for (int i = 1; i < P; ++i) p += x >= pb[i] ? 1u : 0u;
   return p;
 }
+// Whether x (in protein p = protein_at(pb, x)) starts one of p's windows: pe[i] = pb[i] +
+// windows of i <= pb[i + 1], so the proteins whose windows end at or below x are exactly those
+// before p, plus p itself when x is past its last window. A compare count, like protein_at: a
+// select of pe[p] is folded by the compiler into a dynamically indexed private array (scratch
+// memory: 32 bytes per lane stored per block, ~2 GB of writes per c5 launch).
+template <int P>
+__device__ __forceinline__ bool window_at(const uint32_t (&pe)[P], uint32_t x, uint32_t p) {
+  uint32_t ended = 0;
+#pragma unroll
+  for (int i = 0; i < P; ++i) ended += x >= pe[i] ? 1u : 0u;
+  return ended == p;
+}
 
-// The block's proteins [p0, p0 + np) (np <= P), contiguous in the batch. pass 0 / 1: a block
-// of the two-pass grid, which annotates its group only if the group is long (pass 0) / short
-// (pass 1: fewer than defer_below probe steps); pass -1: always.
+// The lane's window within each 256-window slice. KMA_LANE_PERM: quad q's member p takes
+// window 16 p + q of its wave, so that load instruction r (member r of every quad) reads the
+// buckets of 16 consecutive windows — windows that share a minimizer then share a line inside
+// one instruction.
+__device__ __forceinline__ uint32_t lane_window(int t) {
+#if KMA_LANE_PERM
+  return (uint32_t)((t >> 6) * 64 + 16 * (t & 3) + ((t & 63) >> 2));
+#else
+  return (uint32_t)t;
+#endif
+}
+
+// A group's inputs that precede its first probe step: its proteins, the offsets wave 0 reads
+// (lane <= np: offsets[p0 + lane]) and the span start: two dependent round trips with the
+// first residues (offsets, then residues: 4.5 and ~4 us of a ~37 us c5 block at 6 proteins,
+// profiles/r03_ab/r03o block clocks). A persistent grid loading the next group's head under
+// the current group's steps was tried: the group loop cost 48-112 bytes per lane of register
+// spills (scratch memory) at 7 waves per SIMD.
+struct GroupHead {
+  uint32_t p0, np;
+  uint64_t beg_raw;
+  uint64_t span_lo;
+};
+__device__ __forceinline__ void head_offsets(const ProteinArgs& a, uint32_t g, GroupHead& h) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  h.p0 = g * a.block_proteins;  // g < n_groups: p0 < n_seq
+  h.np = min(a.block_proteins, a.n_seq - h.p0);
+  h.beg_raw = wave == 0 && lane <= (int)h.np ? a.offsets[h.p0 + lane] : 0u;
+  h.span_lo = a.offsets[h.p0] - a.offsets[0];
+}
+// The span's residues from the aligned word at or below its first byte (d_residues is 8-byte
+// aligned): window x of the span starts at byte x + mis of `res`.
+__device__ __forceinline__ const uint8_t* head_res(const ProteinArgs& a, const GroupHead& h,
+                                                   uint32_t& mis) {
+  const uint8_t* res0 = a.residues + a.offsets[0] + h.span_lo;
+  mis = (uint32_t)((uintptr_t)res0 & 7u);
+  return res0 - mis;
+}
+// The group's first probe step's residue words (clamped to the batch, which is readable 32
+// bytes past its end; windows past the span are masked in the loop).
+template <int U>
+__device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupHead& h,
+                                              uint32_t tw, WinWords (&ww)[U]) {
+  uint32_t mis;
+  const uint8_t* res = head_res(a, h, mis);
+  const uint64_t lim = a.n_residues - h.span_lo;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint32_t x = j * 256u + tw;
+    ww[j] = window_words(res, (x < lim ? x : 0u) + mis);
+  }
+}
+
+// The group h: proteins [p0, p0 + np) (np <= P), contiguous in the batch, whose first step's
+// residue words are in ww. pass 0 / 1: a block of the two-pass grid, which annotates its group
+// only if the group is long (pass 0) / short (pass 1: fewer than defer_below probe steps);
+// pass -1: always. sm.lut is being loaded (read after the first barrier).
 template <int K, int M, int P>
 __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P>& sm,
-                                               const uint32_t p0, const uint32_t np,
+                                               const GroupHead& h, WinWords (&ww)[kProbeWin],
                                                const int pass = -1) {
   constexpr int U = kProbeWin;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
-  // The lane's window within each 256-window slice. KMA_LANE_PERM: quad q's member p takes
-  // window 16 p + q of its wave, so that load instruction r (member r of every quad) reads the
-  // buckets of 16 consecutive windows — windows that share a minimizer then share a line
-  // inside one instruction.
-#if KMA_LANE_PERM
-  const uint32_t tw = (uint32_t)(wave * 64 + 16 * (lane & 3) + (lane >> 2));
-#else
-  const uint32_t tw = (uint32_t)t;
-#endif
-  // wave 0: the proteins' offsets (issued first); every wave: the span start (scalar)
-  const uint64_t beg_raw = wave == 0 && lane <= (int)np ? a.offsets[p0 + lane] : 0u;
+  const uint32_t tw = lane_window(t);
+  const uint32_t p0 = h.p0, np = h.np;
+  const uint64_t beg_raw = h.beg_raw, span_lo = h.span_lo;
   const uint64_t o0 = a.offsets[0];
-  const uint64_t span_lo = a.offsets[p0] - o0;
-  // The span's residues from the aligned word at or below its first byte (d_residues is
-  // 8-byte aligned): window x of the span starts at byte x + mis of `res`. The first step's
-  // words are loaded now, under the records' round trip (clamped to the batch, which is
-  // readable 32 bytes past its end; windows past the span are masked in the loop).
-  const uint8_t* res0 = a.residues + o0 + span_lo;
-  const uint32_t mis = (uint32_t)((uintptr_t)res0 & 7u);
-  const uint8_t* __restrict__ res = res0 - mis;
-  WinWords ww[U];
-  {
-    const uint64_t lim = a.n_residues - span_lo;
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const uint32_t x = j * 256u + tw;
-      ww[j] = window_words(res, (x < lim ? x : 0u) + mis);
-    }
-  }
-  sm.lut[t] = a.lut[t];
+  uint32_t mis;
+  const uint8_t* __restrict__ res = head_res(a, h, mis);
   if (wave == 0) {  // the block's protein records
     const uint64_t beg = lane <= (int)np ? beg_raw - o0 : 0u;
     const uint64_t end = __shfl_down(beg, 1, 64);
@@ -336,11 +395,11 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   __syncthreads();
   if (pass >= 0 && sm.skip) return;  // block-uniform
   const uint32_t used = sm.chain_q[0][0];
-  uint32_t pb[P + 1], pw[P];
+  uint32_t pb[P + 1], pe[P];
 #pragma unroll
   for (int i = 0; i <= P; ++i) pb[i] = __builtin_amdgcn_readfirstlane(sm.pbeg[i]);
 #pragma unroll
-  for (int i = 0; i < P; ++i) pw[i] = __builtin_amdgcn_readfirstlane(sm.pwin[i]);
+  for (int i = 0; i < P; ++i) pe[i] = __builtin_amdgcn_readfirstlane(sm.pbeg[i] + sm.pwin[i]);
   const uint32_t span = pb[P];
   __syncthreads();  // `used` has been read by every wave
   uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
@@ -360,16 +419,33 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   uint32_t* cq = sm.chain_q[wave];
   uint32_t cn = 0;  // wave-uniform queue length
   constexpr uint32_t stride = 256u * U;
-  // Deferred chain walks: one lane per queued window (re-pack, walk with whole-bucket loads).
+  // Deferred chain walks, 64 queued windows at a time: lane (quad g, member p) takes entry
+  // 16 p + g of the chunk; the chain's first bucket of every entry is loaded and matched by a
+  // quad (the probe loop's cooperative loads: 2 line requests per bucket instead of 8 dwordx4
+  // of one lane), and only an entry whose first chain bucket is full and misses walks on alone.
+  // Deferred chain walks: one lane per queued window (its packed key and protein from the
+  // queue), whole-bucket loads. Measured against alternatives at c5 (profiles/r03_ab): queueing
+  // positions and re-packing the residues 3.955 vs 3.86 ms; the chain's first bucket matched by
+  // quads with cooperative loads 4.01 vs 3.94 ms (6.31 vs 6.35 at load factor 0.9).
   auto chain_flush = [&]() {
     __builtin_amdgcn_wave_barrier();  // queue writes of other lanes are visible (LDS in order)
+    KMA_COUNT(0, 1);
+    KMA_COUNT(1, cn);
     for (uint32_t e = lane; e < cn; e += 64) {
-      const uint32_t x = cq[e];
-      uint64_t key;
-      pack_window<K>(lut, window_bytes(res, x + mis), key);
+      const uint32_t w2 = cq[2 * e + 1];
+      const uint64_t key = (uint64_t)(w2 & 0xFFu) << 32 | cq[2 * e];
+      const uint32_t p = w2 >> 8;
       uint32_t fid = 0, sid = 0;
-      if (walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid))
-        record_hit<P>(sm, a, span_lo, multiset, protein_at<P>(pb, x), fid, sid);
+      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid);
+      if (hit) record_hit<P>(sm, a, span_lo, multiset, p, fid, sid);
+#ifdef KMA_TUNE_COUNT
+      {
+        const uint32_t s1 = chain_bucket(home_bucket(key, K, M, nb), 1u, nb);
+        const bool first = hit && sid / kSlotsPerBucket == s1;  // resolved in chain step 1
+        KMA_COUNT(4, __popcll(__ballot(hit)));
+        KMA_COUNT(5, __popcll(__ballot(first)));
+      }
+#endif
     }
     __builtin_amdgcn_wave_barrier();
     cn = 0;
@@ -384,15 +460,9 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     for (int j = 0; j < U; ++j) {
       const uint32_t x = xs + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
-      uint32_t pbp = pb[0], pwp = pw[0];
-#pragma unroll
-      for (int i = 1; i < P; ++i) {
-        pbp = p == (uint32_t)i ? pb[i] : pbp;
-        pwp = p == (uint32_t)i ? pw[i] : pwp;
-      }
       uint64_t key;
       const bool ok = pack_window<K>(lut, funnel(ww[j].lo, ww[j].hi, ww[j].sh), key) &&
-                      x < span && x - pbp < pwp;
+                      x < span && window_at<P>(pe, x, p);
       o.klo[j] = (uint32_t)key;
       o.khi[j] = (uint32_t)(key >> 32) << 24;
       o.need[j] = filter_need<kSlotsPerBucket>(o.klo[j]);
@@ -446,6 +516,10 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     for (int j = 0; j < U; ++j) {
       const bool probed = c.bk[j] != kNone;
       const uint32_t w = probed ? word[j] : 0u;
+#ifdef KMA_TUNE_COUNT
+      KMA_COUNT(2, __popcll(__ballot(probed)));
+      KMA_COUNT(3, __popcll(__ballot((w & kWordFid) != 0u)));
+#endif
       if (w & kWordFid)
         record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, (w & kWordFid) - 1u,
                       (c.bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
@@ -456,7 +530,11 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const bool pend = probed && w == 0u;
 #endif
       const uint64_t m = __ballot(pend);
-      if (pend) cq[cn + popc_below(m)] = x0 + j * 256u + tw;
+      if (pend) {  // queue entry: key bits 0..31; key bits 32..39 | protein << 8
+        const uint32_t e = cn + popc_below(m);
+        cq[2 * e] = c.klo[j];
+        cq[2 * e + 1] = (c.khi[j] >> 24) | (c.bk[j] >> kBucketBits) << 8;
+      }
       cn += (uint32_t)__popcll(m);
     }
     if (cn > (uint32_t)(kChainQ - 64 * U)) chain_flush();
@@ -472,7 +550,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     gather(cur, q);
     // next step's residues (issued after the bucket loads: waiting for those leaves these in
     // flight, vmcnt counts in order)
-    load_residues(x0 + stride);
+    load_residues(x0 + stride);  // (past the span: clamped to its first word)
     settle(x0, cur, q);
     if (x0 == 0) KMA_CLK(2);
   }
@@ -502,21 +580,41 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 }
 
 template <int K, int M, int P>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void annotate_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kProteinOcc, 8))) void annotate_kernel(
     ProteinArgs a) {
   __shared__ ProteinSmem<P> sm;
+  KMA_CLK(0);
+  const int t = threadIdx.x;
+  sm.lut[t] = a.lut[t];  // read after annotate_block's first barrier
   // Two-pass grid (defer_below > 0): blocks [0, n_groups) annotate the long groups, blocks
   // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
   // one (blocks are dispatched in index order); a block whose group is the other pass's exits
   // after reading its offsets.
-  KMA_CLK(0);
   const bool second = a.defer_below && blockIdx.x >= a.n_groups;
-  const uint32_t p0 = (blockIdx.x - (second ? a.n_groups : 0u)) * a.block_proteins;
-  annotate_block<K, M, P>(a, sm, p0, min(a.block_proteins, a.n_seq - p0),
-                          a.defer_below ? (second ? 1 : 0) : -1);
+  GroupHead h;
+  WinWords ww[kProbeWin];
+  head_offsets(a, blockIdx.x - (second ? a.n_groups : 0u), h);
+  head_residues<kProbeWin>(a, h, lane_window(t), ww);
+  annotate_block<K, M, P>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
   KMA_CLK(5);
   KMA_CLK_HW();
 }
+
+#ifdef KMA_TUNE_COUNT
+}  // namespace
+}  // namespace kma
+extern "C" int kma_debug_walk_stats(uint64_t* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kma::g_walk_stats), 64, 0,
+                                     hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) {
+    const uint64_t z[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(kma::g_walk_stats), z, 64, 0, hipMemcpyHostToDevice);
+  }
+  return (int)e;
+}
+namespace kma {
+namespace {
+#endif
 
 #ifdef KMA_BLOCK_CLOCK
 }  // namespace
@@ -1039,7 +1137,7 @@ struct AnnotateLaunch {
     const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= (uint32_t)P ? a.block_proteins : 4u;
     if (bp != a.block_proteins) return hipErrorInvalidValue;
     const unsigned blocks = (a.n_seq + bp - 1) / bp;
-    if (a.defer_below && a.n_groups != blocks) return hipErrorInvalidValue;
+    if (a.n_groups != blocks) return hipErrorInvalidValue;
     hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(a.defer_below ? 2 * blocks : blocks),
                        dim3(256), 0, stream, a);
     return hipGetLastError();
