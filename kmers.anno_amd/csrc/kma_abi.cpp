@@ -251,9 +251,16 @@ struct kma_workspace {
   uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
   uint64_t res_cap = 0;        // residues per call
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
-  uint64_t* d_cstage = nullptr;
+  kma_hit* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
+  // Emit-offset group sums, two buffers of cgroups: the probe of a call adds into buffer
+  // cparity, its emit pass zeroes the other one's first cdirty[1 - cparity] entries (what the
+  // call before it used) and flips cparity.
   uint64_t* d_cprefix = nullptr;
+  uint64_t cgroups = 0;
+  uint64_t cdirty[2] = {0, 0};
+  int cparity = 0;
+  bool cpending = false;  // a probe was set up whose emit pass has not been enqueued
   uint64_t contig_cap = 0;  // bases
   // Per-phase timing (kma_workspace_timing): a ring of calls, each kMaxEv events (phase i runs
   // from event i to event i + 1) and its phase names.
@@ -808,21 +815,35 @@ kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace*
   a.mlen = t->mlen;
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
-  a.group_sum = ws->d_cprefix;
+  if (ws->cpending) {  // an earlier call failed between its probe and its emit: start clean
+    (void)hipDeviceSynchronize();  // the failed call's probe may still be adding
+    (void)hipMemset(ws->d_cprefix, 0, 2 * ws->cgroups * 8);
+    ws->cdirty[0] = ws->cdirty[1] = 0;
+  }
+  ws->cpending = true;
+  a.group_sum = ws->d_cprefix + ws->cparity * ws->cgroups;
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
   return a;
 }
 
-// Group sums of the probe's block counts + canonical-order emission (after the probe on s).
-int enqueue_contig_emit(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
-                        hipStream_t s) {
-  KMA_HIP(kma::launch_contig_scan(a, contig_blocks(a.total_bases), s));
+// Canonical-order emission after the probe on s (whose atomics summed the block counts into
+// ws's current group-sum buffer); zeroes the other buffer for the next call and flips parity.
+int enqueue_contig_emit(kma_workspace* ws, kma::ContigArgs a, kma_hit* d_hits, uint64_t cap,
+                        uint64_t* d_n_hits, hipStream_t s) {
+  const uint64_t nb = contig_blocks(a.total_bases);
+  const int other = 1 - ws->cparity;
+  a.group_zero = ws->d_cprefix + other * ws->cgroups;
+  a.n_zero = ws->cdirty[other];
+  ws->cdirty[other] = 0;
+  ws->cdirty[ws->cparity] = (nb + kma::kScanGroup - 1) / kma::kScanGroup;
+  ws->cparity = other;
   a.out = d_hits;
   a.cap = d_hits ? cap : 0;
   a.n_hits = d_n_hits;
-  KMA_HIP(kma::launch_contigs_emit(a, contig_blocks(a.total_bases), s));
+  KMA_HIP(kma::launch_contigs_emit(a, nb, s));
+  ws->cpending = false;
   return KMA_OK;
 }
 
@@ -1048,9 +1069,14 @@ int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   free_contig_scratch(ws);
   const uint64_t nb = contig_blocks(n_bases);
-  KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * 8));
-  KMA_HIP(hipMalloc(&ws->d_ccounts, nb * 4));
-  KMA_HIP(hipMalloc(&ws->d_cprefix, nb * 8));
+  const uint64_t ng = (nb + kma::kScanGroup - 1) / kma::kScanGroup;
+  KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * sizeof(kma_hit)));
+  KMA_HIP(hipMalloc(&ws->d_ccounts, ng * kma::kScanGroup * 4));
+  KMA_HIP(hipMalloc(&ws->d_cprefix, 2 * ng * 8));
+  KMA_HIP(hipMemset(ws->d_cprefix, 0, 2 * ng * 8));
+  ws->cgroups = ng;
+  ws->cdirty[0] = ws->cdirty[1] = 0;
+  ws->cparity = 0;
   ws->contig_cap = nb * kma::kContigTile;
   return KMA_OK;
 }
@@ -1258,7 +1284,7 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
   const uint64_t nb = contig_blocks(n_bases);
   KMA_HIP(kma::launch_contigs_probe(a, nb, s));
   KMA_HIP(clk.mark());
-  const int rc = enqueue_contig_emit(a, d_hits, cap, d_n_hits, s);
+  const int rc = enqueue_contig_emit(ws, a, d_hits, cap, d_n_hits, s);
   if (rc == KMA_OK) KMA_HIP(clk.mark());
   return rc;
 }
@@ -1317,12 +1343,15 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
     KMA_HIP(hipMemsetAsync(c->d_aux.p, 0, n_slots * 4, s));
     a.slot_count = c->d_aux.p;
     a.strict_pass = 1;  // count every table key's locations
+    uint64_t* const gs = a.group_sum;
+    a.group_sum = nullptr;  // no emit follows this pass
     KMA_HIP(kma::launch_contigs_probe(a, nb, s));
+    a.group_sum = gs;
     a.strict_pass = 2;  // keep keys with exactly one location
   }
   KMA_HIP(kma::launch_contigs_probe(a, nb, s));
   if (!out_hits) {  // pass 1: count (and tally)
-    if (int rc = enqueue_contig_emit(a, nullptr, 0, d_n, s)) return rc;
+    if (int rc = enqueue_contig_emit(c->ws, a, nullptr, 0, d_n, s)) return rc;
     KMA_HIP(c->h_out.reserve(16 + tb));
     KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
     if (tb) KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, d_tally, tb, hipMemcpyDeviceToHost, s));
@@ -1334,7 +1363,7 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
   // pass 2: emit into d_hits (sized by pass 1's count, passed in *n_hits)
   const uint64_t cap = *n_hits;
   KMA_HIP(c->d_hits.reserve(std::max<uint64_t>(cap, 1)));
-  if (int rc = enqueue_contig_emit(a, c->d_hits.p, cap, d_n, s)) return rc;
+  if (int rc = enqueue_contig_emit(c->ws, a, c->d_hits.p, cap, d_n, s)) return rc;
   KMA_HIP(c->h_out.reserve(16 + cap * sizeof(kma_hit)));
   KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
   KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, c->d_hits.p, cap * sizeof(kma_hit),

@@ -46,8 +46,9 @@ __device__ __forceinline__ uint64_t window_bytes(const uint8_t* __restrict__ res
   const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
   return funnel(src[0], src[1], (uint32_t)(pos & 7) * 8u);
 }
-// The two aligned words of a window, combined later (funnel) so that the load is not consumed
-// in the step that issues it.
+// The two aligned words of a window, combined later (win_bytes: a funnel shift) so that the
+// load is not consumed in the step that issues it. (One unaligned 8-byte load per window saves
+// 3 VGPRs and measured 1% slower at c5, profiles/r03t/.)
 struct WinWords {
   uint64_t lo, hi;
   uint32_t sh;
@@ -56,6 +57,7 @@ __device__ __forceinline__ WinWords window_words(const uint8_t* __restrict__ res
   const uint64_t* src = reinterpret_cast<const uint64_t*>(res + (pos & ~7ull));
   return WinWords{src[0], src[1], (uint32_t)(pos & 7) * 8u};
 }
+__device__ __forceinline__ uint64_t win_bytes(const WinWords& w) { return funnel(w.lo, w.hi, w.sh); }
 
 // 5-bit packing through the table's residue LUT (LDS); false if a byte is not encodable.
 template <int K>
@@ -157,8 +159,8 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 // in a table, so at most one lane matches and OR is the reduction. Every lane of the quad must
 // call it (DPP). Branch-free on purpose: a short-circuit here lets the compiler split the
 // 16-byte loads into a lazily loaded tail behind a branch and a vmcnt(0).
-__device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
-                                               uint32_t kh, uint32_t need, uint32_t part) {
+__device__ __forceinline__ uint32_t match_part_raw(const uint4 (&v)[kBucketHalves], uint32_t kl,
+                                                   uint32_t kh, uint32_t need, uint32_t part) {
   constexpr uint32_t FB = kFilterBits, PM = (1u << (2 * FB)) - 1;  // positions per lane, half
   uint32_t w = 0, missing = 0;
 #pragma unroll
@@ -174,19 +176,40 @@ __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], 
     missing |= want & ~held;
   }
   w |= missing ? kAbsent : 0u;
-  return quad_or(w);
+  return w;
+}
+__device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
+                                               uint32_t kh, uint32_t need, uint32_t part) {
+  return quad_or(match_part_raw(v, kl, kh, need, part));
+}
+
+// Reduce-scatter over a quad of the four buckets' lane verdicts a[r] (match_part_raw): lane
+// `part` returns the OR over the quad of a[part], i.e. its own window's verdict, by a two-round
+// butterfly (3 DPP + 3 OR + 6 lane-constant selects) in place of four quad_or and a select per
+// bucket (8 DPP + 8 OR + 4 selects).
+#ifndef KMA_QUAD_XPOSE
+#define KMA_QUAD_XPOSE 1
+#endif
+__device__ __forceinline__ uint32_t quad_reduce_scatter(const uint32_t (&a)[4], uint32_t part) {
+  const bool hi2 = (part & 2u) != 0u, hi1 = (part & 1u) != 0u;
+  const uint32_t s0 = hi2 ? a[0] : a[2], s1 = hi2 ? a[1] : a[3];  // the partner's half
+  const uint32_t k0 = hi2 ? a[2] : a[0], k1 = hi2 ? a[3] : a[1];  // mine: r = (part & 2) | 0, 1
+  const uint32_t b0 = k0 | (uint32_t)__builtin_amdgcn_mov_dpp((int)s0, 0x4E, 0xF, 0xF, false);
+  const uint32_t b1 = k1 | (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0x4E, 0xF, 0xF, false);
+  const uint32_t sn = hi1 ? b0 : b1, kp = hi1 ? b1 : b0;
+  return kp | (uint32_t)__builtin_amdgcn_mov_dpp((int)sn, 0xB1, 0xF, 0xF, false);
 }
 
 // Wide tables (K > 8, kma_internal.h): lane `part` of the quad holds slot `part` of the bucket
 // in v (and its filter positions 2part .. in .z); same verdict word as match_part.
-__device__ __forceinline__ uint32_t match_wide(const uint4& v, uint32_t kl, uint32_t kh,
-                                               uint32_t need, uint32_t part) {
+__device__ __forceinline__ uint32_t match_wide_raw(const uint4& v, uint32_t kl, uint32_t kh,
+                                                   uint32_t need, uint32_t part) {
   const uint32_t m = (uint32_t)(v.x == kl) & (uint32_t)(v.y == kh);
   uint32_t w = m * ((v.z & kFidMask) + 1u) | m * (part << kSlotShift);
   const uint32_t held = (v.z >> kFidBits) & ((1u << kFilterBits) - 1u);
   const uint32_t want = (need >> (kFilterBits * part)) & ((1u << kFilterBits) - 1u);
   w |= (want & ~held) ? kAbsent : 0u;
-  return quad_or(w);
+  return w;
 }
 
 // walk_chain for wide tables: whole 64-byte buckets of four 16-byte slots, one at a time.
@@ -231,7 +254,13 @@ constexpr uint32_t kBucketIdx = (1u << kBucketBits) - 1u;
 
 // Set-entry index of `key` in a set of `cap` entries (fast range, any capacity).
 __device__ __forceinline__ uint32_t set_slot(uint32_t key, uint32_t cap) {
+#if KMA_HASH_LITE
+  uint32_t h = key * 0x9E3779B1u;
+  h ^= h >> 16;
+  return (uint32_t)(((uint64_t)h * cap) >> 32);
+#else
   return (uint32_t)(((uint64_t)mix32(key * 0x9E3779B1u) * cap) >> 32);
+#endif
 }
 
 }  // namespace

@@ -65,11 +65,26 @@ __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
 // Filter position h (0 .. kFilterBits - 1) of a key in a bucket of S slots (from the key's low
 // dword): position i lives in slot i / kFilterBits, at bit kFidBits + i % kFilterBits of the
 // slot's high dword (narrow) or .z (wide).
+// KMA_HASH_LITE (default 1): the probe's per-window hashes use one 32-bit multiply each where
+// round 3's first build used two to four (the protein and 6-frame probes issue a VALU
+// instruction every ~4 cycles per SIMD: c5 3,107 VALU instructions per wave, profiles/r03q_sq/).
+// Both filter positions come from one product; the minimizer order is a multiplicative hash of
+// the m-mer (a bijection: no ties); the home bucket a one-multiply mix of the minimizer; the
+// paired-home bit the key's parity. c5: 3.84 vs 4.04 ms and 3.99 vs 4.11 ms against the
+// murmur hashes on two boxes, displaced keys 7.58% vs 7.70% (profiles/r03r/, r03s/).
+#ifndef KMA_HASH_LITE
+#define KMA_HASH_LITE 1
+#endif
 template <int S>
 __host__ __device__ inline uint32_t filter_pos(uint32_t klo, int h) {
   constexpr int bits = (S * kFilterBits == 32) ? 5 : (S * kFilterBits == 16) ? 4
                      : (S * kFilterBits == 8) ? 3 : 2;
+#if KMA_HASH_LITE
+  const uint32_t x = klo * 0x9E3779B1u;
+  return h ? (x >> (32 - 2 * bits)) & ((1u << bits) - 1u) : x >> (32 - bits);
+#else
   return ((klo * (h ? 0x85EBCA77u : 0x9E3779B1u)) + (h ? 0x165667B1u : 0u)) >> (32 - bits);
+#endif
 }
 // The key's filter positions as a mask over the bucket's S * kFilterBits positions (computed
 // once per window by its lane and broadcast to the quad that probes it).
@@ -105,6 +120,19 @@ __host__ __device__ inline uint32_t mix32(uint32_t h) {  // murmur3 fmix32
   h ^= h >> 16;
   return h;
 }
+__host__ __device__ inline uint32_t mix32_lite(uint32_t h) {  // one multiply
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  return h;
+}
+__host__ __device__ inline uint32_t parity32(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return (uint32_t)__popc(x) & 1u;
+#else
+  return (uint32_t)__builtin_popcount(x) & 1u;
+#endif
+}
 
 // Minimizer of a packed K-mer: the smallest hash over its K - m + 1 m-mers (5-bit residue
 // codes, first residue most significant). m is a table property (minimizer_len below).
@@ -113,7 +141,11 @@ __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
   uint32_t best = 0xFFFFFFFFu;
   for (int p = 0; p <= k - m; ++p) {
     const uint32_t sub = (uint32_t)(key >> (5 * (k - m - p))) & mask;
+#if KMA_HASH_LITE
+    const uint32_t h = sub * 0x9E3779B1u;
+#else
     const uint32_t h = mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
+#endif
     best = best < h ? best : h;
   }
   return best;
@@ -140,13 +172,22 @@ __host__ __device__ inline uint32_t home_from_hash(uint32_t h, uint64_t key, int
                                                    uint32_t n_buckets) {
   if (KMA_PAIR_HOME && m != 0 && n_buckets >= 2) {
     const uint32_t pair = (uint32_t)(((uint64_t)h * (n_buckets >> 1)) >> 32);
+#if KMA_HASH_LITE
+    return 2u * pair + parity32((uint32_t)key);
+#else
     return 2u * pair + (((uint32_t)key * 0x2C1B3C6Du) >> 31);
+#endif
   }
   return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
 }
 __host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
+#if KMA_HASH_LITE
+  const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
+                            : mix32_lite(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
+#else
   const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
                             : mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
+#endif
   return home_from_hash(h, key, m, n_buckets);
 }
 
@@ -297,9 +338,12 @@ struct ContigArgs {
   uint64_t total_bases;        // offsets[n_contig] - offsets[0] (< 2^39)
   int32_t k;
   int32_t mlen;
-  uint64_t* staging;           // n_blocks x kContigTile*2 packed hits (relative position)
-  uint32_t* block_counts;      // n_blocks
-  uint64_t* group_sum;         // ceil(n_blocks / 256): sums of 256 block counts (emit offsets)
+  kma_hit* staging;            // n_blocks x kContigTile*2 final hit records (block order)
+  uint32_t* block_counts;      // n_blocks (allocated in whole groups of kScanGroup)
+  uint64_t* group_sum;         // ceil(n_blocks / kScanGroup) group sums, zero before the probe
+                               // (which adds its block counts; null: no emit follows)
+  uint64_t* group_zero;        // emit pass: the other parity's group sums, zeroed [0, n_zero)
+  uint64_t n_zero;
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order
@@ -319,6 +363,7 @@ struct ContigArgs {
 // VGPRs (4 waves/SIMD) and measured slower at c3 (0.139 vs 0.124 ms, profiles/r02i_variants.log).
 constexpr int kContigPos = KMA_CONTIG_POS;
 constexpr int kContigTile = 256 * kContigPos;  // forward positions per block
+constexpr uint32_t kScanGroup = 256;  // probe blocks per emit-offset group sum
 
 // ---- the projector's proposal sweep (kma_proposals.hip) ----------------------------------------
 struct PropArgs {
@@ -350,7 +395,6 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
-hipError_t launch_contig_scan(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 // Peg-kmer singleton table (KmerReference.countPegKmers + CountMap.getSingletons): every
 // window i < L-K without 'X' of every peg -> (key or 0, peg index) per residue position; sort;

@@ -461,7 +461,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const uint32_t x = xs + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
       uint64_t key;
-      const bool ok = pack_window<K>(lut, funnel(ww[j].lo, ww[j].hi, ww[j].sh), key) &&
+      const bool ok = pack_window<K>(lut, win_bytes(ww[j]), key) &&
                       x < span && window_at<P>(pe, x, p);
       o.klo[j] = (uint32_t)key;
       o.khi[j] = (uint32_t)(key >> 32) << 24;
@@ -500,6 +500,8 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       word[j] = 0;
+      uint32_t raw[4];
+      (void)raw;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t kl = r == 0 ? quad_bcast<0>(c.klo[j]) : r == 1 ? quad_bcast<1>(c.klo[j])
@@ -508,9 +510,16 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
                           : r == 2 ? quad_bcast<2>(c.khi[j]) : quad_bcast<3>(c.khi[j]);
         const uint32_t nd = r == 0 ? quad_bcast<0>(c.need[j]) : r == 1 ? quad_bcast<1>(c.need[j])
                           : r == 2 ? quad_bcast<2>(c.need[j]) : quad_bcast<3>(c.need[j]);
+#if KMA_QUAD_XPOSE
+        raw[r] = match_part_raw(q[j][r], kl, kh, nd, part);
+#else
         const uint32_t v = match_part(q[j][r], kl, kh, nd, part);
         word[j] = part == r ? v : word[j];
+#endif
       }
+#if KMA_QUAD_XPOSE
+      word[j] = quad_reduce_scatter(raw, part);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -685,7 +694,8 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
 }
 
 template <int K, int M>
-__global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void contigs_probe_quad_kernel(
+    ContigArgs a) {
   // K > 8: a wide table (16-byte slots, kma_internal.h): one slot per lane of the quad.
   constexpr bool kWide = wide_k(K);
   constexpr int kS = kWide ? kWideSlots : kSlotsPerBucket;   // slots per bucket
@@ -700,7 +710,10 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
   __shared__ uint32_t wave_tot[kWavesPerBlock * kContigPos];
   __shared__ uint8_t codon[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
-  const uint64_t base = a.offsets[0], end = base + a.total_bases;
+  // offsets[0] through the constant address space: a scalar load (every block reads it, so the
+  // scalar cache serves it) in place of a vector round trip before the tile's DNA load
+  const uint64_t base = ((const __attribute__((address_space(4))) uint64_t*)a.offsets)[0];
+  const uint64_t end = base + a.total_bases;
   const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
   const uint32_t nb = a.n_buckets;
   KMA_CLK(0);
@@ -762,8 +775,25 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
 #else
   const uint32_t tp = (uint32_t)t;
 #endif
+  // Contig, offset in it and its length of the tile's forward position tt (g < end).
+  auto locate = [&](uint32_t tt, uint32_t& c, int64_t& x, int64_t& len) {
+    const uint64_t g = base + r0 + tt;
+    if (nc <= (uint32_t)kOffCache) {
+      uint32_t lo = 0, hi = nc;  // largest i < nc with offc[i] <= g
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offc[mid] <= g) lo = mid; else hi = mid;
+      }
+      c = c_lo + lo;
+      x = (int64_t)(g - offc[lo]);
+      len = (int64_t)(offc[lo + 1] - offc[lo]);
+    } else {
+      c = contig_of(a.offsets, a.n_contig, g);
+      x = (int64_t)(g - a.offsets[c]);
+      len = (int64_t)(a.offsets[c + 1] - a.offsets[c]);
+    }
+  };
   uint32_t contig[CP];
-  int64_t xs[CP], lens[CP];
   uint64_t key[CP][2];
   uint32_t bk[CP][2];
 #pragma unroll
@@ -772,24 +802,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     const uint64_t g = base + r0 + tt;
     contig[h] = c_lo;
     int64_t x = 0, len = 0;
-    if (g < end) {
-      if (nc <= (uint32_t)kOffCache) {
-        uint32_t lo = 0, hi = nc;  // largest i < nc with offc[i] <= g
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (offc[mid] <= g) lo = mid; else hi = mid;
-        }
-        contig[h] = c_lo + lo;
-        x = (int64_t)(g - offc[lo]);
-        len = (int64_t)(offc[lo + 1] - offc[lo]);
-      } else {
-        contig[h] = contig_of(a.offsets, a.n_contig, g);
-        x = (int64_t)(g - a.offsets[contig[h]]);
-        len = (int64_t)(a.offsets[contig[h] + 1] - a.offsets[contig[h]]);
-      }
-    }
-    xs[h] = x;
-    lens[h] = len;
+    if (g < end) locate(tt, contig[h], x, len);
     bool pv = g < end && x + 3 * K + 3 <= len, mv = g < end && x >= 3 && x + 3 * K <= len;
     key[h][0] = key[h][1] = 0;
 #pragma unroll
@@ -829,7 +842,7 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
       const uint32_t klo = (uint32_t)key[h][j];
       const uint32_t khi = kWide ? (uint32_t)(key[h][j] >> 32) : (uint32_t)(key[h][j] >> 32) << 24;
       const uint32_t need = filter_need<kS>(klo);
-      uint32_t word = 0;
+      uint32_t raw[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const uint32_t kl = rr == 0 ? quad_bcast<0>(klo) : rr == 1 ? quad_bcast<1>(klo)
@@ -838,11 +851,10 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
                           : rr == 2 ? quad_bcast<2>(khi) : quad_bcast<3>(khi);
         const uint32_t nd = rr == 0 ? quad_bcast<0>(need) : rr == 1 ? quad_bcast<1>(need)
                           : rr == 2 ? quad_bcast<2>(need) : quad_bcast<3>(need);
-        uint32_t v;
-        if constexpr (kWide) v = match_wide(q[h][j][rr][0], kl, kh, nd, part);
-        else v = match_part(q[h][j][rr], kl, kh, nd, part);
-        word = part == rr ? v : word;
+        if constexpr (kWide) raw[rr] = match_wide_raw(q[h][j][rr][0], kl, kh, nd, part);
+        else raw[rr] = match_part_raw(q[h][j][rr], kl, kh, nd, part);
       }
+      const uint32_t word = quad_reduce_scatter(raw, part);
       const uint32_t w = bk[h][j] != kNone ? word : 0u;
       hit[h][j] = (w & kWordFid) != 0u;
       fid[h][j] = (w & kWordFid) - 1u;
@@ -860,8 +872,6 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
       if (a.tally && hit[h][j] && fid[h][j] < a.n_fid)
         atomicAdd(a.tally + (uint64_t)contig[h] * a.n_fid + fid[h][j], 1u);
     }
-  (void)xs;
-  (void)lens;
   KMA_CLK(4);  // matched (chain walks done)
 #if KMA_LANE_PERM
   {  // back to position order: lane t takes position t's verdicts
@@ -891,8 +901,10 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
     if (lane == 0) wave_tot[h * kWavesPerBlock + wave] = (uint32_t)(__popcll(bp[h]) + __popcll(bm[h]));
   }
   __syncthreads();
+  // Staged records are the final kma_hit (the emit pass only copies them): contig, left =
+  // KmerPosition.calcLeft, fid, strand and frame (KmerPosition.java:50-93).
   uint32_t total = 0;
-  uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
+  uint4* st = reinterpret_cast<uint4*>(a.staging) + (uint64_t)blockIdx.x * (2 * kContigTile);
 #pragma unroll
   for (int h = 0; h < CP; ++h) {
     uint32_t o = total + popc_below(bp[h]) + popc_below(bm[h]);
@@ -900,11 +912,23 @@ __global__ __launch_bounds__(256) void contigs_probe_quad_kernel(ContigArgs a) {
       if (w < wave) o += wave_tot[h * kWavesPerBlock + w];
       total += wave_tot[h * kWavesPerBlock + w];
     }
-    const uint64_t r = r0 + t + 256u * h;
-    if (hit[h][0]) st[o++] = (r << 25) | fid[h][0];               // strand bit 24 = 0: '+'
-    if (hit[h][1]) st[o] = (r << 25) | (1ull << 24) | fid[h][1];  // '-'
+    if (hit[h][0] || hit[h][1]) {  // hits only at positions inside a contig (g < end)
+      uint32_t c;
+      int64_t x, len;
+      locate(t + 256u * h, c, x, len);
+      const uint32_t left = (uint32_t)(x + 1);
+      if (hit[h][0]) st[o++] = make_uint4(c, left, fid[h][0], '+' | (uint32_t)(x % 3 + 1) << 8);
+      if (hit[h][1])
+        st[o] = make_uint4(c, left, fid[h][1], '-' | (uint32_t)((len - 3 * K - x) % 3 + 1) << 8);
+    }
   }
-  if (t == 0) a.block_counts[blockIdx.x] = total;
+  if (t == 0) {
+    a.block_counts[blockIdx.x] = total;
+    // the emit pass's group sums (zeroed by the previous emit pass on this workspace)
+    if (a.group_sum && total)
+      __hip_atomic_fetch_add(a.group_sum + blockIdx.x / kScanGroup, (uint64_t)total,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   KMA_CLK(5);
   KMA_CLK_HW();
 }
@@ -1033,64 +1057,61 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
   }
 }
 
-// The emit pass's offsets, in two levels: group_sum_kernel sums the probe's block counts in
-// groups of kScanGroup blocks (one workgroup per group, fully parallel); an emit block adds the
-// sums of the groups before its own and the counts before it in its group (one wave, a few
-// loads per lane). Measured alternatives (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us;
-// a ticket letting the probe's last block scan, 0.6 ms (20k atomics on one address
-// serialize); a one-block scan kernel, ~18 us (a single CU's dependent round trips).
-constexpr uint32_t kScanGroup = 256;
-__global__ __launch_bounds__(256) void group_sum_kernel(const uint32_t* __restrict__ counts,
-                                                        uint64_t* __restrict__ group_sum,
-                                                        uint32_t n) {
-  __shared__ uint32_t ws[kWavesPerBlock];
-  const uint32_t i = blockIdx.x * kScanGroup + threadIdx.x;
-  const uint32_t v = wave_sum(i < n ? counts[i] : 0u);  // <= 512 hits per block: fits u32
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) group_sum[blockIdx.x] = (uint64_t)ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-// Exclusive prefix of block b's count (wave 0 of the emit block; wave-uniform result).
+// Exclusive prefix of block b's hit count (wave 0 of the emit block; wave-uniform result): the
+// group sums of the groups before b's (kScanGroup probe blocks each, summed by the probe's
+// atomics) and the counts before b in its group, every load issued at once (one round trip for
+// up to 64 groups).
 __device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b) {
   const uint32_t lane = threadIdx.x & 63, g = b / kScanGroup;
   uint64_t s = 0;
   for (uint32_t i = lane; i < g; i += 64) s += a.group_sum[i];
-  for (uint32_t i = g * kScanGroup + lane; i < b; i += 64) s += a.block_counts[i];
+  const uint32_t c0 = g * kScanGroup + 4u * lane;  // counts are allocated in whole groups
+  if (c0 < b) {
+    const uint4 v = *reinterpret_cast<const uint4*>(a.block_counts + c0);
+    s += (uint64_t)v.x + (c0 + 1 < b ? v.y : 0u) + (c0 + 2 < b ? v.z : 0u) +
+         (c0 + 3 < b ? v.w : 0u);
+  }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
   return s;
 }
 
-// Emit pass: block b's staged hits go to out[prefix[b] ..], those past `cap` are dropped; the
-// last block publishes the total (the caller compares it with cap).
-__global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a) {
-  __shared__ uint64_t off;
-  const uint32_t n = a.block_counts[blockIdx.x];
-  if (threadIdx.x < 64) {
-    const uint64_t o = emit_offset(a, blockIdx.x);
-    if (threadIdx.x == 0) off = o;
+// Emit pass: an emit block takes kEmitSpan consecutive probe blocks; probe block b's staged
+// records go to out[prefix[b] ..], those past `cap` are dropped; the last emit block publishes
+// the total (the caller compares it with cap). The grid also zeroes the group sums the next
+// call on this workspace accumulates into (the other parity's buffer). Measured alternatives
+// for the offsets (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us; a ticket letting
+// the probe's last block scan, 0.6 ms (20k atomics on one address serialize); a one-block scan
+// kernel, ~18 us (a single CU's dependent round trips); a group-sum kernel between probe and
+// emit, and one emit block per probe block (12.5 us for c3's 19.5k blocks of ~9 hits).
+constexpr uint32_t kEmitSpan = 16;
+__global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_t n_blocks) {
+  __shared__ uint64_t pre[kEmitSpan];
+  __shared__ uint32_t cnt[kEmitSpan];
+  const uint32_t b0 = blockIdx.x * kEmitSpan, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < a.n_zero; i += (uint64_t)gridDim.x * 256)
+    a.group_zero[i] = 0;
+  if (wave == 0) {
+    const uint32_t c = lane < kEmitSpan && b0 + lane < n_blocks ? a.block_counts[b0 + lane] : 0u;
+    const uint64_t base = emit_offset(a, b0);
+    uint64_t inc = c;  // inclusive scan over the span's counts (lanes < kEmitSpan)
+#pragma unroll
+    for (int d = 1; d < (int)kEmitSpan; d <<= 1) {
+      const uint64_t v = __shfl_up(inc, d, 64);
+      inc += lane >= (uint32_t)d ? v : 0u;
+    }
+    if (lane < kEmitSpan) {
+      pre[lane] = base + inc - c;
+      cnt[lane] = c;
+    }
+    if (blockIdx.x == gridDim.x - 1 && lane == kEmitSpan - 1) *a.n_hits = base + inc;
   }
   __syncthreads();
-  const uint64_t p0 = off;
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *a.n_hits = p0 + n;
-  const uint64_t* st = a.staging + (uint64_t)blockIdx.x * (2 * kContigTile);
-  const uint64_t base = a.offsets[0];
-  for (uint32_t i = threadIdx.x; i < n && p0 + i < a.cap; i += blockDim.x) {
-    const uint64_t v = st[i];
-    const uint64_t g = base + (v >> 25);
-    const bool minus = (v >> 24) & 1u;
-    const uint32_t c = contig_of(a.offsets, a.n_contig, g);
-    const int64_t x = (int64_t)(g - a.offsets[c]);
-    const int64_t len = (int64_t)(a.offsets[c + 1] - a.offsets[c]);
-    kma_hit h;
-    h.contig = c;
-    h.left = (int32_t)(x + 1);
-    h.fid = (uint32_t)v & 0xFFFFFFu;
-    h.strand = minus ? '-' : '+';
-    h.frame = (uint8_t)((minus ? (len - 3 * a.k - x) : x) % 3 + 1);
-    h.pad = 0;
-    a.out[p0 + i] = h;
+  uint4* out = reinterpret_cast<uint4*>(a.out);
+  for (uint32_t i = wave; i < kEmitSpan && b0 + i < n_blocks; i += kWavesPerBlock) {
+    const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)(b0 + i) * (2 * kContigTile);
+    const uint64_t o = pre[i];
+    for (uint32_t r = lane; r < cnt[i] && o + r < a.cap; r += 64) out[o + r] = st[r];
   }
 }
 
@@ -1238,14 +1259,9 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
   return hipGetLastError();
 }
 
-hipError_t launch_contig_scan(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
-  hipLaunchKernelGGL(group_sum_kernel, dim3((unsigned)((n_blocks + kScanGroup - 1) / kScanGroup)),
-                     dim3(256), 0, stream, a.block_counts, a.group_sum, (uint32_t)n_blocks);
-  return hipGetLastError();
-}
-
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
-  hipLaunchKernelGGL(contigs_emit_kernel, dim3((unsigned)n_blocks), dim3(256), 0, stream, a);
+  const unsigned g = (unsigned)((n_blocks + kEmitSpan - 1) / kEmitSpan);
+  hipLaunchKernelGGL(contigs_emit_kernel, dim3(g), dim3(256), 0, stream, a, (uint32_t)n_blocks);
   return hipGetLastError();
 }
 
