@@ -154,7 +154,7 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v) {
 // One quad's verdict on a bucket it loaded cooperatively: lane `part` holds slots 2part and
 // 2part + 1 of each 64-byte half h of the bucket in v[h] (slots 8h + 2part, 8h + 2part + 1)
 // for key (kl, kh) with filter mask `need` (filter_need of the key, the same in every lane of
-// the quad): the verdict word of kma_internal.h (fid + 1, slot, kAbsent). Lane `part` holds
+// the quad): the verdict word of kma_internal.h (fid, hit flag, slot, absent bits). Lane `part` holds
 // the filter positions of its two slots (position i in slot i / kFilterBits). Keys are unique
 // in a table, so at most one lane matches and OR is the reduction. Every lane of the quad must
 // call it (DPP). Branch-free on purpose: a short-circuit here lets the compiler split the
@@ -167,16 +167,18 @@ __device__ __forceinline__ uint32_t match_part_raw(const uint4 (&v)[kBucketHalve
   for (int h = 0; h < kBucketHalves; ++h) {
     const uint32_t m0 = (uint32_t)(v[h].x == kl) & (uint32_t)((v[h].y & kKeyHiMask) == kh);
     const uint32_t m1 = (uint32_t)(v[h].z == kl) & (uint32_t)((v[h].w & kKeyHiMask) == kh);
-    w |= (m0 * ((v[h].y & kFidMask) + 1u)) | (m1 * ((v[h].w & kFidMask) + 1u));
-    w |= (m0 | m1) * ((8u * h + 2u * part + m1) << kSlotShift);  // slot within the bucket
+    // the matching slot's fid (keys are unique: at most one of m0, m1), masked once
+    w |= ((m0 ? v[h].y : 0u) | (m1 ? v[h].w : 0u)) & kFidMask;
+    // slot within the bucket and the hit flag: a lane constant chosen by m1, kept by m0 | m1
+    const uint32_t c0 = ((8u * h + 2u * part) << kSlotShift) | kWordHit;
+    w |= (m0 | m1) ? (m1 ? c0 + (1u << kSlotShift) : c0) : 0u;
     // the lane's positions: slot 8h + 2part (bits of .y), slot 8h + 2part + 1 (bits of .w)
     const uint32_t held = ((v[h].y >> kFidBits) & ((1u << FB) - 1u)) |
                           (((v[h].w >> kFidBits) & ((1u << FB) - 1u)) << FB);
     const uint32_t want = (need >> (2u * FB * (4u * h + part))) & PM;
     missing |= want & ~held;
   }
-  w |= missing ? kAbsent : 0u;
-  return w;
+  return w | missing << kAbsentShift;  // nonzero: a filter position of the key is clear
 }
 __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,
                                                uint32_t kh, uint32_t need, uint32_t part) {
@@ -205,10 +207,10 @@ __device__ __forceinline__ uint32_t quad_reduce_scatter(const uint32_t (&a)[4], 
 __device__ __forceinline__ uint32_t match_wide_raw(const uint4& v, uint32_t kl, uint32_t kh,
                                                    uint32_t need, uint32_t part) {
   const uint32_t m = (uint32_t)(v.x == kl) & (uint32_t)(v.y == kh);
-  uint32_t w = m * ((v.z & kFidMask) + 1u) | m * (part << kSlotShift);
+  uint32_t w = m ? (v.z & kFidMask) | kWordHit | part << kSlotShift : 0u;
   const uint32_t held = (v.z >> kFidBits) & ((1u << kFilterBits) - 1u);
   const uint32_t want = (need >> (kFilterBits * part)) & ((1u << kFilterBits) - 1u);
-  w |= (want & ~held) ? kAbsent : 0u;
+  w |= (want & ~held) << kAbsentShift;
   return w;
 }
 

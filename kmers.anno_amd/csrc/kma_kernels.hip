@@ -527,10 +527,10 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const uint32_t w = probed ? word[j] : 0u;
 #ifdef KMA_TUNE_COUNT
       KMA_COUNT(2, __popcll(__ballot(probed)));
-      KMA_COUNT(3, __popcll(__ballot((w & kWordFid) != 0u)));
+      KMA_COUNT(3, __popcll(__ballot((w & kWordHit) != 0u)));
 #endif
-      if (w & kWordFid)
-        record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, (w & kWordFid) - 1u,
+      if (w & kWordHit)
+        record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, w & kFidMask,
                       (c.bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
       // rare: the home bucket missed and the key's filter positions are set -> deferred walk
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
@@ -856,8 +856,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
       const uint32_t word = quad_reduce_scatter(raw, part);
       const uint32_t w = bk[h][j] != kNone ? word : 0u;
-      hit[h][j] = (w & kWordFid) != 0u;
-      fid[h][j] = (w & kWordFid) - 1u;
+      hit[h][j] = (w & kWordHit) != 0u;
+      fid[h][j] = w & kFidMask;
       uint32_t sid = bk[h][j] * kS + ((w >> kSlotShift) & (kS - 1));
       if (bk[h][j] != kNone && w == 0u) {  // rare: home missed, every filter position set
         if constexpr (kWide)

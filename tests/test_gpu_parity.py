@@ -523,6 +523,43 @@ def test_contigs_device_api_planted_genome(kma, oracle_c):
         ws.close()
 
 
+def test_contigs_device_repeated_calls_of_different_sizes(kma, oracle_c):
+    """One workspace, calls alternating between a whole genome and a prefix of its contigs (a
+    different number of emit-offset groups): the probe adds block counts into one of two
+    group-sum buffers and each emit pass zeroes the other, so every call must start from clean
+    sums whatever the size of the call before it."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_contig_workload(400_000, 8, 41, table_size=200_000, n_fid=500)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    cases = []
+    for nc in (wl.n_contig, 2, wl.n_contig, 1, 2, wl.n_contig):
+        off = wl.offsets[:nc + 1]
+        cases.append((nc, off, oracle_c.annotate_contigs(ot, wl.dna[:int(off[-1])], off, 11, K)))
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        ws = kma.Workspace(0)
+        ws.reserve_contigs(int(wl.offsets[-1]))
+        d_dna = torch.from_numpy(wl.dna).to(dev)
+        d_nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        for nc, off, e in cases:
+            d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+            cap = len(e[0]) + 1
+            d_hits = torch.zeros(cap * kma.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), nc,
+                                        int(off[-1] - off[0]), 11, d_hits.data_ptr(), cap,
+                                        d_nh.data_ptr(), 0, 0, stream)
+            torch.cuda.synchronize()
+            assert int(d_nh.item()) == len(e[0]), nc
+            hits = d_hits.cpu().numpy().view(kma.HIT_DTYPE)[:len(e[0])]
+            for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"],
+                             hits["fid"]), e):
+                assert (a == b).all(), nc
+        ws.close()
+
+
 def test_contigs_replicated_host_fan_out(kma, oracle_c):
     """6-frame host calls on a two-replica table: contig shards, hits re-based and merged in
     canonical order, tally rows per shard; equal to the single-replica answer."""
