@@ -136,16 +136,18 @@ __host__ __device__ inline uint32_t parity32(uint32_t x) {
 
 // Minimizer of a packed K-mer: the smallest hash over its K - m + 1 m-mers (5-bit residue
 // codes, first residue most significant). m is a table property (minimizer_len below).
+__host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
+#if KMA_HASH_LITE
+  return sub * 0x9E3779B1u;
+#else
+  return mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
+#endif
+}
 __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
   const uint32_t mask = (uint32_t)((1ull << (5 * m)) - 1);
   uint32_t best = 0xFFFFFFFFu;
   for (int p = 0; p <= k - m; ++p) {
-    const uint32_t sub = (uint32_t)(key >> (5 * (k - m - p))) & mask;
-#if KMA_HASH_LITE
-    const uint32_t h = sub * 0x9E3779B1u;
-#else
-    const uint32_t h = mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
-#endif
+    const uint32_t h = mmer_hash((uint32_t)(key >> (5 * (k - m - p))) & mask);
     best = best < h ? best : h;
   }
   return best;
@@ -180,15 +182,20 @@ __host__ __device__ inline uint32_t home_from_hash(uint32_t h, uint64_t key, int
   }
   return (uint32_t)(((uint64_t)h * n_buckets) >> 32);
 }
-__host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
+// The home of a key (minimizer layouts) from its minimizer hash.
+__host__ __device__ inline uint32_t home_from_min(uint32_t mn, uint64_t key, int m,
+                                                  uint32_t n_buckets) {
 #if KMA_HASH_LITE
-  const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
-                            : mix32_lite(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
+  return home_from_hash(mix32_lite(mn ^ 0x85EBCA77u), key, m, n_buckets);
 #else
-  const uint32_t h = m == 0 ? mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u))
-                            : mix32(minimizer_hash(key, k, m) ^ 0x85EBCA77u);
+  return home_from_hash(mix32(mn ^ 0x85EBCA77u), key, m, n_buckets);
 #endif
-  return home_from_hash(h, key, m, n_buckets);
+}
+__host__ __device__ inline uint32_t home_bucket(uint64_t key, int k, int m, uint32_t n_buckets) {
+  if (m == 0)
+    return home_from_hash(mix32((uint32_t)key ^ mix32((uint32_t)(key >> 32) + 0x9E3779B9u)),
+                          key, m, n_buckets);
+  return home_from_min(minimizer_hash(key, k, m), key, m, n_buckets);
 }
 
 // Step i of the probe chain of a key homed at `home` (step 0 = home).
