@@ -222,7 +222,8 @@ int kma_workspace_destroy(kma_workspace* ws);
  *                  strings): proteins {annotate_kernel}; contigs {contigs_probe_kernel,
  *                  scan_emit}.
  *   _timing_read : kernel_ms = proteins: every phase / contigs: the probe; rest_ms = contigs:
- *                  the block-count scan and the emit pass.                                   */
+ *                  the emit pass (offsets from the group sums the probe adds; the phase keeps
+ *                  its ABI-3 name scan_emit).                                                */
 #define KMA_MAX_PHASES 8
 int kma_workspace_timing(kma_workspace* ws, int enable);
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
