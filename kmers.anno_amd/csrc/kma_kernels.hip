@@ -290,6 +290,24 @@ __device__ __forceinline__ uint32_t lane_window(int t) {
 // profiles/r03_ab/r03o block clocks). A persistent grid loading the next group's head under
 // the current group's steps was tried: the group loop cost 48-112 bytes per lane of register
 // spills (scratch memory) at 7 waves per SIMD.
+// KMA_XCD_GROUPS: block b -> group so that the blocks dispatched to one XCD (b mod 8, the
+// round-robin dispatch) take consecutive groups: their offsets and span-edge residue lines
+// then meet in that XCD's L2. A bijection on [0, n): the last n mod 8 blocks keep their index.
+// Measured (profiles/r03_session2/r03z_steps.log, arms interleaved): c5 3.618-3.631 vs
+// 3.634-3.637 ms, c4 2.811 vs 2.824; c2 (two-pass grid) 2-7% slower, so not used there.
+#ifndef KMA_XCD_GROUPS
+#define KMA_XCD_GROUPS 1
+#endif
+__device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t n) {
+#if KMA_XCD_GROUPS
+  const uint32_t per = n >> 3;
+  return b < 8u * per ? (b & 7u) * per + (b >> 3) : b;
+#else
+  (void)n;
+  return b;
+#endif
+}
+
 struct GroupHead {
   uint32_t p0, np;
   uint64_t beg_raw;
@@ -602,7 +620,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kProteinOcc
   const bool second = a.defer_below && blockIdx.x >= a.n_groups;
   GroupHead h;
   WinWords ww[kProbeWin];
-  head_offsets(a, blockIdx.x - (second ? a.n_groups : 0u), h);
+  // (the two-pass grid keeps block order: its long-first order is what it is for)
+  const uint32_t b = blockIdx.x - (second ? a.n_groups : 0u);
+  head_offsets(a, a.defer_below ? b : xcd_group(b, a.n_groups), h);
   head_residues<kProbeWin>(a, h, lane_window(t), ww);
   annotate_block<K, M, P>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
   KMA_CLK(5);
