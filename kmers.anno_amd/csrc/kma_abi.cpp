@@ -867,18 +867,24 @@ const char* const kDirectPhases[] = {"annotate_kernel"};
 const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
 // Proteins per annotate_kernel block (KMA_BLOCK_PROTEINS=1..8 overrides, read per call): 6 for
-// batches of more than 4 resident waves of such blocks, else 4. A block's fixed costs (the
+// batches of more than 4 resident waves of such blocks against a table larger than the Infinity
+// Cache, else 4. A block's fixed costs (the
 // offsets and first residues round trips, the final chain walks, the vote) are amortized over
 // more probe steps with more proteins, while a batch of few waves of blocks ends with a longer
 // tail. Measured on MI355X (profiles/r03_ab/r03m, r03n): c5 3.94 / 3.77 / 3.88 ms at 4 / 6 / 8
 // (3.87 / 3.72 / 3.84 with queued keys), c2 51 vs 66 us at 4 vs 6. (Round 2, before the walk
 // queue and the scratch fix: c5 4.53 / 4.66 / 4.86 ms at 4 / 6 / 8, r02f_block_proteins.log.)
-uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq) {
+// Round 3 (interleaved A/B, profiles/r03_session2/r03bp_steps.log): c5 (10^8 rows, 1.5 GiB
+// table in HBM) 3.59-3.63 / 3.69-3.71 / 3.80-3.81 ms at 6 / 7 / 8; c4 (10^7 rows, a 153 MiB
+// table inside the 256 MiB Infinity Cache) 2.752 vs 2.819 ms at 4 vs 6: 6 only for tables
+// larger than the Infinity Cache.
+constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
+uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes) {
   const char* e = getenv("KMA_BLOCK_PROTEINS");
   const int f = (e && *e) ? atoi(e) : 0;
   if (f >= 1 && f <= kma::kBlockProteins) return (uint32_t)f;
   const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
-  return (uint64_t)n_seq / 6 > 4 * slots ? 6u : 4u;
+  return (uint64_t)n_seq / 6 > 4 * slots && table_bytes > kInfinityCacheBytes ? 6u : 4u;
 }
 
 // Deferral of short groups (annotate_kernel's two-pass grid), in probe steps: groups below it
@@ -921,7 +927,7 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
-  a.block_proteins = block_proteins(ws, n_seq);
+  a.block_proteins = block_proteins(ws, n_seq, t->n_buckets * (uint64_t)kma::kBucketBytes);
   a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
   a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
   PhaseClock clk(ws, s, kDirectPhases, 1);
