@@ -243,8 +243,8 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
             f"built in {ms:.1f} ms")
         del winner, keys, fids
     if world > 1:
-        kdist.broadcast_table(slots, src=0)  # RCCL over xGMI
-        dist.broadcast(layout, src=0)
+        kdist.broadcast_table(slots, src=0)  # RCCL over xGMI (host-staged under gloo)
+        kdist.broadcast(layout, src=0)
         torch.cuda.synchronize()
     m = int(layout.item())
     return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m), slots
@@ -284,7 +284,7 @@ def timed(step, ws, args, world, stream, dev, before=None, after=None):
     stats = torch.tensor([elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names],
                          dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        kdist.all_reduce_max(stats)
     v = stats.tolist()
     return v[0], v[1], dict(zip(names, v[2:]))
 
@@ -380,7 +380,7 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                        "probed_windows_per_gpu": n_probe, "hits_per_gpu": n_hits,
                        "table_entries": t_size, "functions": n_fid, "k": K,
                        "genetic_code": 11, "load_factor": args.load_factor,
-                       "parallelism": f"genome-shard x{world}, table replicated (RCCL broadcast)"},
+                       "parallelism": f"genome-shard x{world}" + collective_note(args, world)},
             "seqs_per_s": n_contig * args.steps * world / elapsed,
             "gpu_ms_per_step": gpu_ms / args.steps,
             "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
@@ -410,6 +410,75 @@ def e2e_host(table, residues, offsets, n_fid, reps=3):
     return best * 1e3
 
 
+def slots_digest(slots) -> int:
+    """Order-sensitive checksum of a replica's slot array (sum of slot XOR its index mix)."""
+    v = slots.view(torch.int64)
+    total, chunk = 0, 1 << 26
+    for a in range(0, v.numel(), chunk):
+        x = v[a:a + chunk]
+        idx = torch.arange(a, a + x.numel(), dtype=torch.int64, device=x.device)
+        total = (total + int(torch.bitwise_xor(x, idx * 0x9E3779B97F4A7C15 % (1 << 62)).sum())) % (1 << 64)
+    return total
+
+
+def verify_proteins(args, sig, table, slots, rank, world, strong, full, own, lo, outs, tally_job,
+                    n_fid, qseed0):
+    """Multi-rank parity of the timed path (--verify), checked on rank 0:
+      table    every rank's replica of the broadcast table has the same slot digest and answers
+               one probe batch identically (host entry point on each rank);
+      outputs  the per-rank outputs (disjoint shards of one batch for c4, each rank's own batch
+               for c5 / c2) gathered on rank 0 equal ONE single-rank whole-batch call there;
+      tally    the tally reduced over ranks inside the timed region equals steps x the sum of
+               the single-rank tallies;
+      fan-out  the same whole batch through the host entry point after kma_table_replicate
+               added two more replicas on rank 0's device (the ABI's own residue-balanced
+               fan-out over replicas, one host thread each) equals the single-replica answer."""
+    d_fid, d_cnt, d_st = outs
+    mine = (lo, d_fid.cpu().numpy(), d_cnt.cpu().numpy(), d_st.cpu().numpy())
+    probe_res, probe_off, _, _ = synth.make_queries(sig, 3000, 4242)
+    probe = kmeranno.annotate_proteins(table, probe_res, probe_off, MIN_HITS, 0)[:3]
+    digest = slots_digest(slots)
+    parts = kdist.gather_objects((mine, probe, digest))
+    if rank != 0:
+        return None
+    out = {"ranks": world}
+    out["table_identical_across_ranks"] = bool(
+        all(d == parts[0][2] for _, _, d in parts) and
+        all(all((a == b).all() for a, b in zip(p, parts[0][1])) for _, p, _ in parts))
+    # single-rank answers of the same work
+    if strong:
+        batches = [full]
+    else:  # rank r's own batch is regenerated here from its seed
+        batches = [own if r == 0 else synth.make_queries(sig, args.n_seq or len(own[1]) - 1,
+                                                         qseed0 + r)[:2]
+                   for r in range(world)]
+    single, tally = [], np.zeros(n_fid, np.int64)
+    for res, off in batches:
+        f, c, s, t = kmeranno.annotate_proteins(table, res, off, MIN_HITS, 0, n_fid=n_fid)
+        single.append((f, c, s))
+        tally += t
+    if strong:
+        got = [np.concatenate([p[0][i] for p in sorted(parts, key=lambda p: p[0][0])])
+               for i in (1, 2, 3)]
+        out["outputs_equal_single_rank"] = bool(all((g == e).all()
+                                                    for g, e in zip(got, single[0])))
+    else:
+        out["outputs_equal_single_rank"] = bool(all(
+            all((g == e).all() for g, e in zip(parts[r][0][1:], single[r]))
+            for r in range(world)))
+    out["tally_equals_single_rank"] = bool((tally_job.astype(np.int64) ==
+                                            tally * args.steps).all())
+    out["called"] = int(sum(int((s[2] == kmeranno.STATUS_CALLED).sum()) for s in single))
+    dev = table.info.device
+    table.replicate([dev, dev])
+    out["replicas"] = table.replicas
+    res, off = batches[0]
+    fan = kmeranno.annotate_proteins(table, res, off, MIN_HITS, 0, n_fid=n_fid)
+    out["replica_fanout_equals"] = bool(all((a == b).all() for a, b in zip(fan[:3], single[0])))
+    out["ok"] = all(v for k, v in out.items() if k.endswith(("_ranks", "_rank", "_equals")))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -422,17 +491,30 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the gather ceiling and the host-path (e2e) measurement")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="collectives: nccl = RCCL over xGMI (one GPU per rank); gloo = host-"
+                         "staged, to rehearse several ranks on one GPU (with --same-device)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank uses device 0 (multi-rank rehearsal on a 1-GPU box)")
+    ap.add_argument("--verify", action="store_true",
+                    help="after timing, check the multi-rank outputs, tally and table against "
+                         "single-rank calls on rank 0 (exit 1 on a mismatch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.same_device and world > 1 and args.dist_backend == "nccl":
+        ap.error("--same-device needs --dist-backend gloo (RCCL takes one rank per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
@@ -452,6 +534,7 @@ def main():
     batch_windows = int(np.maximum(np.diff(offsets).astype(np.int64) - K + 1, 0).sum())
     batch_seqs = len(offsets) - 1
     lo = 0
+    full = (residues, offsets)  # the whole batch (c4) / this rank's batch (c5, c2)
     if strong:  # this rank's residue-balanced contiguous shard of the one batch
         residues, offsets, lo = kdist.shard(residues, offsets, world, rank)
     n_seq = len(offsets) - 1
@@ -476,11 +559,22 @@ def main():
                                           d_st.data_ptr(), d_tally.data_ptr(), n_fid, sp)
 
     # per-function tallies of the whole job -> rank 0, inside the timed region
-    reduce = (lambda: kdist.reduce_tallies(d_tally, dst=0)) if world > 1 else None
+    job_tally = torch.zeros_like(d_tally)
+
+    def reduce():
+        if world > 1:
+            kdist.reduce_tallies(d_tally, dst=0)
+        job_tally.copy_(d_tally)
+
     elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev, before=d_tally.zero_,
                                 after=reduce)
     st = d_st.cpu().numpy()
     called = int((st == kmeranno.STATUS_CALLED).sum())
+    verify = None
+    if args.verify:
+        verify = verify_proteins(args, sig, table, slots, rank, world, strong, full, full, lo,
+                                 (d_fid, d_cnt, d_st), job_tally.cpu().numpy(), n_fid,
+                                 seed * 1_000_003 + 17)
     if rank == 0:
         total_lookups = (batch_windows if strong else n_win * world) * args.steps
         value = total_lookups / elapsed
@@ -499,8 +593,7 @@ def main():
                        "load_factor": args.load_factor, "min_hits": MIN_HITS,
                        "table_layout_m": table.info.minimizer_len,
                        "parallelism": (f"input-shard x{world} of one batch" if strong else
-                                       f"input-shard x{world}") +
-                                      ", table replicated (RCCL broadcast), tally reduce (RCCL)"},
+                                       f"input-shard x{world}") + collective_note(args, world)},
             "seqs_per_s": seqs * args.steps / elapsed,
             "called_per_batch": called,
             "gpu_ms_per_step": gpu_ms / args.steps,
@@ -518,11 +611,25 @@ def main():
                     "seqs_per_s": n_seq / (ms * 1e-3)}
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(sig.keys, sig.fids, residues, offsets)
+        if verify is not None:
+            out["verify"] = verify
         print(json.dumps(out), flush=True)
     ws.close()
     table.close()
     if world > 1:
         dist.destroy_process_group()
+    if verify is not None and not verify["ok"]:
+        sys.exit(1)
+
+
+def collective_note(args, world: int) -> str:
+    if world == 1:
+        return ", table on this GPU"
+    if args.dist_backend == "nccl":
+        return ", table replicated (RCCL broadcast over xGMI), tally reduce (RCCL)"
+    return (", table replicated (gloo broadcast, host-staged), tally reduce (gloo)" +
+            ("; every rank on device 0 (multi-rank rehearsal, ranks share one GPU)"
+             if args.same_device else ""))
 
 
 if __name__ == "__main__":

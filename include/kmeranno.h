@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 4
+#define KMA_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -138,6 +138,31 @@ int kma_abi_version(void);
 const char* kma_last_error(void);
 int kma_device_count(int* out_n);
 
+/* ---- options ---------------------------------------------------------------------------------
+ * Library-wide tuning defaults, read by every later call (the library reads no environment
+ * variables; tuning builds compiled with -DKMA_TUNING_ENV=1 seed these from KMA_MINIMIZER,
+ * KMA_BLOCK_PROTEINS, KMA_DEFER, KMA_HOST_PIECES and KMA_HASH_SLICE). Defaults in brackets.
+ *   KMA_OPT_LAYOUT          table creators' layout [-1: size rule + measurement, see
+ *                           kma_table_layout_for]; 0 = flat, 6 / 7 = minimizer m = min(K, value)
+ *   KMA_OPT_BLOCK_PROTEINS  proteins per annotate_kernel block [0: by batch and table size];
+ *                           1..8
+ *   KMA_OPT_DEFER           the protein kernel's two-pass grid [-1: automatic for grids of 1-4
+ *                           resident waves]; 0 = off; 1..64 = groups of fewer probe steps start
+ *                           after every longer one, on any batch
+ *   KMA_OPT_HOST_PIECES     host protein calls: staging / kernel pipeline pieces [0: up to 8];
+ *                           1..16
+ *   KMA_OPT_HASH_SLICE      kma_hash_annotate: candidates per prototype slice [0: 2^31 - 1]
+ * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
+ * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
+#define KMA_OPT_LAYOUT 1
+#define KMA_OPT_BLOCK_PROTEINS 2
+#define KMA_OPT_DEFER 3
+#define KMA_OPT_HOST_PIECES 4
+#define KMA_OPT_HASH_SLICE 5
+#define KMA_OPT_DEFAULT INT64_MIN
+int kma_option_set(int option, int64_t value);
+int kma_option_get(int option, int64_t* value);
+
 /* Pack n kmers of length K (rows of `text` delimited by offsets[0..n]) with the standard
  * alphabet + the table's extra symbols. out_keys[r] = 0 for a row that is not of length K or
  * contains a byte the table cannot encode. Host-side helper; no device needed.             */
@@ -166,7 +191,7 @@ int kma_bucket_slots_for(int k);
  * past their home bucket or a chain exceeds 32 buckets (keys that pile onto few minimizers),
  * the creators above also build the table flat (layout 0) and keep it if it halves the
  * displaced keys or the longest chain. kma_table_layout_for gives the size-derived layout
- * (KMA_MINIMIZER=0|6|7 in the environment forces one).                                       */
+ * (KMA_OPT_LAYOUT = 0 / 6 / 7 forces one).                                                    */
 int kma_table_layout_for(int k, uint64_t n_buckets);
 
 /* ---- replicas (the table replicated on every device of the node) -------------
@@ -214,6 +239,7 @@ int kma_workspace_create(int device, kma_workspace** out);
 int kma_workspace_reserve(kma_workspace* ws, uint64_t n_residues);
 int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t n_seq);
 int kma_workspace_destroy(kma_workspace* ws);
+int kma_workspace_option_set(kma_workspace* ws, int option, int64_t value); /* see options */
 /* Device timing of the _device calls made with this workspace: with enable = 1 each call
  * records hipEvents on its stream at its phase boundaries. Not for graph capture. Both reads
  * synchronise on the recorded events (the last 256 calls) and clear the accumulators.
@@ -236,8 +262,8 @@ int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phase
  * min_hits >= 1 (ApplyKmerProcessor.java:91-92). out_tally (optional, length n_fid) receives
  * += 1 per CALLED protein at its fid (the APPLY report's role counts before column mapping).
  * Host form: synchronous, host buffers. A batch of >= 32 MiB of residues is cut into pieces of
- * whole proteins (up to 8; KMA_HOST_PIECES in the environment overrides, 1..16) whose staging
- * and H2D run on the context's copy stream under the previous piece's kernel.                 */
+ * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16) whose staging and H2D run on
+ * the context's copy stream under the previous piece's kernel.                                */
 int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
@@ -271,7 +297,9 @@ int kma_annotate_contigs(const kma_table* table, const uint8_t* dna, const uint6
  * d_dna readable for 64 bytes past the last base. Hits [0, cap) go to d_hits in canonical
  * order and *d_n_hits (device u64) receives the total, which may exceed cap (then the hits
  * past cap are dropped: compare and call again with a larger buffer). d_tally (n_contig x
- * n_fid u32, optional) is accumulated into. Never allocates or synchronises.                 */
+ * n_fid u32, optional) is accumulated into. Never allocates or synchronises; keeps no host
+ * state between calls (the emit pass leaves the workspace's group sums zero), so a call may be
+ * captured in a hipGraph and replayed. Calls on one workspace are ordered on one stream.     */
 int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases);
 int kma_annotate_contigs_device(const kma_table* table, kma_workspace* ws, const uint8_t* d_dna,
                                 const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,

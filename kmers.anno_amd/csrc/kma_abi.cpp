@@ -30,14 +30,45 @@
 #include "kma_internal.h"
 
 namespace {
-// KMA_MINIMIZER=0|6|7 forces a table layout (tests run every layout in one process, so the
-// variable is read per table, not cached). -1 = not forced.
-int forced_layout() {
-  const char* e = getenv("KMA_MINIMIZER");
-  if (!e || !*e) return -1;
-  const int v = atoi(e);
-  return (v == 0 || v == 6 || v == 7) ? v : -1;
+// ---- options (kma_option_set; include/kmeranno.h) ----------------------------------------------
+// Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
+// environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
+// a library a JVM loads must not change its kernel geometry because of a stray variable.
+constexpr int kNumOpts = 6;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}};
+constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
+
+bool option_valid(int opt, int64_t v) {
+  switch (opt) {
+    case KMA_OPT_LAYOUT: return v == -1 || v == 0 || v == 6 || v == 7;
+    case KMA_OPT_BLOCK_PROTEINS: return v >= 0 && v <= kma::kBlockProteins;
+    case KMA_OPT_DEFER: return v >= -1 && v <= 64;
+    case KMA_OPT_HOST_PIECES: return v >= 0 && v <= 16;
+    case KMA_OPT_HASH_SLICE: return v >= 0;
+    default: return false;
+  }
 }
+
+#if KMA_TUNING_ENV
+struct EnvOptions {  // tuning builds: the A/B scripts' variables seed the defaults once
+  EnvOptions() {
+    const std::pair<const char*, int> vars[] = {
+        {"KMA_MINIMIZER", KMA_OPT_LAYOUT}, {"KMA_BLOCK_PROTEINS", KMA_OPT_BLOCK_PROTEINS},
+        {"KMA_DEFER", KMA_OPT_DEFER}, {"KMA_HOST_PIECES", KMA_OPT_HOST_PIECES},
+        {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}};
+    for (const auto& [name, opt] : vars)
+      if (const char* e = getenv(name); e && *e) {
+        const int64_t v = strtoll(e, nullptr, 10);
+        if (option_valid(opt, v)) g_opt[opt] = v;
+      }
+  }
+} g_env_options;
+#endif
+
+int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
+
+// The forced table layout (KMA_OPT_LAYOUT): -1 = not forced.
+int forced_layout() { return (int)opt(KMA_OPT_LAYOUT); }
 }  // namespace
 
 int kma::minimizer_len(int k, uint64_t n_buckets) {
@@ -253,15 +284,16 @@ struct kma_workspace {
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
   kma_hit* d_cstage = nullptr;
   uint32_t* d_ccounts = nullptr;
-  // Emit-offset group sums, two buffers of cgroups: the probe of a call adds into buffer
-  // cparity, its emit pass zeroes the other one's first cdirty[1 - cparity] entries (what the
-  // call before it used) and flips cparity.
+  // Emit-offset group sums (cgroups u64) and the emit pass's done counter (one u64 after
+  // them): zero between calls — the probe adds into the sums, the emit pass's last block
+  // zeroes both — so a call keeps no host state and may be graph-captured.
   uint64_t* d_cprefix = nullptr;
   uint64_t cgroups = 0;
-  uint64_t cdirty[2] = {0, 0};
-  int cparity = 0;
   bool cpending = false;  // a probe was set up whose emit pass has not been enqueued
   uint64_t contig_cap = 0;  // bases
+  // Per-workspace overrides of KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER (kOptUnset: the default).
+  int64_t opt_block_proteins = kOptUnset;
+  int64_t opt_defer = kOptUnset;
   // Per-phase timing (kma_workspace_timing): a ring of calls, each kMaxEv events (phase i runs
   // from event i to event i + 1) and its phase names.
   bool timing = false;
@@ -587,6 +619,20 @@ extern "C" {
 
 int kma_abi_version(void) { return KMA_ABI_VERSION; }
 
+int kma_option_set(int option, int64_t value) {
+  if (option < 1 || option >= kNumOpts || !option_valid(option, value))
+    return fail(KMA_E_INVALID, "option %d: value %lld out of range", option, (long long)value);
+  g_opt[option] = value;
+  return KMA_OK;
+}
+
+int kma_option_get(int option, int64_t* value) {
+  if (!value || option < 1 || option >= kNumOpts)
+    return fail(KMA_E_INVALID, "option %d unknown (or null value)", option);
+  *value = opt(option);
+  return KMA_OK;
+}
+
 const char* kma_last_error(void) { return g_err.c_str(); }
 
 int kma_device_count(int* out_n) {
@@ -722,6 +768,7 @@ int kma_table_replicas(const kma_table* t, int* n, int* device_ids, int cap) {
 
 int kma_table_info_get(const kma_table* table, kma_table_info* out) {
   if (!table || !out) return fail(KMA_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> g(table->reps_mu);  // kma_table_replicate writes n_replicas
   *out = table->info;
   return KMA_OK;
 }
@@ -801,9 +848,9 @@ void codon_codes(const char* code, uint8_t out[64]) {
     out[i] = (code[i] == '*' || code[i] == 'X') ? 0 : (uint8_t)(code[i] - 'A' + 1);
 }
 
-kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace* ws,
-                            const uint8_t* d_dna, const uint64_t* d_offsets, uint32_t n_contig,
-                            uint64_t n_bases, const char* code, uint32_t* d_tally, uint32_t n_fid) {
+int contig_args(const kma_table* t, const Replica& r, kma_workspace* ws, const uint8_t* d_dna,
+                const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases, const char* code,
+                uint32_t* d_tally, uint32_t n_fid, hipStream_t s, kma::ContigArgs* out) {
   kma::ContigArgs a{};
   a.slots = r.d_slots;
   a.n_buckets = (uint32_t)t->n_buckets;
@@ -815,30 +862,24 @@ kma::ContigArgs contig_args(const kma_table* t, const Replica& r, kma_workspace*
   a.mlen = t->mlen;
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
-  if (ws->cpending) {  // an earlier call failed between its probe and its emit: start clean
-    (void)hipDeviceSynchronize();  // the failed call's probe may still be adding
-    (void)hipMemset(ws->d_cprefix, 0, 2 * ws->cgroups * 8);
-    ws->cdirty[0] = ws->cdirty[1] = 0;
-  }
+  // An earlier call failed between its probe and its emit: start clean, ordered on this
+  // call's stream (calls on one workspace are ordered on one stream, kmeranno.h).
+  if (ws->cpending) KMA_HIP(hipMemsetAsync(ws->d_cprefix, 0, (ws->cgroups + 1) * 8, s));
   ws->cpending = true;
-  a.group_sum = ws->d_cprefix + ws->cparity * ws->cgroups;
+  a.group_sum = ws->d_cprefix;
+  a.emit_done = reinterpret_cast<uint32_t*>(ws->d_cprefix + ws->cgroups);
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
-  return a;
+  *out = a;
+  return KMA_OK;
 }
 
 // Canonical-order emission after the probe on s (whose atomics summed the block counts into
-// ws's current group-sum buffer); zeroes the other buffer for the next call and flips parity.
+// ws's group sums); the emit pass leaves the sums zero for the next call.
 int enqueue_contig_emit(kma_workspace* ws, kma::ContigArgs a, kma_hit* d_hits, uint64_t cap,
                         uint64_t* d_n_hits, hipStream_t s) {
   const uint64_t nb = contig_blocks(a.total_bases);
-  const int other = 1 - ws->cparity;
-  a.group_zero = ws->d_cprefix + other * ws->cgroups;
-  a.n_zero = ws->cdirty[other];
-  ws->cdirty[other] = 0;
-  ws->cdirty[ws->cparity] = (nb + kma::kScanGroup - 1) / kma::kScanGroup;
-  ws->cparity = other;
   a.out = d_hits;
   a.cap = d_hits ? cap : 0;
   a.n_hits = d_n_hits;
@@ -880,8 +921,8 @@ const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 // larger than the Infinity Cache.
 constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes) {
-  const char* e = getenv("KMA_BLOCK_PROTEINS");
-  const int f = (e && *e) ? atoi(e) : 0;
+  const int64_t f = ws->opt_block_proteins != kOptUnset ? ws->opt_block_proteins
+                                                         : opt(KMA_OPT_BLOCK_PROTEINS);
   if (f >= 1 && f <= kma::kBlockProteins) return (uint32_t)f;
   const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
   return (uint64_t)n_seq / 6 > 4 * slots && table_bytes > kInfinityCacheBytes ? 6u : 4u;
@@ -898,8 +939,8 @@ uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_
 // KMA_DEFER=<steps> forces it on any batch (read per call).
 uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
   const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
-  const char* e = getenv("KMA_DEFER");
-  if (e && *e) return (uint32_t)std::max(0, std::min(64, atoi(e)));
+  const int64_t f = ws->opt_defer != kOptUnset ? ws->opt_defer : opt(KMA_OPT_DEFER);
+  if (f >= 0) return (uint32_t)std::min<int64_t>(64, f);
   return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
 }
 
@@ -1015,9 +1056,8 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   // at most KMA_HOST_PIECES (default 8, <= kMaxPieces; read per call); a small call is one
   // piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (profiles/r02r_host_pipeline/).
   constexpr uint64_t kPieceBytes = 16ull << 20;
-  const char* pe = std::getenv("KMA_HOST_PIECES");
-  const uint64_t max_pieces = pe ? std::clamp<uint64_t>(std::strtoull(pe, nullptr, 10), 1,
-                                                       kMaxPieces) : 8;
+  const int64_t po = opt(KMA_OPT_HOST_PIECES);
+  const uint64_t max_pieces = po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : 8;
   uint8_t* hin = c->h_in.p;
   hipStream_t s = c->stream, cs = c->copy;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
@@ -1078,11 +1118,10 @@ int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   const uint64_t ng = (nb + kma::kScanGroup - 1) / kma::kScanGroup;
   KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * sizeof(kma_hit)));
   KMA_HIP(hipMalloc(&ws->d_ccounts, ng * kma::kScanGroup * 4));
-  KMA_HIP(hipMalloc(&ws->d_cprefix, 2 * ng * 8));
-  KMA_HIP(hipMemset(ws->d_cprefix, 0, 2 * ng * 8));
+  KMA_HIP(hipMalloc(&ws->d_cprefix, (ng + 1) * 8));
+  KMA_HIP(hipMemset(ws->d_cprefix, 0, (ng + 1) * 8));
   ws->cgroups = ng;
-  ws->cdirty[0] = ws->cdirty[1] = 0;
-  ws->cparity = 0;
+  ws->cpending = false;
   ws->contig_cap = nb * kma::kContigTile;
   return KMA_OK;
 }
@@ -1122,6 +1161,17 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
   free_protein_scratch(ws);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
   ws->res_cap = n_residues;
+  return KMA_OK;
+}
+
+int kma_workspace_option_set(kma_workspace* ws, int option, int64_t value) {
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  if (option != KMA_OPT_BLOCK_PROTEINS && option != KMA_OPT_DEFER)
+    return fail(KMA_E_INVALID, "option %d is not a workspace option", option);
+  if (value != KMA_OPT_DEFAULT && !option_valid(option, value))
+    return fail(KMA_E_INVALID, "option %d: value %lld out of range", option, (long long)value);
+  (option == KMA_OPT_BLOCK_PROTEINS ? ws->opt_block_proteins : ws->opt_defer) =
+      value == KMA_OPT_DEFAULT ? kOptUnset : value;
   return KMA_OK;
 }
 
@@ -1283,8 +1333,10 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
   if (n_bases > ws->contig_cap)
     return fail(KMA_E_CAPACITY, "workspace reserved for %llu bases, call needs %llu",
                 (unsigned long long)ws->contig_cap, (unsigned long long)n_bases);
-  const kma::ContigArgs a =
-      contig_args(t, *r, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid);
+  kma::ContigArgs a;
+  if (int rc = contig_args(t, *r, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid,
+                           s, &a))
+    return rc;
   PhaseClock clk(ws, s, kContigPhases, 2);
   KMA_HIP(clk.mark());
   const uint64_t nb = contig_blocks(n_bases);
@@ -1340,8 +1392,10 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
     std::memcpy(ht, tally, tb);
     KMA_HIP(hipMemcpyAsync(d_tally, ht, tb, hipMemcpyHostToDevice, s));
   }
-  kma::ContigArgs a =
-      contig_args(t, r, c->ws, c->d_in.p, c->d_off.p, n, total, code, d_tally, n_fid);
+  kma::ContigArgs a;
+  if (int rc = contig_args(t, r, c->ws, c->d_in.p, c->d_off.p, n, total, code, d_tally, n_fid, s,
+                           &a))
+    return rc;
   const uint64_t nb = contig_blocks(total);
   if (strict) {
     const uint64_t n_slots = t->n_buckets * kma::slots_for_k(t->k);
@@ -1961,10 +2015,10 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
   // Candidates are scored in slices of whole prototypes (file order) whose sort and run-length
   // encoding stay below 2^31 elements (hipcub's int counts); a slice's best per protein
   // replaces the running best only when strictly higher, so earlier prototypes keep ties.
-  // KMA_HASH_SLICE (tests) lowers the slice size.
+  // KMA_OPT_HASH_SLICE (tests) lowers the slice size.
   uint64_t slice_cap = (1ull << 31) - 1;
-  if (const char* e = getenv("KMA_HASH_SLICE"))
-    slice_cap = std::max<uint64_t>(1, std::min<uint64_t>(slice_cap, strtoull(e, nullptr, 10)));
+  if (const int64_t o = opt(KMA_OPT_HASH_SLICE); o > 0)
+    slice_cap = std::min<uint64_t>(slice_cap, (uint64_t)o);
   std::vector<uint64_t> cum(n_pt + 1, 0);
   if (n_cand) {
     uint64_t* d_cum;

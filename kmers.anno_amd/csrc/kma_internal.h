@@ -348,9 +348,11 @@ struct ContigArgs {
   kma_hit* staging;            // n_blocks x kContigTile*2 final hit records (block order)
   uint32_t* block_counts;      // n_blocks (allocated in whole groups of kScanGroup)
   uint64_t* group_sum;         // ceil(n_blocks / kScanGroup) group sums, zero before the probe
-                               // (which adds its block counts; null: no emit follows)
-  uint64_t* group_zero;        // emit pass: the other parity's group sums, zeroed [0, n_zero)
-  uint64_t n_zero;
+                               // (which adds its block counts; null: no emit follows); the
+                               // emit pass leaves them zero again
+  uint32_t* emit_done;         // emit blocks done (zero before the emit; left zero)
+  uint32_t n_groups;           // emit pass (set by launch_contigs_emit)
+  uint32_t groups_scanned;     // emit pass: group_sum holds exclusive prefixes
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
   kma_hit* out;                // emit pass: hits [0, cap) in canonical order
@@ -371,6 +373,9 @@ struct ContigArgs {
 constexpr int kContigPos = KMA_CONTIG_POS;
 constexpr int kContigTile = 256 * kContigPos;  // forward positions per block
 constexpr uint32_t kScanGroup = 256;  // probe blocks per emit-offset group sum
+// Up to this many groups (16 loads per lane, one round trip) an emit block sums the group sums
+// before its own; beyond, a one-block scan turns them into prefixes first.
+constexpr uint32_t kDirectGroups = 1024;
 
 // ---- the projector's proposal sweep (kma_proposals.hip) ----------------------------------------
 struct PropArgs {

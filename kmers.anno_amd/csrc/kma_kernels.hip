@@ -1079,12 +1079,17 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
 
 // Exclusive prefix of block b's hit count (wave 0 of the emit block; wave-uniform result): the
 // group sums of the groups before b's (kScanGroup probe blocks each, summed by the probe's
-// atomics) and the counts before b in its group, every load issued at once (one round trip for
-// up to 64 groups).
+// atomics; every load issued at once: one round trip for up to 64 groups) — or, for calls of
+// more than kDirectGroups groups, the exclusive group prefix contigs_group_scan_kernel left in
+// place of the sums (one load) — plus the counts before b in its group.
 __device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b) {
   const uint32_t lane = threadIdx.x & 63, g = b / kScanGroup;
   uint64_t s = 0;
-  for (uint32_t i = lane; i < g; i += 64) s += a.group_sum[i];
+  if (a.groups_scanned) {
+    if (lane == 0) s = a.group_sum[g];
+  } else {
+    for (uint32_t i = lane; i < g; i += 64) s += a.group_sum[i];
+  }
   const uint32_t c0 = g * kScanGroup + 4u * lane;  // counts are allocated in whole groups
   if (c0 < b) {
     const uint4 v = *reinterpret_cast<const uint4*>(a.block_counts + c0);
@@ -1096,21 +1101,47 @@ __device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b)
   return s;
 }
 
+// Calls of more than kDirectGroups groups (> 67M bases): one block turns the group sums into
+// exclusive prefixes in place, so an emit block reads one value instead of summing every group
+// before its own (which grows as blocks x groups: ~2e9 loads at 1 Gbp).
+__global__ __launch_bounds__(1024) void contigs_group_scan_kernel(uint64_t* sums, uint32_t n) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
+  const uint64_t lo = (uint64_t)t * per, hi = lo + per < n ? lo + per : n;
+  uint64_t s = 0;
+  for (uint64_t i = lo; i < hi; ++i) s += sums[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the parts
+    const uint64_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = t ? part[t - 1] : 0u;
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t x = sums[i];
+    sums[i] = run;
+    run += x;
+  }
+}
+
 // Emit pass: an emit block takes kEmitSpan consecutive probe blocks; probe block b's staged
 // records go to out[prefix[b] ..], those past `cap` are dropped; the last emit block publishes
-// the total (the caller compares it with cap). The grid also zeroes the group sums the next
-// call on this workspace accumulates into (the other parity's buffer). Measured alternatives
-// for the offsets (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us; a ticket letting
-// the probe's last block scan, 0.6 ms (20k atomics on one address serialize); a one-block scan
-// kernel, ~18 us (a single CU's dependent round trips); a group-sum kernel between probe and
-// emit, and one emit block per probe block (12.5 us for c3's 19.5k blocks of ~9 hits).
+// the total (the caller compares it with cap). The call leaves no state behind: every emit
+// block counts itself done (one agent-scope atomic, issued once its offsets are read) and the
+// block that finishes last zeroes the group sums and the counter for the next call (so calls
+// on one workspace may be graph-captured and replayed). Measured alternatives for the offsets
+// (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us; a ticket letting the probe's last
+// block scan, 0.6 ms (20k atomics on one address serialize); a one-block scan kernel, ~18 us (a
+// single CU's dependent round trips); a group-sum kernel between probe and emit, and one emit
+// block per probe block (12.5 us for c3's 19.5k blocks of ~9 hits).
 constexpr uint32_t kEmitSpan = 16;
 __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_t n_blocks) {
   __shared__ uint64_t pre[kEmitSpan];
   __shared__ uint32_t cnt[kEmitSpan];
+  __shared__ uint32_t last;
   const uint32_t b0 = blockIdx.x * kEmitSpan, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < a.n_zero; i += (uint64_t)gridDim.x * 256)
-    a.group_zero[i] = 0;
   if (wave == 0) {
     const uint32_t c = lane < kEmitSpan && b0 + lane < n_blocks ? a.block_counts[b0 + lane] : 0u;
     const uint64_t base = emit_offset(a, b0);
@@ -1127,11 +1158,19 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
     if (blockIdx.x == gridDim.x - 1 && lane == kEmitSpan - 1) *a.n_hits = base + inc;
   }
   __syncthreads();
+  if (t == 0)  // this block's reads of the group sums are done (their values are in pre[])
+    last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_ACQ_REL,
+                                  __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   uint4* out = reinterpret_cast<uint4*>(a.out);
   for (uint32_t i = wave; i < kEmitSpan && b0 + i < n_blocks; i += kWavesPerBlock) {
     const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)(b0 + i) * (2 * kContigTile);
     const uint64_t o = pre[i];
     for (uint32_t r = lane; r < cnt[i] && o + r < a.cap; r += 64) out[o + r] = st[r];
+  }
+  __syncthreads();
+  if (last) {  // every other emit block has read its offsets: clean up for the next call
+    for (uint32_t i = t; i < a.n_groups; i += 256) a.group_sum[i] = 0;
+    if (t == 0) *a.emit_done = 0;
   }
 }
 
@@ -1280,8 +1319,16 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
 }
 
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  ContigArgs e = a;
+  e.n_groups = (uint32_t)((n_blocks + kScanGroup - 1) / kScanGroup);
+  e.groups_scanned = e.n_groups > kDirectGroups;
+  if (e.groups_scanned) {
+    hipLaunchKernelGGL(contigs_group_scan_kernel, dim3(1), dim3(1024), 0, stream, e.group_sum,
+                       e.n_groups);
+    if (hipError_t err = hipGetLastError()) return err;
+  }
   const unsigned g = (unsigned)((n_blocks + kEmitSpan - 1) / kEmitSpan);
-  hipLaunchKernelGGL(contigs_emit_kernel, dim3(g), dim3(256), 0, stream, a, (uint32_t)n_blocks);
+  hipLaunchKernelGGL(contigs_emit_kernel, dim3(g), dim3(256), 0, stream, e, (uint32_t)n_blocks);
   return hipGetLastError();
 }
 

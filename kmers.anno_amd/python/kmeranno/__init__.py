@@ -8,6 +8,7 @@ calls raise ``KmerAnnoError``.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -36,7 +37,16 @@ EXPORTS = (
     "kma_bucket_slots", "kma_protein_distances", "kma_protein_best_match",
     "kma_workspace_reserve_batch", "kma_workspace_phases_read", "kma_propose_pegs",
     "kma_hash_annotate", "kma_bucket_slots_for", "kma_table_buckets_for_k",
+    "kma_option_set", "kma_option_get", "kma_workspace_option_set",
 )
+
+# Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
+OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
+OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
+                OPT_HASH_SLICE: 0}
+OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
+_OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
+              "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE}
 
 
 class KmerAnnoError(RuntimeError):
@@ -133,6 +143,9 @@ def load(path: str | None = None):
                                        C.c_double, _int, _vp, _u64, C.POINTER(_u64), _u64p]
         L.kma_contig_window_count.restype = _u64
         L.kma_contig_window_count.argtypes = [_u64p, _u32, _int]
+        L.kma_option_set.argtypes = [_int, C.c_int64]
+        L.kma_option_get.argtypes = [_int, C.POINTER(C.c_int64)]
+        L.kma_workspace_option_set.argtypes = [_vp, _int, C.c_int64]
         _lib = L
     return _lib
 
@@ -140,6 +153,36 @@ def load(path: str | None = None):
 def _check(rc: int):
     if rc != OK:
         raise KmerAnnoError(rc, load().kma_last_error().decode(errors="replace"))
+
+
+def set_option(option: int, value: int):
+    """Library-wide tuning default (OPT_* ; see include/kmeranno.h)."""
+    _check(load().kma_option_set(option, int(value)))
+
+
+def get_option(option: int) -> int:
+    v = C.c_int64()
+    _check(load().kma_option_get(option, C.byref(v)))
+    return v.value
+
+
+def reset_options():
+    for o, v in OPT_DEFAULTS.items():
+        set_option(o, v)
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Set options by name (layout=, block_proteins=, defer=, host_pieces=, hash_slice=) for
+    the body, then restore the previous values."""
+    old = {_OPT_NAMES[k]: get_option(_OPT_NAMES[k]) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(_OPT_NAMES[k], v)
+        yield
+    finally:
+        for o, v in old.items():
+            set_option(o, v)
 
 
 def device_count() -> int:
@@ -295,6 +338,10 @@ class Workspace:
     def reserve_contigs(self, n_bases: int):
         _check(load().kma_workspace_reserve_contigs(self._h, n_bases))
 
+    def set_option(self, option: int, value: int = OPT_DEFAULT):
+        """Per-workspace override of OPT_BLOCK_PROTEINS / OPT_DEFER (OPT_DEFAULT: none)."""
+        _check(load().kma_workspace_option_set(self._h, option, int(value)))
+
     def timing(self, enable: bool = True):
         """Per-phase hipEvent timing of the device calls made with this workspace."""
         _check(load().kma_workspace_timing(self._h, int(enable)))
@@ -351,10 +398,10 @@ def choose_layout(k: int, n_buckets: int, build):
     themselves (kma_table_build_device into their own buffer, e.g. one RCCL broadcasts):
     build(m) builds the table with layout m into the caller's buffer and returns its status
     {full, entries, longest chain, displaced}. Returns (m, status); the kept layout is the one
-    built last. KMA_MINIMIZER forces the size rule's answer."""
+    built last. A forced layout (OPT_LAYOUT) is the size rule's answer."""
     m = layout_for(k, n_buckets)
     st = build(m)
-    if os.environ.get("KMA_MINIMIZER", "") in ("0", "6", "7"):
+    if get_option(OPT_LAYOUT) != -1:
         return m, st
 
     def disp(s):

@@ -36,20 +36,55 @@ def shard(residues: np.ndarray, offsets: np.ndarray, world: int, rank: int):
     return res, off, lo
 
 
-def broadcast_table(slots, src: int = 0):
-    """Replicate the signature table's slot array (a torch tensor) from `src` to every rank."""
+def _multi() -> bool:
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.broadcast(slots, src=src)
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _staged(op, tensor, writes_back: bool = True, **kw):
+    """Run collective `op` on `tensor`. RCCL ("nccl") works on device memory directly; gloo
+    (the CPU backend, used to rehearse several ranks on one GPU) has no device reduce, so a
+    device tensor is staged through host memory around the collective and copied back where
+    the collective defines the result (`writes_back`)."""
+    import torch.distributed as dist
+    if getattr(tensor, "is_cuda", False) and dist.get_backend() == "gloo":
+        host = tensor.cpu()
+        op(host, **kw)
+        if writes_back:
+            tensor.copy_(host)
+    else:
+        op(tensor, **kw)
+    return tensor
+
+
+def broadcast_table(slots, src: int = 0):
+    """Replicate the signature table's slot array (a torch tensor) from `src` to every rank
+    (RCCL broadcast over xGMI; host-staged under gloo)."""
+    import torch.distributed as dist
+    if _multi():
+        _staged(dist.broadcast, slots, src=src)
     return slots
+
+
+def broadcast(tensor, src: int = 0):
+    """Any small tensor from `src` to every rank (layout choice, flags)."""
+    return broadcast_table(tensor, src)
 
 
 def reduce_tallies(tally, dst: int = 0):
     """Sum the per-function tallies (int32 tensor) of every rank into rank `dst`."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(tally, dst=dst)
+    if _multi():
+        _staged(dist.reduce, tally, writes_back=dist.get_rank() == dst, dst=dst)
     return tally
+
+
+def all_reduce_max(tensor):
+    """Element-wise max over ranks, in place (the bench's per-rank times)."""
+    import torch.distributed as dist
+    if _multi():
+        _staged(dist.all_reduce, tensor, op=dist.ReduceOp.MAX)
+    return tensor
 
 
 def gather_results(local: np.ndarray, n_total: int, lo: int, dst: int = 0):
@@ -67,3 +102,13 @@ def gather_results(local: np.ndarray, n_total: int, lo: int, dst: int = 0):
         out[start:start + len(arr)] = arr
     _ = torch  # torch is the transport; numpy holds the result
     return out
+
+
+def gather_objects(obj, dst: int = 0):
+    """Every rank's `obj` as a list on rank `dst` (None elsewhere; [obj] with one rank)."""
+    import torch.distributed as dist
+    if not _multi():
+        return [obj]
+    parts = [None] * dist.get_world_size() if dist.get_rank() == dst else None
+    dist.gather_object(obj, parts, dst=dst)
+    return parts

@@ -34,6 +34,16 @@ def native_lib():
     return kmeranno.load()
 
 
+@pytest.fixture(autouse=True)
+def _library_options():
+    """Every test starts and ends with the library's default tuning options (tests that force a
+    layout, block size or grid set them through the ABI, kma_option_set)."""
+    yield
+    import kmeranno
+    if kmeranno._lib is not None:
+        kmeranno.reset_options()
+
+
 @pytest.fixture(scope="session")
 def oracle_c():
     from oracle import c_oracle

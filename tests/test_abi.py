@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -25,8 +26,29 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 4
+    assert native_lib.kma_abi_version() == 5
     assert isinstance(native_lib.kma_last_error(), bytes)
+
+
+def test_options_set_get_validate_restore(native_lib):
+    """Tuning options go through the ABI (kma_option_set / _get), not the environment: defaults,
+    range checks (KMA_E_INVALID, value unchanged), the context manager restores, and the
+    library ignores the old environment variables (a plain build has no KMA_TUNING_ENV)."""
+    import kmeranno as k
+    for o, v in k.OPT_DEFAULTS.items():
+        assert k.get_option(o) == v
+    for o, bad in ((k.OPT_LAYOUT, 5), (k.OPT_BLOCK_PROTEINS, 9), (k.OPT_DEFER, 65),
+                   (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (99, 0)):
+        with pytest.raises(k.KmerAnnoError) as e:
+            k.set_option(o, bad)
+        assert e.value.code == k.E_INVALID
+    with k.options(layout=7, block_proteins=1, defer=0, host_pieces=3, hash_slice=1000):
+        assert [k.get_option(o) for o in (1, 2, 3, 4, 5)] == [7, 1, 0, 3, 1000]
+        assert k.layout_for(8, 1000) == 7
+    assert [k.get_option(o) for o in (1, 2, 3, 4, 5)] == [-1, 0, -1, 0, 0]
+    assert k.layout_for(8, 1000) == 6
+    src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
+    assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src
 
 
 def test_bucket_sizing_host_helper(native_lib):
@@ -56,16 +78,16 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
 
 def test_table_layout_host_helper(native_lib, monkeypatch):
     """Layout choice: minimizer m = 6 up to 134M keys at load factor 0.5 (2^28 slots), m = 7
-    beyond; KMA_MINIMIZER forces 0 (flat), 6 or 7, read per call."""
+    beyond; the KMA_OPT_LAYOUT option forces 0 (flat), 6 or 7, read per call."""
     import kmeranno
-    monkeypatch.delenv("KMA_MINIMIZER", raising=False)
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1)
     nb6 = (1 << 28) // kmeranno.bucket_slots()
     assert kmeranno.layout_for(8, nb6) == 6
     assert kmeranno.layout_for(8, nb6 + 1) == 7
     assert kmeranno.layout_for(5, 1 << 30) == 5  # m <= K
-    monkeypatch.setenv("KMA_MINIMIZER", "0")
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, 0)
     assert kmeranno.layout_for(8, 1000) == 0
-    monkeypatch.setenv("KMA_MINIMIZER", "7")
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, 7)
     assert kmeranno.layout_for(8, 1000) == 7
 
 

@@ -66,11 +66,11 @@ def test_config5_size_sample_and_properties(kma, oracle_c, c5data, monkeypatch):
         assert t.info.n_entries > 0.99 * len(sig.keys)
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
         # property 0: the two-pass grid gives the same outputs on the whole batch
-        monkeypatch.setenv("KMA_DEFER", "3")
+        kma.set_option(kma.OPT_DEFER, 3)
         got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
         for a, b in zip(got, (fid, cnt, st, tally)):
             assert (a == b).all()
-        monkeypatch.delenv("KMA_DEFER")
+        kma.set_option(kma.OPT_DEFER, -1)
         # property 1: the same batch cut into uneven shards through the device entry point
         d_res = torch.from_numpy(res).to(dev)
         d_off = torch.from_numpy(off.view(np.int64)).to(dev)
@@ -105,7 +105,7 @@ def test_config5_load_factor_09(kma, oracle_c, c5data, monkeypatch):
     tables of the other layouts."""
     sig, res, off, _, _ = c5data
     n_fid = sig.n_fid
-    monkeypatch.delenv("KMA_MINIMIZER", raising=False)
+    kma.set_option(kma.OPT_LAYOUT, -1)
     with kma.SignatureTable.from_packed(sig.keys, sig.fids, K) as t:
         ref = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
     with kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=0.9) as t:
@@ -125,7 +125,7 @@ def test_config5_load_factor_09(kma, oracle_c, c5data, monkeypatch):
     assert (tally == np.bincount(fid[st == 1], minlength=n_fid)).all()
     _sample_vs_oracle(oracle_c, sig, res, off, fid, cnt, st, seed=91)
     for m in {"0", "6", "7"} - {str(kept)}:
-        monkeypatch.setenv("KMA_MINIMIZER", m)
+        kma.set_option(kma.OPT_LAYOUT, int(m))
         with kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=0.9) as t:
             assert t.info.minimizer_len == int(m)
             other = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)

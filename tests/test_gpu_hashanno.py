@@ -115,7 +115,7 @@ def test_hash_annotate_rejects_bad_input(kma):
 @pytest.mark.parametrize("slice_cand", ["1", "700", "5000"])
 def test_hash_scores_in_prototype_slices(kma, oracle_c, small_gto, monkeypatch, slice_cand):
     """Candidates are sorted and run-length encoded in slices of whole prototypes (each below
-    hipcub's 2^31 element limit; KMA_HASH_SLICE lowers the slice size here): a slice's best
+    hipcub's 2^31 element limit; the KMA_OPT_HASH_SLICE option lowers the slice size here): a slice's best
     similarity replaces the running best only when strictly higher, so ties still go to the
     earlier prototype (exact copies placed in different slices) and the result equals the
     one-slice call and the oracle."""
@@ -125,7 +125,7 @@ def test_hash_scores_in_prototype_slices(kma, oracle_c, small_gto, monkeypatch, 
     protos = [_mut(rng, p, rng.uniform(0.1, 0.4)) for p in prots]
     protos = protos[:150] + prots[:10] + protos[150:] + prots[:10]  # ties across slices
     ref = _both(kma, oracle_c, prots, protos, 8, 0.0125)
-    monkeypatch.setenv("KMA_HASH_SLICE", slice_cand)
+    kma.set_option(kma.OPT_HASH_SLICE, int(slice_cand))
     got = _both(kma, oracle_c, prots, protos, 8, 0.0125)
     for a, b in zip(got, ref):
         assert (a == b).all()

@@ -24,21 +24,22 @@ K = 8
 @pytest.fixture(params=["auto", "7", "0"], ids=["m-auto", "m7", "flat"])
 def layout(request, monkeypatch):
     """Table layouts: the size-derived minimizer layout (m = 6 up to 134M keys at load factor
-    0.5, c5 included), the m = 7 layout of larger tables, and the flat fallback (KMA_MINIMIZER is read
-    per table creation)."""
-    if request.param == "auto":
-        monkeypatch.delenv("KMA_MINIMIZER", raising=False)
-    else:
-        monkeypatch.setenv("KMA_MINIMIZER", request.param)
+    0.5, c5 included), the m = 7 layout of larger tables, and the flat fallback (the KMA_OPT_LAYOUT
+    option, read per table creation)."""
+    import kmeranno
+    kmeranno.load()
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1 if request.param == "auto" else int(request.param))
     return request.param
 
 
 @pytest.fixture(params=["direct", "defer"])
 def path(request, monkeypatch):
-    """Grids of the protein kernel: every group in block order (KMA_DEFER=0), and the two-pass
+    """Grids of the protein kernel: every group in block order (KMA_OPT_DEFER = 0), and the two-pass
     grid deferring groups of fewer than 2 probe steps (forced on every batch; automatic only
-    for grids of 1-4 resident waves). KMA_DEFER is read per call."""
-    monkeypatch.setenv("KMA_DEFER", "0" if request.param == "direct" else "2")
+    for grids of 1-4 resident waves). The option is read per call."""
+    import kmeranno
+    kmeranno.load()
+    kmeranno.set_option(kmeranno.OPT_DEFER, 0 if request.param == "direct" else 2)
     return request.param
 
 
@@ -151,10 +152,10 @@ def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defe
     kmers = [synth.unpack_key(x) for x in wl.keys]
     ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
-    monkeypatch.setenv("KMA_DEFER", defer)
+    kma.set_option(kma.OPT_DEFER, int(defer))
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
         for bp in ("4", "1", "4", "1"):
-            monkeypatch.setenv("KMA_BLOCK_PROTEINS", bp)
+            kma.set_option(kma.OPT_BLOCK_PROTEINS, int(bp))
             fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0,
                                                         n_fid=2000)
             assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
@@ -303,7 +304,7 @@ def test_config2_size_vs_oracle(kma, oracle_c, path, monkeypatch):
         assert t.info.minimizer_len == 6
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
         if path == "direct":
-            monkeypatch.delenv("KMA_DEFER")
+            kma.set_option(kma.OPT_DEFER, -1)
             got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
             for a, b in zip(got, (fid, cnt, st, tally)):
                 assert (a == b).all()
@@ -523,11 +524,109 @@ def test_contigs_device_api_planted_genome(kma, oracle_c):
         ws.close()
 
 
+def test_contigs_device_graph_capture_replay(kma, oracle_c):
+    """kma_annotate_contigs_device keeps no host state between calls (the emit pass's last
+    block zeroes the group sums the probe added into), so one call captured in a hipGraph and
+    replayed several times gives the oracle's hits and total every time, and the tally grows by
+    one call's worth per replay."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_contig_workload(300_000, 5, 57, table_size=200_000, n_fid=400)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    e = oracle_c.annotate_contigs(oracle_c.Table(kmers, wl.fids.astype(np.int32)), wl.dna,
+                                  wl.offsets, 11, K)
+    dev = torch.device("cuda", 0)
+    n_bases = int(wl.offsets[-1])
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        ws = kma.Workspace(0)
+        ws.reserve_contigs(n_bases)
+        d_dna = torch.from_numpy(wl.dna).to(dev)
+        d_off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
+        cap = len(e[0]) + 3
+        d_hits = torch.zeros(cap * kma.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        d_nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        tally = torch.zeros(wl.n_contig * 400, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), wl.n_contig,
+                                        n_bases, 11, d_hits.data_ptr(), cap, d_nh.data_ptr(),
+                                        tally.data_ptr(), 400,
+                                        torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert int(d_nh.item()) == 0  # captured, not run
+        for rep in range(1, 4):
+            d_hits.zero_()
+            d_nh.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert int(d_nh.item()) == len(e[0]), rep
+            hits = d_hits.cpu().numpy().view(kma.HIT_DTYPE)[:len(e[0])]
+            for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"],
+                             hits["fid"]), e):
+                assert (a == b).all(), rep
+            expect = np.zeros((wl.n_contig, 400), np.int64)
+            np.add.at(expect, (e[0], e[4]), rep)
+            assert (tally.cpu().numpy().reshape(wl.n_contig, 400) == expect).all(), rep
+        del g
+        ws.close()
+
+
+def test_contigs_device_many_groups_scanned(kma):
+    """A device call of more than kDirectGroups x 256 probe blocks (> 67M bases: the emit pass
+    scans the group sums first instead of summing them per block) equals the same genome cut
+    into calls below that size, hit for hit after re-basing, with the same total."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_contig_workload(2_000_000, 8, 77, table_size=300_000, n_fid=300)
+    # 40 copies of the genome: 80 Mbp in 320 contigs (1,221 emit-offset groups)
+    reps = 40
+    n0 = int(wl.offsets[-1])
+    dna = np.concatenate([np.tile(wl.dna[:n0], reps), np.zeros(64, np.uint8)])
+    off = np.concatenate([[0]] + [wl.offsets[1:] + np.uint64(i * n0) for i in range(reps)])
+    off = off.astype(np.uint64)
+    n_contig, n_bases = len(off) - 1, int(off[-1])
+    assert n_bases > 1024 * 256 * 256
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
+        ws = kma.Workspace(0)
+        ws.reserve_contigs(n_bases)
+        d_dna = torch.from_numpy(dna).to(dev)
+        d_nh = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def call(lo, hi):
+            sub = off[lo:hi + 1]
+            d_off = torch.from_numpy(sub.view(np.int64)).to(dev)
+            cap = 12_000_000
+            d_hits = torch.zeros(cap * kma.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), hi - lo,
+                                        int(sub[-1] - sub[0]), 11, d_hits.data_ptr(), cap,
+                                        d_nh.data_ptr(), 0, 0, stream)
+            torch.cuda.synchronize()
+            nh = int(d_nh.item())
+            assert nh <= cap
+            return d_hits.cpu().numpy().view(kma.HIT_DTYPE)[:nh].copy()
+
+        whole = call(0, n_contig)
+        per = len(wl.offsets) - 1
+        pieces = []
+        for i in range(reps):
+            h = call(i * per, (i + 1) * per)
+            h["contig"] += i * per
+            pieces.append(h)
+        again = call(0, n_contig)
+        ws.close()
+    cut = np.concatenate(pieces)
+    assert len(whole) > 100_000 and len(whole) == len(cut)
+    for f in ("contig", "left", "strand", "frame", "fid"):
+        assert (whole[f] == cut[f]).all() and (again[f] == whole[f]).all()
+
+
 def test_contigs_device_repeated_calls_of_different_sizes(kma, oracle_c):
     """One workspace, calls alternating between a whole genome and a prefix of its contigs (a
-    different number of emit-offset groups): the probe adds block counts into one of two
-    group-sum buffers and each emit pass zeroes the other, so every call must start from clean
-    sums whatever the size of the call before it."""
+    different number of emit-offset groups): every call must start from clean group sums
+    whatever the size of the call before it (the emit pass of each call zeroes them)."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(400_000, 8, 41, table_size=200_000, n_fid=500)

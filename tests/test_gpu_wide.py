@@ -24,10 +24,9 @@ def kma(native_lib):
 
 @pytest.fixture(params=["auto", "7", "0"], ids=["m-auto", "m7", "flat"])
 def layout(request, monkeypatch):
-    if request.param == "auto":
-        monkeypatch.delenv("KMA_MINIMIZER", raising=False)
-    else:
-        monkeypatch.setenv("KMA_MINIMIZER", request.param)
+    import kmeranno
+    kmeranno.load()
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1 if request.param == "auto" else int(request.param))
     return request.param
 
 
