@@ -417,7 +417,7 @@ def slots_digest(slots) -> int:
     for a in range(0, v.numel(), chunk):
         x = v[a:a + chunk]
         idx = torch.arange(a, a + x.numel(), dtype=torch.int64, device=x.device)
-        total = (total + int(torch.bitwise_xor(x, idx * 0x9E3779B97F4A7C15 % (1 << 62)).sum())) % (1 << 64)
+        total = (total + int(torch.bitwise_xor(x, idx * 0x1E3779B97F4A7C15 % (1 << 62)).sum())) % (1 << 64)
     return total
 
 

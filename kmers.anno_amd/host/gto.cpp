@@ -119,6 +119,96 @@ struct Parser {
       }
     }
   }
+  // Skip one value without building it (the apply loader's unwanted members: contig DNA,
+  // feature locations, ...): strings by a memchr to each quote, containers by depth.
+  void skip_string() {
+    ++p;  // opening quote
+    for (;;) {
+      const char* q = static_cast<const char*>(std::memchr(p, '"', end - p));
+      if (!q) error("unterminated string");
+      const char* b = q;
+      while (b > p && b[-1] == '\\') --b;
+      p = q + 1;
+      if (((q - b) & 1) == 0) return;  // an even run of backslashes: the quote closes
+    }
+  }
+  void skip() {
+    ws();
+    if (p >= end) error("unexpected end");
+    if (*p == '"') return skip_string();
+    if (*p != '{' && *p != '[') {
+      (void)value();  // scalars are small
+      return;
+    }
+    int depth = 0;
+    while (p < end) {
+      const char c = *p;
+      if (c == '"') {
+        skip_string();
+        continue;
+      }
+      ++p;
+      if (c == '{' || c == '[') ++depth;
+      else if ((c == '}' || c == ']') && --depth == 0) return;
+    }
+    error("unterminated container");
+  }
+  // Members of an object, calling f(key) with p at the value; f consumes the value.
+  template <class F>
+  void members(F f) {
+    ws();
+    if (p >= end || *p != '{') error("expected object");
+    ++p;
+    ws();
+    if (p < end && *p == '}') {
+      ++p;
+      return;
+    }
+    for (;;) {
+      ws();
+      const std::string k = string();
+      ws();
+      if (p >= end || *p != ':') error("expected ':'");
+      ++p;
+      ws();
+      f(k);
+      ws();
+      if (p < end && *p == ',') {
+        ++p;
+        continue;
+      }
+      if (p < end && *p == '}') {
+        ++p;
+        return;
+      }
+      error("expected ',' or '}'");
+    }
+  }
+  template <class F>
+  void elements(F f) {
+    ws();
+    if (p >= end || *p != '[') error("expected array");
+    ++p;
+    ws();
+    if (p < end && *p == ']') {
+      ++p;
+      return;
+    }
+    for (;;) {
+      ws();
+      f();
+      ws();
+      if (p < end && *p == ',') {
+        ++p;
+        continue;
+      }
+      if (p < end && *p == ']') {
+        ++p;
+        return;
+      }
+      error("expected ',' or ']'");
+    }
+  }
   Json value() {
     ws();
     if (p >= end) error("unexpected end");
@@ -211,14 +301,58 @@ struct Parser {
 };
 
 std::string slurp(const std::string& path) {
-  std::ifstream f(path, std::ios::binary);
+  FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("cannot open " + path);
-  std::ostringstream o;
-  o << f.rdbuf();
-  return o.str();
+  std::string s;
+  struct stat st;
+  if (fstat(fileno(f), &st) == 0 && st.st_size > 0) s.resize((size_t)st.st_size);
+  size_t n = s.empty() ? 0 : std::fread(&s[0], 1, s.size(), f);
+  s.resize(n);
+  char buf[1 << 16];  // whatever fstat did not announce (pipes, growing files)
+  while (size_t m = std::fread(buf, 1, sizeof buf, f)) s.append(buf, m);
+  std::fclose(f);
+  return s;
+}
+
+std::string scalar_string(Parser& ps) {  // a string or number member as text
+  ps.ws();
+  if (ps.p < ps.end && *ps.p == '"') return ps.string();
+  return ps.value().as_string();
 }
 
 }  // namespace
+
+Genome load_genome_pegs(const std::string& path) {
+  const std::string text = slurp(path);
+  Parser ps{text.data(), text.data(), text.data() + text.size()};
+  Genome g;
+  ps.members([&](const std::string& k) {
+    if (k == "id") {
+      g.id = scalar_string(ps);
+    } else if (k == "scientific_name") {
+      g.name = scalar_string(ps);
+    } else if (k == "genetic_code") {
+      g.genetic_code = (int)ps.value().as_int(11);
+    } else if (k == "features") {
+      ps.elements([&]() {
+        Feature ft;
+        ps.members([&](const std::string& fk) {
+          if (fk == "id") ft.id = scalar_string(ps);
+          else if (fk == "type") ft.type = scalar_string(ps);
+          else if (fk == "function") ft.function = scalar_string(ps);
+          else if (fk == "protein_translation") ft.protein = scalar_string(ps);
+          else ps.skip();
+        });
+        g.features.push_back(std::move(ft));
+      });
+    } else {
+      ps.skip();  // contigs (their DNA), close genomes, subsystems, ...
+    }
+  });
+  ps.ws();
+  if (ps.p != ps.end) ps.error("trailing characters");
+  return g;
+}
 
 Json parse_json(const std::string& text) {
   Parser ps{text.data(), text.data(), text.data() + text.size()};

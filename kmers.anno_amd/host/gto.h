@@ -43,6 +43,10 @@ struct Genome {
   std::vector<const Feature*> pegs() const;  // Genome.getPegs(): CDS features in file order
 };
 Genome load_genome(const std::string& path);
+// What `apply` reads (ApplyKmerProcessor.java:116-147): id, name, genetic code and the features'
+// id / type / function / protein_translation. Every other member (contig DNA above all) is
+// skipped without being built; contigs stays empty.
+Genome load_genome_pegs(const std::string& path);
 
 // GenomeDirectory: the *.gto files of a directory, sorted by file name.
 std::vector<std::string> genome_files(const std::string& dir);

@@ -41,19 +41,19 @@ def _multi() -> bool:
     return dist.is_initialized() and dist.get_world_size() > 1
 
 
-def _staged(op, tensor, writes_back: bool = True, **kw):
-    """Run collective `op` on `tensor`. RCCL ("nccl") works on device memory directly; gloo
+def _staged(collective, tensor, writes_back: bool = True, **kw):
+    """Run `collective` on `tensor`. RCCL ("nccl") works on device memory directly; gloo
     (the CPU backend, used to rehearse several ranks on one GPU) has no device reduce, so a
     device tensor is staged through host memory around the collective and copied back where
     the collective defines the result (`writes_back`)."""
     import torch.distributed as dist
     if getattr(tensor, "is_cuda", False) and dist.get_backend() == "gloo":
         host = tensor.cpu()
-        op(host, **kw)
+        collective(host, **kw)
         if writes_back:
             tensor.copy_(host)
     else:
-        op(tensor, **kw)
+        collective(tensor, **kw)
     return tensor
 
 

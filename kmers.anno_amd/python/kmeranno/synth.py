@@ -152,6 +152,66 @@ def make_workload(n_seq: int, table_size: int, n_fid: int, seed: int, k: int = 8
     return Workload(sig.keys, sig.fids, n_fid, residues, offsets, kinds, true_fid)
 
 
+def role_name(fid: int) -> str:
+    return f"ROLE{fid:07d}"
+
+
+def write_kmer_db(path: str, keys: np.ndarray, fids: np.ndarray, k: int = 8):
+    """The headerless kmerdb.tbl of `apply` (kmer<TAB>roleId per row, file order)."""
+    codes = np.zeros((len(keys), k + 1), np.uint8)
+    for j in range(k):
+        codes[:, j] = ((keys >> np.uint64(5 * (k - 1 - j))) & np.uint64(31)).astype(np.uint8) + 64
+    codes[:, k] = ord("\t")
+    with open(path, "wb") as f:
+        step = 1 << 20
+        for a in range(0, len(keys), step):
+            roles = np.char.add(np.char.mod("ROLE%07d", fids[a:a + step].astype(np.int64)), "\n")
+            rows = np.char.add(codes[a:a + step].view(f"S{k + 1}").ravel(),
+                               roles.astype("S"))
+            f.write(b"".join(rows.tolist()))
+
+
+def write_roles_in_use(path: str, n_fid: int, every: int = 1):
+    """roles.in.use: role id<TAB>description, every `every`-th function."""
+    with open(path, "w") as f:
+        f.writelines(f"{role_name(i)}\tsynthetic role {i}\n" for i in range(0, n_fid, every))
+
+
+def write_genome_dir(out_dir: str, sig: SignatureSet, n_genomes: int, pegs_per_genome: int,
+                     seed: int, contig_bp: int = 0, first: int = 0) -> list:
+    """Synthetic GTO files for `apply` (small.gto-like: id, scientific_name, genetic_code,
+    contigs, features of type CDS with protein_translation; the function is the peg's true
+    role or "hypothetical protein"). Proteins come from make_queries (the SURVEY §8(d) mix);
+    each genome gets one random contig of contig_bp bases (skipped by the apply loader, but
+    read). Returns [(genome id, residues, offsets)] per genome, in file-name order."""
+    os.makedirs(out_dir, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    out = []
+    for g in range(first, first + n_genomes):
+        res, off, _, true_fid = make_queries(sig, pegs_per_genome, seed * 7919 + g)
+        gid = f"{100000 + g}.{g % 97 + 1}"
+        feats = []
+        for i in range(pegs_per_genome):
+            prot = res[int(off[i]):int(off[i + 1])].tobytes().decode()
+            fn = role_name(int(true_fid[i])) if true_fid[i] >= 0 else "hypothetical protein"
+            loc = f'[["{gid}.con.0001", {3 * i + 1}, "+", {3 * len(prot) + 3}]]'
+            feats.append(f'{{"id": "fig|{gid}.peg.{i + 1}", "type": "CDS", "location": {loc}, '
+                         f'"function": "{fn}", "protein_translation": "{prot}", '
+                         f'"annotations": [["synthetic", "bench", 0.0]]}}')
+        dna = b"acgt"[0:0]
+        if contig_bp:
+            dna = np.frombuffer(b"acgt", np.uint8)[rng.integers(0, 4, contig_bp)].tobytes()
+        text = (f'{{"id": "{gid}", "scientific_name": "Synthetica genomica {g}", '
+                f'"genetic_code": 11, "domain": "Bacteria", '
+                f'"contigs": [{{"id": "{gid}.con.0001", "dna": "{dna.decode()}"}}], '
+                f'"features": [' + ", ".join(feats) + ']}')
+        with open(os.path.join(out_dir, f"{gid}.gto"), "w") as f:
+            f.write(text)
+        out.append((gid, res, off))
+    order = sorted(range(len(out)), key=lambda i: f"{out[i][0]}.gto")
+    return [out[i] for i in order]
+
+
 # BASELINE.json configs -> (n_seq, table_size, n_fid, seed)
 CONFIGS = {
     "c1": (100, 1_000, 100, 1),

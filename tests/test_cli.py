@@ -3,6 +3,7 @@ reference's own genome fixture small.gto. Expected reports are built here from t
 per-protein calls with the reporters' rules (rep/DefaultApplyKmerReporter.java:43-55,
 rep/VerifyApplyKmerReporter.java:32-45). Error-path tests need no GPU."""
 import gzip
+import json
 import os
 import shutil
 import subprocess
@@ -80,6 +81,59 @@ def test_kma_apply_reports(kma_bin, oracle_c, small_gto, apply_inputs, min_hits)
     out = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.splitlines() == exp_apply
+    out = subprocess.run(args[:2] + ["--format", "VERIFY"] + args[2:], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == exp_verify
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,batch", [(1, 1), (4, 500_000), (8, 1 << 40)])
+def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads, batch):
+    """`kma apply` over a directory of 14 synthetic GTOs (600 pegs each, a contig of DNA the
+    loader skips): GTOs parsed ahead by a thread pool, consecutive genomes batched into one
+    native call of >= `batch` residues (1: a call per genome, as round 3; 500k: several
+    genomes per call; 2^40: one call for the directory). APPLY and VERIFY reports equal the
+    oracle-derived reports line for line, genomes in file-name order
+    (ApplyKmerProcessor.java:116-151, rep/DefaultApplyKmerReporter.java:43-55)."""
+    from kmeranno import synth
+    sig = synth.make_table(200_000, 400, 5, 8)
+    gdir = tmp_path / "gtos"
+    genomes = synth.write_genome_dir(str(gdir), sig, 14, 600, seed=3, contig_bp=20_000)
+    synth.write_kmer_db(str(tmp_path / "db.tbl"), sig.keys, sig.fids)
+    synth.write_roles_in_use(str(tmp_path / "roles"), 400, every=3)
+    kmers = [synth.unpack_key(x) for x in sig.keys]
+    ot = oracle_c.Table(kmers, sig.fids.astype(np.int32))
+    col = {synth.role_name(i): j for j, i in enumerate(range(0, 400, 3))}
+    exp_apply, exp_verify = [], ["genome_id\tpeg_id\trole\thits\tfunction"]
+    for gid, res, off in genomes:
+        fid, cnt, st = oracle_c.apply(ot, res, off, 8, 5, 0)
+        counts = [0] * len(col)
+        for i in np.flatnonzero(st == 1):
+            role = synth.role_name(int(fid[i]))
+            if role in col:
+                counts[col[role]] += 1
+        exp_apply.append(gid + "\t" + "\t".join(map(str, counts)))
+        _, _, _, true_fid = synth.make_queries(sig, 600, 3 * 7919 + int(gid.split(".")[0]) - 100000)
+        for i in np.flatnonzero(st == 1):
+            fn = synth.role_name(int(true_fid[i])) if true_fid[i] >= 0 else "hypothetical protein"
+            exp_verify.append(f"{gid}\tfig|{gid}.peg.{i + 1}\t{synth.role_name(int(fid[i]))}\t"
+                              f"{int(cnt[i])}\t{fn}")
+    args = [kma_bin, "apply", "--threads", str(threads), "--batch", str(batch),
+            str(tmp_path / "db.tbl"), str(tmp_path / "roles"), str(gdir)]
+    out = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == exp_apply
+    stats = [ln for ln in out.stderr.splitlines() if "apply-stats" in ln]
+    assert len(stats) == 1
+    st = json.loads(stats[0].split("apply-stats ", 1)[1])
+    assert st["genomes"] == 14 and st["proteins"] == 14 * 600
+    if batch == 1:
+        assert st["calls"] == 14
+    elif batch == 1 << 40:
+        assert st["calls"] == 1
+    else:
+        assert 1 < st["calls"] < 14
     out = subprocess.run(args[:2] + ["--format", "VERIFY"] + args[2:], capture_output=True,
                          text=True, timeout=300)
     assert out.returncode == 0, out.stderr

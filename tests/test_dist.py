@@ -54,6 +54,14 @@ def _worker(rank, world, port, q):
         g_st = dist.gather_results(st, wl.n_seq, lo)
         slots = torch.arange(16, dtype=torch.int64) if rank == 0 else torch.zeros(16, dtype=torch.int64)
         dist.broadcast_table(slots, src=0)
+        # the bench's other collectives: per-rank times max-reduced, the layout broadcast
+        times = torch.tensor([1.0 + rank, 5.0 - rank], dtype=torch.float64)
+        dist.all_reduce_max(times)
+        lay = torch.tensor([7 if rank == 0 else 0], dtype=torch.int32)
+        dist.broadcast(lay, src=0)
+        objs = dist.gather_objects(("r", rank))
+        assert times.tolist() == [2.0, 5.0] and int(lay.item()) == 7
+        assert objs == ([("r", 0), ("r", 1)] if rank == 0 else None)
         if rank == 0:
             efid, ecnt, est = c_oracle.apply(table, wl.residues, wl.offsets, 8, 5, 0)
             ok = ((g_fid == efid).all() and (g_st == est).all()
