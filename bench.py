@@ -398,6 +398,93 @@ def bench_contigs(args, rank, world, dev, stream, sp):
     del slots
 
 
+def bench_genomes(args):
+    """The drop-in's own regime: `kma apply` (the C++ mirror of ApplyKmerProcessor over the C
+    ABI) on a directory of synthetic GTOs, as a SEEDtk pipeline runs it (ApplyKmerProcessor.
+    java:116-151: genome by genome, every peg's protein). Timed: the command's genome loop
+    (parse + native calls + reports; its apply-stats line), pipelined (GTO parse-ahead pool,
+    several genomes per native call) and as round 3 ran it (one thread, one call per genome).
+    The APPLY report is checked line for line against the oracle's calls."""
+    import shutil
+    import tempfile
+    from oracle import c_oracle
+    n_gen, pegs = args.genomes, 4000
+    t_size, n_fid, seed = 10_000_000, 10_000, 4  # c4's function model and 10^7-row table
+    root = tempfile.mkdtemp(prefix="kma_genomes_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        t0 = time.perf_counter()
+        sig = synth.make_table(t_size, n_fid, seed, K)
+        db, roles, gdir = (os.path.join(root, x) for x in ("kmerdb.tbl", "roles.in.use", "gtos"))
+        synth.write_kmer_db(db, sig.keys, sig.fids)
+        synth.write_roles_in_use(roles, n_fid, every=10)
+        genomes = []
+        for a in range(0, n_gen, 50):  # progress every 50 genomes
+            genomes += synth.write_genome_dir(gdir, sig, min(50, n_gen - a), pegs, seed=8,
+                                              contig_bp=args.contig_bp, first=a)
+            log(f"genomes written: {a + min(50, n_gen - a)} ({time.perf_counter() - t0:.0f}s)")
+        genomes.sort(key=lambda g: g[0] + ".gto")
+        gbytes = sum(os.path.getsize(os.path.join(gdir, f)) for f in os.listdir(gdir))
+        n_prot = sum(len(g[2]) - 1 for g in genomes)
+        n_win = sum(int(np.maximum(np.diff(g[2]).astype(np.int64) - K + 1, 0).sum())
+                    for g in genomes)
+        log(f"{n_gen} GTOs ({gbytes / 1e9:.2f} GB), {n_prot} proteins, {n_win} windows, "
+            f"generated in {time.perf_counter() - t0:.0f}s")
+        kma = os.path.join(ROOT, "kmers.anno_amd", "build", "kma")
+
+        def run(extra, tag):
+            out_path = os.path.join(root, f"apply_{tag}.txt")
+            with open(out_path, "w") as out:
+                p = subprocess.run([kma, "apply", *extra, db, roles, gdir], stdout=out,
+                                   stderr=subprocess.PIPE, text=True, timeout=1200)
+            if p.returncode != 0:
+                raise RuntimeError(f"kma apply {tag}: rc {p.returncode}\n{p.stderr[-3000:]}")
+            line = [ln for ln in p.stderr.splitlines() if "apply-stats" in ln][-1]
+            stats = json.loads(line.split("apply-stats ", 1)[1])
+            log(f"kma apply {tag}: {stats}")
+            return stats, open(out_path).read().splitlines()
+
+        piped, report = run([], "pipelined")
+        piped2, report2 = run([], "pipelined2")  # the GTOs are in the page cache for both
+        seq, report_seq = run(["--threads", "1", "--batch", "1"], "per_genome")
+        best = min((piped, piped2), key=lambda s: s["loop_s"])
+        # parity: the oracle's calls (restatement of the same loop) -> the APPLY report
+        table, load_s = oracle_table(sig.keys, sig.fids)
+        col = {synth.role_name(i): j for j, i in enumerate(range(0, n_fid, 10))}
+        expect = []
+        for gid, res, off in genomes:
+            fid, _, st = c_oracle.apply_mt(table, res, off, K, MIN_HITS, 0, host_threads())
+            counts = np.zeros(len(col), np.int64)
+            called = fid[st == kmeranno.STATUS_CALLED]
+            keep = called[called % 10 == 0] // 10
+            np.add.at(counts, keep, 1)
+            expect.append(gid + "\t" + "\t".join(map(str, counts.tolist())))
+        parity = report == expect and report2 == expect and report_seq == expect
+        loop = best["loop_s"]
+        out = {
+            "metric": "genomes annotated/s through `kma apply` (ApplyKmerProcessor mirror over "
+                      "the C ABI), GTO directory",
+            "value": n_gen / loop, "unit": "genomes/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "u64", "data": "synthetic GTOs (seeded; SURVEY.md §8(d) protein mix)",
+            "config": {"workload": f"genomes: {n_gen} GTOs x {pegs} pegs (small.gto-like, one "
+                                   f"{args.contig_bp}-bp contig each) vs the 10^7-row table "
+                                   "(c4's function model), roles.in.use of 1,000 roles",
+                       "gto_bytes": gbytes, "proteins": n_prot, "windows": n_win,
+                       "table_entries": t_size, "k": K, "min_hits": MIN_HITS},
+            "seqs_per_s": n_prot / loop, "lookups_per_s": n_win / loop,
+            "pipelined": best, "pipelined_runs_loop_s": [piped["loop_s"], piped2["loop_s"]],
+            "per_genome_sequential": dict(seq, genomes_per_s=n_gen / seq["loop_s"]),
+            "speedup_vs_per_genome": seq["loop_s"] / loop,
+            "native_call_share": best["native_call_s"] / loop,
+            "apply_report_equals_oracle": parity,
+            "oracle_table_load_s": load_s,
+        }
+        print(json.dumps(out), flush=True)
+        if not parity:
+            sys.exit(1)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
 def e2e_host(table, residues, offsets, n_fid, reps=3):
     """kma_annotate_proteins from host memory (H2D + kernel + D2H through the table's pooled
     pinned staging): best of `reps` calls after one warmup call, in ms."""
@@ -484,7 +571,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["genomes"])
+    ap.add_argument("--genomes", type=int, default=500,
+                    help="genomes workload: GTO files (4,000 pegs each)")
+    ap.add_argument("--contig-bp", type=int, default=4_000_000,
+                    help="genomes workload: bases of each GTO's contig")
     ap.add_argument("--load-factor", type=float, default=0.5)
     ap.add_argument("--n-seq", type=int, default=0,
                     help="override the workload's proteins per rank (tuning runs only)")
@@ -501,6 +592,9 @@ def main():
                          "single-rank calls on rank 0 (exit 1 on a mismatch)")
     args = ap.parse_args()
 
+    if args.workload == "genomes":  # a command-level run: `kma apply` as a child process
+        bench_genomes(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
