@@ -587,11 +587,16 @@ def main():
                          "staged, to rehearse several ranks on one GPU (with --same-device)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses device 0 (multi-rank rehearsal on a 1-GPU box)")
+    ap.add_argument("--packed-input", type=int, default=1, choices=(0, 1),
+                    help="KMA_OPT_PACKED_INPUT: 1 = residues packed to 5 bits by a pack kernel "
+                         "inside the step, then the packed probe (default); 0 = the probe packs "
+                         "ASCII itself")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, check the multi-rank outputs, tally and table against "
                          "single-rank calls on rank 0 (exit 1 on a mismatch)")
     args = ap.parse_args()
 
+    kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, args.packed_input)
     if args.workload == "genomes":  # a command-level run: `kma apply` as a child process
         bench_genomes(args)
         return

@@ -152,6 +152,10 @@ int kma_device_count(int* out_n);
  *   KMA_OPT_HOST_PIECES     host protein calls: staging / kernel pipeline pieces [0: up to 8];
  *                           1..16
  *   KMA_OPT_HASH_SLICE      kma_hash_annotate: candidates per prototype slice [0: 2^31 - 1]
+ *   KMA_OPT_PACKED_INPUT    protein calls [1]: residues are packed to 5 bits before the probe
+ *                           (host calls while staging: the H2D moves 0.625 B per residue;
+ *                           device calls with a pack kernel into the workspace) and the probe
+ *                           reads the packed stream; 0 = the probe packs ASCII itself
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -159,6 +163,7 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_DEFER 3
 #define KMA_OPT_HOST_PIECES 4
 #define KMA_OPT_HASH_SLICE 5
+#define KMA_OPT_PACKED_INPUT 6
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);
@@ -273,13 +278,33 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
  * offsets[n_seq]; n_residues = offsets[n_seq] - offsets[0] (<= the workspace reservation);
  * d_tally (n_fid u32) is accumulated into, not cleared. Asynchronous on `stream`: one kernel
  * launch (annotate_kernel: each window probes the table where it stands, per-protein sets and
- * the vote in LDS).                                                                           */
+ * the vote in LDS), preceded by a pack kernel into the workspace under KMA_OPT_PACKED_INPUT.  */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
                                  uint32_t n_seq, uint64_t n_residues, int min_hits,
                                  uint32_t flags, int32_t* d_fid, int32_t* d_count,
                                  uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
                                  void* stream);
+
+/* ---- packed residue streams ------------------------------------------------------------------
+ * The protein kernel's input format: residue j of a call is the 5-bit code (the table's packing,
+ * 0 for a byte without a code) at bits [5j, 5j + 5) of a big-endian bit stream — byte b of the
+ * stream holds bits [8b, 8b + 8), most significant first; 8 residues fill 5 bytes.
+ *   kma_packed_bytes  : stream bytes for n residues, read padding included (40 per 64 + 16)
+ *   kma_pack_residues : host packing (AVX2 where the CPU has it) of residues[0, n) into out
+ *                       (out_bytes >= kma_packed_bytes(n); the rest is zeroed) with the table's
+ *                       codes (table NULL: the standard alphabet); no device needed
+ *   kma_annotate_packed_device : kma_annotate_proteins_device on a packed stream already in
+ *                       device memory (8-byte aligned): stream residue 0 is residue
+ *                       d_offsets[0]; one kernel launch.                                      */
+uint64_t kma_packed_bytes(uint64_t n_residues);
+int kma_pack_residues(const kma_table* table, const uint8_t* residues, uint64_t n, uint8_t* out,
+                      uint64_t out_bytes);
+int kma_annotate_packed_device(const kma_table* table, kma_workspace* ws, const uint8_t* d_stream,
+                               const uint64_t* d_offsets, uint32_t n_seq, uint64_t n_residues,
+                               int min_hits, uint32_t flags, int32_t* d_fid, int32_t* d_count,
+                               uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
+                               void* stream);
 
 /* ---- 6-frame contig annotation (KmerReference.java:157-203 + table probe) -----------------
  * dna: contigs concatenated (any case; bases other than ACGT translate to 'X'); offsets as

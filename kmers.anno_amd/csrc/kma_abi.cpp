@@ -28,14 +28,15 @@
 #include "kma_distance.h"
 #include "kma_hashanno.h"
 #include "kma_internal.h"
+#include "kma_pack.h"
 
 namespace {
 // ---- options (kma_option_set; include/kmeranno.h) ----------------------------------------------
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 6;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}};
+constexpr int kNumOpts = 7;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
@@ -45,6 +46,7 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_DEFER: return v >= -1 && v <= 64;
     case KMA_OPT_HOST_PIECES: return v >= 0 && v <= 16;
     case KMA_OPT_HASH_SLICE: return v >= 0;
+    case KMA_OPT_PACKED_INPUT: return v == 0 || v == 1;
     default: return false;
   }
 }
@@ -55,7 +57,7 @@ struct EnvOptions {  // tuning builds: the A/B scripts' variables seed the defau
     const std::pair<const char*, int> vars[] = {
         {"KMA_MINIMIZER", KMA_OPT_LAYOUT}, {"KMA_BLOCK_PROTEINS", KMA_OPT_BLOCK_PROTEINS},
         {"KMA_DEFER", KMA_OPT_DEFER}, {"KMA_HOST_PIECES", KMA_OPT_HOST_PIECES},
-        {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}};
+        {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}, {"KMA_PACKED_INPUT", KMA_OPT_PACKED_INPUT}};
     for (const auto& [name, opt] : vars)
       if (const char* e = getenv(name); e && *e) {
         const int64_t v = strtoll(e, nullptr, 10);
@@ -280,6 +282,7 @@ struct kma_workspace {
   int device = 0;
   int n_cu = 256;
   uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
+  uint8_t* d_packed = nullptr; // the call's residues packed (kma_internal.h packed_bytes)
   uint64_t res_cap = 0;        // residues per call
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
   kma_hit* d_cstage = nullptr;
@@ -825,7 +828,9 @@ int kma_table_device_ptr(const kma_table* table, void** d_slots, uint64_t* bytes
 namespace {
 void free_protein_scratch(kma_workspace* ws) {
   if (ws->d_gset) (void)hipFree(ws->d_gset);
+  if (ws->d_packed) (void)hipFree(ws->d_packed);
   ws->d_gset = nullptr;
+  ws->d_packed = nullptr;
   ws->res_cap = 0;
 }
 
@@ -905,6 +910,7 @@ struct PhaseClock {
 };
 
 const char* const kDirectPhases[] = {"annotate_kernel"};
+const char* const kPackedPhases[] = {"pack_kernel", "annotate_kernel"};
 const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
 // Proteins per annotate_kernel block (KMA_BLOCK_PROTEINS=1..8 overrides, read per call): 6 for
@@ -944,17 +950,25 @@ uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
   return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
 }
 
+// How the protein kernel gets its residues: ASCII read directly; ASCII packed on the device
+// first (pack_kernel into the workspace, then the packed kernel: the device entry point's
+// default, KMA_OPT_PACKED_INPUT); a packed stream the caller staged (host entry, packed device
+// entry; stream residue `stream_first` = residue offsets[0]).
+enum class Input { kAscii, kPackOnDevice, kStream };
+
 // The protein path on one replica (device buffers, asynchronous on s).
 int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws,
                          const uint8_t* d_residues, const uint64_t* d_offsets, uint32_t n_seq,
                          uint64_t n_residues, int min_hits, uint32_t flags, int32_t* d_fid,
                          int32_t* d_count, uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
-                         hipStream_t s) {
+                         hipStream_t s, Input input = Input::kAscii, uint64_t stream_first = 0) {
   kma::ProteinArgs a{};
   a.slots = r.d_slots;
   a.n_buckets = (uint32_t)t->n_buckets;
   a.lut = r.d_lut;
-  a.residues = d_residues;
+  a.residues = input == Input::kPackOnDevice ? ws->d_packed : d_residues;
+  a.packed = input != Input::kAscii;
+  a.stream_first = input == Input::kStream ? stream_first : 0;
   a.offsets = d_offsets;
   a.n_seq = n_seq;
   a.n_residues = (uint32_t)n_residues;
@@ -971,8 +985,14 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.block_proteins = block_proteins(ws, n_seq, t->n_buckets * (uint64_t)kma::kBucketBytes);
   a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
   a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
-  PhaseClock clk(ws, s, kDirectPhases, 1);
+  const bool pack = input == Input::kPackOnDevice;
+  PhaseClock clk(ws, s, pack ? kPackedPhases : kDirectPhases, pack ? 2 : 1);
   KMA_HIP(clk.mark());
+  if (pack) {
+    KMA_HIP(kma::launch_pack_residues(d_residues, d_offsets, n_residues, r.d_lut, ws->d_packed,
+                                      s));
+    KMA_HIP(clk.mark());
+  }
   KMA_HIP(kma::launch_annotate(a, s));
   KMA_HIP(clk.mark());
   return KMA_OK;
@@ -1025,6 +1045,48 @@ hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size
   return (hipError_t)err.load();
 }
 
+// The packed form of stage_h2d: stream groups [ga, gb) (64 residues, 40 bytes each) packed from
+// src (residue 64 ga onwards; residues past n_res read as no code) into the pinned buffer and
+// copied to d_stream, in chunks of 2^17 groups on up to 8 threads; `tail` extra zero bytes
+// (the kernel's read padding) follow the last group.
+hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* lut,
+                          const uint8_t* residues, uint64_t n_res, uint64_t ga, uint64_t gb,
+                          uint64_t tail, int device, hipStream_t s) {
+  constexpr uint64_t kChunkGroups = 1u << 17;
+  const uint64_t n_chunks = std::max<uint64_t>(1, (gb - ga + kChunkGroups - 1) / kChunkGroups);
+  auto chunk = [&](uint64_t i) -> hipError_t {
+    const uint64_t g0 = ga + i * kChunkGroups, g1 = std::min(gb, g0 + kChunkGroups);
+    const uint64_t r0 = 64 * g0, r1 = std::min(64 * g1, n_res);
+    const uint64_t bytes = 40 * (g1 - g0) + (g1 == gb ? tail : 0);
+    kma::pack_residues_host(lut, residues + r0, r1 > r0 ? r1 - r0 : 0, h_stream + 40 * g0, bytes);
+    return bytes ? hipMemcpyAsync(d_stream + 40 * g0, h_stream + 40 * g0, bytes,
+                                  hipMemcpyHostToDevice, s)
+                 : hipSuccess;
+  };
+  if (n_chunks <= 2) {
+    for (uint64_t i = 0; i < n_chunks; ++i)
+      if (hipError_t e = chunk(i)) return e;
+    return hipSuccess;
+  }
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t n_threads = std::min<size_t>({8, hw, n_chunks});
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> err{(int)hipSuccess};
+  auto work = [&]() {
+    if (hipSetDevice(device) != hipSuccess) {
+      err = (int)hipErrorInvalidDevice;
+      return;
+    }
+    for (uint64_t i; (i = next++) < n_chunks;)
+      if (hipError_t e = chunk(i)) err = (int)e;
+  };
+  std::vector<std::thread> pool;
+  for (size_t i = 1; i < n_threads; ++i) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  return (hipError_t)err.load();
+}
+
 int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                   const uint64_t* offsets, uint32_t lo, uint32_t hi, int min_hits,
                   uint32_t flags, int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
@@ -1040,7 +1102,11 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   CtxGuard guard{t, c};
   DeviceScope ds(r.device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r.device);
-  const size_t in_bytes = (nres + kResPad + 7) & ~7ull;
+  // KMA_OPT_PACKED_INPUT (default): residues are packed to 5 bits while they are staged (the
+  // H2D moves 0.625 bytes per residue) and the packed kernel reads the stream.
+  const bool packed = opt(KMA_OPT_PACKED_INPUT) != 0;
+  const uint64_t n_groups = (nres + 63) / 64;
+  const size_t in_bytes = packed ? (size_t)kma::packed_bytes(nres) : (nres + kResPad + 7) & ~7ull;
   const size_t off_bytes = (n + 1) * 8ull;
   const size_t out_bytes = n * 9ull + (tally ? n_fid * 4ull : 0) + 16;
   KMA_HIP(c->d_in.reserve(in_bytes));
@@ -1071,6 +1137,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   if (d_tally) KMA_HIP(hipMemsetAsync(d_tally, 0, n_fid * 4ull, s));
   const int n_pieces = (int)std::max<uint64_t>(1, std::min<uint64_t>(max_pieces, nres / kPieceBytes));
   uint32_t pa = 0;  // first protein of the piece (relative to lo)
+  uint64_t ga = 0;  // packed: first stream group the piece stages
   for (int i = 0; i < n_pieces; ++i) {
     uint32_t pb = n;
     if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
@@ -1078,18 +1145,26 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
       pb = (uint32_t)(std::lower_bound(hoff + pa, hoff + n, target) - hoff);
     }
     const uint64_t ra = hoff[pa], rb = i + 1 < n_pieces ? hoff[pb] : nres;
-    KMA_HIP(stage_h2d(c->d_in.p + ra, hin + ra, residues + base + ra, rb - ra, r.device, cs));
-    if (i + 1 == n_pieces) {
-      std::memset(hin + nres, 0, in_bytes - nres);
-      KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres,
-                             hipMemcpyHostToDevice, cs));
+    if (packed) {  // the group holding the piece boundary goes with the earlier piece
+      const uint64_t gb = i + 1 < n_pieces ? std::min(n_groups, (rb + 63) / 64) : n_groups;
+      KMA_HIP(stage_pack_h2d(c->d_in.p, hin, t->lut, residues + base, nres, ga, gb,
+                             i + 1 == n_pieces ? in_bytes - 40 * n_groups : 0, r.device, cs));
+      ga = gb;
+    } else {
+      KMA_HIP(stage_h2d(c->d_in.p + ra, hin + ra, residues + base + ra, rb - ra, r.device, cs));
+      if (i + 1 == n_pieces) {
+        std::memset(hin + nres, 0, in_bytes - nres);
+        KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres,
+                               hipMemcpyHostToDevice, cs));
+      }
     }
     KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
     KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
     if (pb > pa)
       if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + pa, pb - pa,
                                         hoff[pb] - hoff[pa], min_hits, flags, d_fid + pa,
-                                        d_cnt + pa, d_st + pa, d_tally, n_fid, s))
+                                        d_cnt + pa, d_st + pa, d_tally, n_fid, s,
+                                        packed ? Input::kStream : Input::kAscii, hoff[pa]))
         return rc;
     pa = pb;
   }
@@ -1160,6 +1235,7 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   free_protein_scratch(ws);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
+  KMA_HIP(hipMalloc(&ws->d_packed, kma::packed_bytes(n_residues + kResPad)));
   ws->res_cap = n_residues;
   return KMA_OK;
 }
@@ -1269,7 +1345,46 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r->device);
   return annotate_proteins_on(t, *r, ws, d_residues, d_offsets, n_seq, n_residues, min_hits,
                               flags, d_fid, d_count, d_status, d_tally, n_fid,
-                              static_cast<hipStream_t>(stream));
+                              static_cast<hipStream_t>(stream),
+                              opt(KMA_OPT_PACKED_INPUT) ? Input::kPackOnDevice : Input::kAscii);
+}
+
+uint64_t kma_packed_bytes(uint64_t n_residues) { return kma::packed_bytes(n_residues); }
+
+int kma_pack_residues(const kma_table* t, const uint8_t* residues, uint64_t n, uint8_t* out,
+                      uint64_t out_bytes) {
+  if ((n && !residues) || !out) return fail(KMA_E_INVALID, "null argument");
+  if (out_bytes < kma::packed_bytes(n))
+    return fail(KMA_E_CAPACITY, "packed stream of %llu residues needs %llu bytes",
+                (unsigned long long)n, (unsigned long long)kma::packed_bytes(n));
+  uint8_t std_lut[256];
+  if (!t) standard_lut(std_lut);
+  kma::pack_residues_host(t ? t->lut : std_lut, residues, n, out, out_bytes);
+  return KMA_OK;
+}
+
+int kma_annotate_packed_device(const kma_table* t, kma_workspace* ws, const uint8_t* d_stream,
+                               const uint64_t* d_offsets, uint32_t n_seq, uint64_t n_residues,
+                               int min_hits, uint32_t flags, int32_t* d_fid, int32_t* d_count,
+                               uint8_t* d_status, uint32_t* d_tally, uint32_t n_fid,
+                               void* stream) {
+  if (int rc = check_protein_call(t, min_hits, flags)) return rc;
+  if (!ws) return fail(KMA_E_INVALID, "null workspace");
+  Replica rep;
+  if (!replica_on(t, ws->device, &rep))
+    return fail(KMA_E_INVALID, "table has no replica on the workspace's device %d", ws->device);
+  if (n_seq == 0) return KMA_OK;
+  if (!d_stream || !d_offsets || !d_fid || !d_count || !d_status)
+    return fail(KMA_E_INVALID, "null device buffer");
+  if ((uintptr_t)d_stream & 7) return fail(KMA_E_INVALID, "stream must be 8-byte aligned");
+  if (n_residues > ws->res_cap)
+    return fail(KMA_E_CAPACITY, "workspace reserved for %llu residues, call needs %llu",
+                (unsigned long long)ws->res_cap, (unsigned long long)n_residues);
+  DeviceScope ds(rep.device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", rep.device);
+  return annotate_proteins_on(t, rep, ws, d_stream, d_offsets, n_seq, n_residues, min_hits, flags,
+                              d_fid, d_count, d_status, d_tally, n_fid,
+                              static_cast<hipStream_t>(stream), Input::kStream, 0);
 }
 
 int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const uint64_t* offsets,

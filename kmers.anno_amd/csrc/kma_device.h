@@ -59,6 +59,32 @@ __device__ __forceinline__ WinWords window_words(const uint8_t* __restrict__ res
 }
 __device__ __forceinline__ uint64_t win_bytes(const WinWords& w) { return funnel(w.lo, w.hi, w.sh); }
 
+// Packed residue streams (kma_pack_residues, pack_residues_kernel): residue j of a call is the
+// 5-bit code at bits [5j, 5j + 5) of a big-endian bit stream (stream byte b holds bits
+// [8b, 8b + 8), most significant first), so the window at residue j is the stream's 5K bits
+// from bit 5j: exactly its key (first residue most significant). A window's words are the two
+// aligned u64 around its first byte; `sh` packs the byte shift (bits 3..5) and the bit shift
+// within the byte (bits 0..2).
+__device__ __forceinline__ WinWords window_words_packed(const uint8_t* __restrict__ stream,
+                                                        uint64_t j) {
+  const uint64_t bit = 5 * j, byte = bit >> 3;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(stream + (byte & ~7ull));
+  return WinWords{src[0], src[1], (uint32_t)(((byte & 7) << 3) | (bit & 7))};
+}
+__device__ __forceinline__ uint64_t bswap64(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t slo = __builtin_amdgcn_perm(0u, lo, 0x00010203u);  // byte-reverse each dword
+  const uint32_t shi = __builtin_amdgcn_perm(0u, hi, 0x00010203u);
+  return (uint64_t)slo << 32 | shi;
+}
+// The packed window's key. Residues that had no code (0) leave a zero 5-bit group, which no
+// table key has (codes are 1..31): such a window is probed and misses, as its String would.
+template <int K>
+__device__ __forceinline__ uint64_t packed_key(const WinWords& w) {
+  const uint64_t be = bswap64(funnel(w.lo, w.hi, w.sh & 56u));  // stream bytes, MSB first
+  return (be << (w.sh & 7u)) >> (64 - 5 * K);
+}
+
 // 5-bit packing through the table's residue LUT (LDS); false if a byte is not encodable.
 template <int K>
 __device__ __forceinline__ bool pack_window(const uint8_t* lut, uint64_t bytes, uint64_t& key) {

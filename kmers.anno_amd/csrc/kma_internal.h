@@ -334,6 +334,10 @@ struct ProteinArgs {
   // has fewer, so that short groups start after every long one.
   uint32_t defer_below;
   uint32_t n_groups;
+  // Input format: 0 = ASCII residues (a.residues + offsets[s]); 1 = the packed stream of
+  // kma_device.h (5 bits per residue, stream residue 0 = residue offsets[0]).
+  uint32_t packed;
+  uint64_t stream_first;  // packed: stream residue index of residue offsets[0]
 };
 
 struct ContigArgs {
@@ -406,6 +410,12 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
+// ASCII residues [offsets[0], offsets[0] + n) -> the packed stream (packed_bytes(n) bytes; the
+// LUT of the table's replica): pack_residues_kernel.
+hipError_t launch_pack_residues(const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                                const uint8_t* lut, uint8_t* out, hipStream_t stream);
+// Bytes of the packed stream of n residues: 40 per 64 residues and 16 of read padding.
+__host__ __device__ constexpr uint64_t packed_bytes(uint64_t n) { return 40 * ((n + 63) / 64) + 16; }
 hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 hipError_t launch_contigs_probe(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream);
 // Peg-kmer singleton table (KmerReference.countPegKmers + CountMap.getSingletons): every

@@ -320,26 +320,37 @@ __device__ __forceinline__ void head_offsets(const ProteinArgs& a, uint32_t g, G
   h.beg_raw = wave == 0 && lane <= (int)h.np ? a.offsets[h.p0 + lane] : 0u;
   h.span_lo = a.offsets[h.p0] - a.offsets[0];
 }
-// The span's residues from the aligned word at or below its first byte (d_residues is 8-byte
-// aligned): window x of the span starts at byte x + mis of `res`.
+// Window x of the span is at position x + pos0 of `res`. ASCII residues: `res` is the aligned
+// word at or below the span's first byte (d_residues is 8-byte aligned) and pos0 < 8 the byte
+// offset; packed streams (Packed): `res` is the stream and pos0 the span's first residue in it
+// (the stream starts at the call's first residue).
+template <bool Packed>
 __device__ __forceinline__ const uint8_t* head_res(const ProteinArgs& a, const GroupHead& h,
-                                                   uint32_t& mis) {
+                                                   uint64_t& pos0) {
+  if (Packed) {
+    pos0 = a.stream_first + h.span_lo;
+    return a.residues;
+  }
   const uint8_t* res0 = a.residues + a.offsets[0] + h.span_lo;
-  mis = (uint32_t)((uintptr_t)res0 & 7u);
-  return res0 - mis;
+  pos0 = (uintptr_t)res0 & 7u;
+  return res0 - pos0;
 }
-// The group's first probe step's residue words (clamped to the batch, which is readable 32
-// bytes past its end; windows past the span are masked in the loop).
-template <int U>
+template <bool Packed>
+__device__ __forceinline__ WinWords load_win(const uint8_t* __restrict__ res, uint64_t pos) {
+  return Packed ? window_words_packed(res, pos) : window_words(res, pos);
+}
+// The group's first probe step's residue words (clamped to the batch, which is readable past
+// its end; windows past the span are masked in the loop).
+template <int U, bool Packed>
 __device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupHead& h,
                                               uint32_t tw, WinWords (&ww)[U]) {
-  uint32_t mis;
-  const uint8_t* res = head_res(a, h, mis);
+  uint64_t pos0;
+  const uint8_t* res = head_res<Packed>(a, h, pos0);
   const uint64_t lim = a.n_residues - h.span_lo;
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint32_t x = j * 256u + tw;
-    ww[j] = window_words(res, (x < lim ? x : 0u) + mis);
+    ww[j] = load_win<Packed>(res, (x < lim ? x : 0u) + pos0);
   }
 }
 
@@ -347,7 +358,7 @@ __device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupH
 // residue words are in ww. pass 0 / 1: a block of the two-pass grid, which annotates its group
 // only if the group is long (pass 0) / short (pass 1: fewer than defer_below probe steps);
 // pass -1: always. sm.lut is being loaded (read after the first barrier).
-template <int K, int M, int P>
+template <int K, int M, int P, bool Packed>
 __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P>& sm,
                                                const GroupHead& h, WinWords (&ww)[kProbeWin],
                                                const int pass = -1) {
@@ -358,8 +369,8 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   const uint32_t p0 = h.p0, np = h.np;
   const uint64_t beg_raw = h.beg_raw, span_lo = h.span_lo;
   const uint64_t o0 = a.offsets[0];
-  uint32_t mis;
-  const uint8_t* __restrict__ res = head_res(a, h, mis);
+  uint64_t pos0;
+  const uint8_t* __restrict__ res = head_res<Packed>(a, h, pos0);
   if (wave == 0) {  // the block's protein records
     const uint64_t beg = lane <= (int)np ? beg_raw - o0 : 0u;
     const uint64_t end = __shfl_down(beg, 1, 64);
@@ -479,8 +490,13 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const uint32_t x = xs + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
       uint64_t key;
-      const bool ok = pack_window<K>(lut, win_bytes(ww[j]), key) &&
-                      x < span && window_at<P>(pe, x, p);
+      bool ok;
+      if (Packed) {
+        key = packed_key<K>(ww[j]);
+        ok = x < span && window_at<P>(pe, x, p);
+      } else {
+        ok = pack_window<K>(lut, win_bytes(ww[j]), key) && x < span && window_at<P>(pe, x, p);
+      }
       o.klo[j] = (uint32_t)key;
       o.khi[j] = (uint32_t)(key >> 32) << 24;
       o.need[j] = filter_need<kSlotsPerBucket>(o.klo[j]);
@@ -509,7 +525,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint32_t x = xs + j * 256u + tw;
-      ww[j] = window_words(res, (x < span ? x : 0u) + mis);
+      ww[j] = load_win<Packed>(res, (x < span ? x : 0u) + pos0);
     }
   };
   // Compare the quad's buckets, record hits, queue chain walks.
@@ -606,13 +622,13 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   }
 }
 
-template <int K, int M, int P>
+template <int K, int M, int P, bool Packed>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kProteinOcc, 8))) void annotate_kernel(
     ProteinArgs a) {
   __shared__ ProteinSmem<P> sm;
   KMA_CLK(0);
   const int t = threadIdx.x;
-  sm.lut[t] = a.lut[t];  // read after annotate_block's first barrier
+  if (!Packed) sm.lut[t] = a.lut[t];  // read after annotate_block's first barrier
   // Two-pass grid (defer_below > 0): blocks [0, n_groups) annotate the long groups, blocks
   // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
   // one (blocks are dispatched in index order); a block whose group is the other pass's exits
@@ -623,8 +639,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kProteinOcc
   // (the two-pass grid keeps block order: its long-first order is what it is for)
   const uint32_t b = blockIdx.x - (second ? a.n_groups : 0u);
   head_offsets(a, a.defer_below ? b : xcd_group(b, a.n_groups), h);
-  head_residues<kProbeWin>(a, h, lane_window(t), ww);
-  annotate_block<K, M, P>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
+  head_residues<kProbeWin, Packed>(a, h, lane_window(t), ww);
+  annotate_block<K, M, P, Packed>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
   KMA_CLK(5);
   KMA_CLK_HW();
 }
@@ -1174,9 +1190,75 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Residue packing (ASCII -> the packed stream of kma_device.h): a thread turns 64 residues of
+// the call (from d_residues + offsets[0]) into 5 stream words (320 bits), codes through the
+// table's LUT (0 for a byte without a code). Aligned 8-byte loads around the residues, one
+// funnel shift per word; the last, partial group by bytes. Reads 1 B and writes 0.625 B per
+// residue: ~0.1 ms for c5's 310M residues.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pack64(const uint8_t (&lut)[256], const uint8_t (&b)[64],
+                                       uint64_t* __restrict__ out) {
+  uint64_t w[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint64_t c = lut[b[i]];
+    const int k = (5 * i) >> 6, o = (5 * i) & 63;  // MSB-first bit o of stream word k
+    if (o <= 59) {
+      w[k] |= c << (59 - o);
+    } else {
+      w[k] |= c >> (o - 59);
+      w[k + 1] |= c << (123 - o);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) out[k] = bswap64(w[k]);  // stream bytes in memory order
+}
+
+__global__ __launch_bounds__(256) void pack_residues_kernel(const uint8_t* __restrict__ residues,
+                                                            const uint64_t* __restrict__ offsets,
+                                                            uint64_t n, const uint8_t* lut_g,
+                                                            uint64_t* __restrict__ out) {
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = lut_g[threadIdx.x];
+  __syncthreads();
+  const uint8_t* base = residues + offsets[0];
+  const uint32_t mis = (uint32_t)((uintptr_t)base & 7u);
+  const uint64_t* aligned = reinterpret_cast<const uint64_t*>(base - mis);
+  const uint64_t groups = (n + 63) / 64;
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += gridDim.x * 256ull) {
+    uint8_t b[64];
+    if (64 * g + 64 <= n) {  // whole group: 9 aligned words (the batch is readable past its end)
+      uint64_t v[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) v[k] = aligned[8 * g + k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t x = funnel(v[k], v[k + 1], mis * 8u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[8 * k + j] = (uint8_t)(x >> (8 * j));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) b[i] = 64 * g + i < n ? base[64 * g + i] : 0u;
+    }
+    pack64(lut, b, out + 5 * g);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) out[5 * groups + threadIdx.x] = 0;  // read padding
+}
+
 }  // namespace
 
 // ---- launchers ----------------------------------------------------------------------------------
+hipError_t launch_pack_residues(const uint8_t* residues, const uint64_t* offsets, uint64_t n,
+                                const uint8_t* lut, uint8_t* out, hipStream_t stream) {
+  const uint64_t groups = (n + 63) / 64;
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (groups + 255) / 256));
+  hipLaunchKernelGGL(pack_residues_kernel, dim3(g), dim3(256), 0, stream, residues, offsets, n,
+                     lut, reinterpret_cast<uint64_t*>(out));
+  return hipGetLastError();
+}
+
 static unsigned grid_for(uint64_t n, unsigned cap = 8192) {
   uint64_t g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -1218,8 +1300,11 @@ struct AnnotateLaunch {
     if (bp != a.block_proteins) return hipErrorInvalidValue;
     const unsigned blocks = (a.n_seq + bp - 1) / bp;
     if (a.n_groups != blocks) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((annotate_kernel<K, M, P>), dim3(a.defer_below ? 2 * blocks : blocks),
-                       dim3(256), 0, stream, a);
+    const dim3 grid(a.defer_below ? 2 * blocks : blocks);
+    if (a.packed)
+      hipLaunchKernelGGL((annotate_kernel<K, M, P, true>), grid, dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((annotate_kernel<K, M, P, false>), grid, dim3(256), 0, stream, a);
     return hipGetLastError();
     }
   }

@@ -38,15 +38,18 @@ EXPORTS = (
     "kma_workspace_reserve_batch", "kma_workspace_phases_read", "kma_propose_pegs",
     "kma_hash_annotate", "kma_bucket_slots_for", "kma_table_buckets_for_k",
     "kma_option_set", "kma_option_get", "kma_workspace_option_set",
+    "kma_packed_bytes", "kma_pack_residues", "kma_annotate_packed_device",
 )
 
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
+OPT_PACKED_INPUT = 6
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
-                OPT_HASH_SLICE: 0}
+                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1}
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
 _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
-              "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE}
+              "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
+              "packed_input": OPT_PACKED_INPUT}
 
 
 class KmerAnnoError(RuntimeError):
@@ -146,6 +149,11 @@ def load(path: str | None = None):
         L.kma_option_set.argtypes = [_int, C.c_int64]
         L.kma_option_get.argtypes = [_int, C.POINTER(C.c_int64)]
         L.kma_workspace_option_set.argtypes = [_vp, _int, C.c_int64]
+        L.kma_packed_bytes.restype = _u64
+        L.kma_packed_bytes.argtypes = [_u64]
+        L.kma_pack_residues.argtypes = [_vp, _u8p, _u64, _u8p, _u64]
+        L.kma_annotate_packed_device.argtypes = [_vp, _vp, _vp, _vp, _u32, _u64, _int, _u32,
+                                                 _vp, _vp, _vp, _vp, _u32, _vp]
         _lib = L
     return _lib
 
@@ -450,6 +458,30 @@ def annotate_proteins_device(table: SignatureTable, ws: Workspace, d_residues: i
     _check(load().kma_annotate_proteins_device(table._h, ws._h, d_residues, d_offsets, n_seq,
                                                n_residues, min_hits, flags, d_fid, d_count,
                                                d_status, d_tally or None, n_fid, stream or None))
+
+
+def packed_bytes(n_residues: int) -> int:
+    return int(load().kma_packed_bytes(n_residues))
+
+
+def pack_residues(table, residues: np.ndarray, n: int | None = None) -> np.ndarray:
+    """The packed residue stream (5 bits per residue, the table's codes; table None: the
+    standard alphabet) of residues[0, n)."""
+    residues = np.ascontiguousarray(residues, np.uint8)
+    n = len(residues) if n is None else n
+    out = np.empty(packed_bytes(n), np.uint8)
+    _check(load().kma_pack_residues(table._h if table is not None else None, residues, n, out,
+                                    len(out)))
+    return out
+
+
+def annotate_packed_device(table: SignatureTable, ws: Workspace, d_stream: int, d_offsets: int,
+                           n_seq: int, n_residues: int, min_hits: int, flags: int, d_fid: int,
+                           d_count: int, d_status: int, d_tally: int = 0, n_fid: int = 0,
+                           stream: int = 0):
+    _check(load().kma_annotate_packed_device(table._h, ws._h, d_stream, d_offsets, n_seq,
+                                             n_residues, min_hits, flags, d_fid, d_count,
+                                             d_status, d_tally or None, n_fid, stream or None))
 
 
 def annotate_contigs(table: SignatureTable, dna: np.ndarray, offsets: np.ndarray,

@@ -113,3 +113,27 @@ def test_choose_layout_rule():
             return st[m]
         m, s = kmeranno.choose_layout(8, 25_000_000, build)
         assert m == want[case] and built[-1] == m and s == st[m], (case, built)
+
+
+def _pack_reference(res: np.ndarray) -> np.ndarray:
+    """The packed stream spelled out bit by bit (include/kmeranno.h): residue j's standard code
+    at big-endian stream bits [5j, 5j + 5)."""
+    from kmeranno import std_codes
+    codes = std_codes(res).astype(np.uint8)
+    bits = ((codes[:, None] >> np.arange(4, -1, -1, dtype=np.uint8)) & 1).reshape(-1)
+    return np.packbits(bits)  # MSB first, zero-padded to a byte
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 63, 64, 65, 200, 4096 + 37, 100_003])
+def test_pack_residues_host_matches_bitwise_reference(native_lib, n):
+    """kma_pack_residues (AVX2 body + scalar tail, chosen by the CPU) against a bitwise numpy
+    spelling of the format, on residues with every byte class: A-Z, '*', lower case, digits,
+    bytes >= 128 (no code: a zero group); the padding after the stream is zero."""
+    import kmeranno
+    rng = np.random.default_rng(n)
+    pool = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYBJOUXZ*az09-\xff\x80", np.uint8)
+    res = pool[rng.integers(0, len(pool), n)]
+    got = kmeranno.pack_residues(None, res)
+    want = _pack_reference(res)
+    assert len(got) == kmeranno.packed_bytes(n) == 40 * ((n + 63) // 64) + 16
+    assert (got[:len(want)] == want).all() and not got[len(want):].any()

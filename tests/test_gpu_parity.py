@@ -43,6 +43,17 @@ def path(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["packed", "ascii"])
+def input_mode(request):
+    """The protein kernel's input: residues packed to 5 bits first (KMA_OPT_PACKED_INPUT = 1,
+    the default: on the host while staging, or by the pack kernel for device calls), or ASCII
+    packed by the probe itself through the LDS LUT (0)."""
+    import kmeranno
+    kmeranno.load()
+    kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, 1 if request.param == "packed" else 0)
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def kma(native_lib):
     import kmeranno
@@ -76,7 +87,7 @@ def _oracle_apply(oracle_c, rows, prots, min_hits=5, flags=0):
     return [[int(s), inv.get(int(f)), int(n)] for f, n, s in zip(efid, ecnt, est)]
 
 
-def test_edge_cases_golden(kma, layout, path):
+def test_edge_cases_golden(kma, layout, path, input_mode):
     for c in json.load(open(os.path.join(GOLDEN, "apply_edge.json"))):
         got = _gpu_apply(kma, [tuple(r) for r in c["rows"]], c["proteins"], c["min_hits"],
                          c["flags"])
@@ -108,7 +119,7 @@ def test_min_hits_must_be_positive(kma):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2])
-def test_config1_golden(kma, layout, flags, path):
+def test_config1_golden(kma, layout, flags, path, input_mode):
     z = np.load(os.path.join(GOLDEN, "apply_c1.npz"))
     with kma.SignatureTable.from_rows([bytes(r).decode() for r in z["table_kmers"]],
                                       z["table_fids"], K) as t:
@@ -122,7 +133,7 @@ def test_config1_golden(kma, layout, flags, path):
 
 
 @pytest.mark.parametrize("lf,flags", [(0.5, 0), (0.5, 1), (0.5, 2), (0.9, 0), (0.95, 0)])
-def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags):
+def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags, input_mode):
     """2,000 proteins vs a 200k-entry table (seeded), packed-key table path, load factors up
     to 0.95 (overflow chains and filter bits), both window conventions and multiset counting."""
     from kmeranno import synth
@@ -162,7 +173,7 @@ def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defe
             assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
 
 
-def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path):
+def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path, input_mode):
     """Proteins whose distinct-kmer sets do not fit the block's LDS pool keep them in workspace
     memory: long ones, and short ones behind a long one in the same block; duplicates inside
     them still count once."""
@@ -702,3 +713,47 @@ def test_peg_connect_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, stric
     assert len(hits) == len(e[0])
     for a, b in zip((hits["contig"], hits["left"], hits["strand"], hits["frame"], hits["fid"]), e):
         assert (a == b).all()
+
+
+def test_packed_stream_device_entry_equals_ascii(kma, oracle_c):
+    """kma_annotate_packed_device on a stream packed on the host (kma_pack_residues: the AVX2 /
+    scalar packer, the table's codes, extra table symbols included) equals the ASCII kernel and
+    the oracle on proteins holding bytes with no code (lower case, digits, 'X', '*', bytes >=
+    128: their windows are probed as zero-group keys and miss), called on uneven sub-batches
+    whose d_offsets[0] is not 0 (stream residue 0 = residue d_offsets[0])."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    rng = np.random.default_rng(77)
+    wl = synth.make_workload(3000, 150_000, 700, seed=12)
+    res = wl.residues.copy()
+    n_res = int(wl.offsets[-1])
+    noise = rng.random(n_res) < 0.004
+    res[:n_res][noise] = np.frombuffer(b"xq7X*-\xc3", np.uint8)[rng.integers(0, 7, int(noise.sum()))]
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    kmers[:40] = [k[:3] + "-" + k[4:] for k in kmers[:40]]  # an extra table symbol ('-')
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    efid, ecnt, est = oracle_c.apply(ot, res, wl.offsets, K, 5, 0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    with kma.SignatureTable.from_rows(kmers, wl.fids, K) as t:
+        assert t.info.n_extra_syms == 1
+        ws = kma.Workspace(0, n_res)
+        cuts = [0, 1, 2, 999, 1000, 2047, 3000]
+        d_off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
+        outs = [torch.empty(wl.n_seq, dtype=d, device=dev) for d in (torch.int32, torch.int32, torch.uint8)]
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            r0, r1 = int(wl.offsets[lo]), int(wl.offsets[hi])
+            stream_h = kma.pack_residues(t, res[r0:r1])
+            d_stream = torch.from_numpy(stream_h).to(dev)
+            kma.annotate_packed_device(t, ws, d_stream.data_ptr(), d_off.data_ptr() + 8 * lo, hi - lo,
+                                       r1 - r0, 5, 0, outs[0].data_ptr() + 4 * lo,
+                                       outs[1].data_ptr() + 4 * lo, outs[2].data_ptr() + lo, 0, 0,
+                                       stream)
+        torch.cuda.synchronize()
+        fid, cnt, st = (o.cpu().numpy() for o in outs)
+        kma.set_option(kma.OPT_PACKED_INPUT, 0)
+        afid, acnt, ast, _ = kma.annotate_proteins(t, res, wl.offsets, 5, 0)
+        ws.close()
+    assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    assert (ast == est).all() and (afid == efid).all() and (acnt == ecnt).all()
+    assert (st == 1).sum() > 500
