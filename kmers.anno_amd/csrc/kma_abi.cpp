@@ -2064,29 +2064,29 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
   KMA_HIP(b.alloc(&uhead, gw));
   size_t need = 0, tb = 0;
   auto grow = [&](size_t t) { need = std::max(need, t); };
-  KMA_HIP(kma::cub_select_flagged_u64(nullptr, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u64(nullptr, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
   grow(tb);
-  KMA_HIP(kma::cub_select_flagged_u32(nullptr, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u32(nullptr, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
   grow(tb);
-  KMA_HIP(kma::cub_sort_pairs_u64_u32(nullptr, &tb, gpk, skey, gpp, sprot, g.total, kb, nullptr));
+  KMA_HIP(kma::prim_sort_pairs_u64_u32(nullptr, &tb, gpk, skey, gpp, sprot, g.total, kb, nullptr));
   grow(tb);
-  KMA_HIP(kma::cub_excl_sum_u32_u64(nullptr, &tb, nullptr, nullptr, std::max<uint64_t>(p.total, 1), nullptr));
+  KMA_HIP(kma::prim_excl_sum_u32_u64(nullptr, &tb, nullptr, nullptr, std::max<uint64_t>(p.total, 1), nullptr));
   grow(tb);
   void* temp;
   KMA_HIP(b.alloc(&temp, need ? need : 1));
   tb = need;
-  KMA_HIP(kma::cub_select_flagged_u64(temp, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u64(temp, &tb, g.sorted, g.first, gpk, d_n, g.total, nullptr));
   tb = need;
-  KMA_HIP(kma::cub_select_flagged_u32(temp, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u32(temp, &tb, g.owner, g.first, gpp, d_n, g.total, nullptr));
   uint64_t n_pairs = 0;
   KMA_HIP(hipMemcpy(&n_pairs, d_n, 8, hipMemcpyDeviceToHost));
   tb = need;
-  KMA_HIP(kma::cub_sort_pairs_u64_u32(temp, &tb, gpk, skey, gpp, sprot, n_pairs, kb, nullptr));
+  KMA_HIP(kma::prim_sort_pairs_u64_u32(temp, &tb, gpk, skey, gpp, sprot, n_pairs, kb, nullptr));
   KMA_HIP(kma::launch_run_heads(skey, n_pairs, uhead, uidx, nullptr));
   tb = need;
-  KMA_HIP(kma::cub_select_flagged_u64(temp, &tb, skey, uhead, ukeys, d_n + 1, n_pairs, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u64(temp, &tb, skey, uhead, ukeys, d_n + 1, n_pairs, nullptr));
   tb = need;
-  KMA_HIP(kma::cub_select_flagged_u32(temp, &tb, uidx, uhead, ustart, d_n + 1, n_pairs, nullptr));
+  KMA_HIP(kma::prim_select_flagged_u32(temp, &tb, uidx, uhead, ustart, d_n + 1, n_pairs, nullptr));
   KMA_HIP(kma::launch_set_end(ustart, d_n + 1, n_pairs, nullptr));
   // candidates: one (prototype, protein) per shared distinct key
   kma::HashArgs a{};
@@ -2109,7 +2109,7 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
   a.coff = coff;
   KMA_HIP(kma::launch_cand_count(a, nullptr));
   tb = need;
-  KMA_HIP(kma::cub_excl_sum_u32_u64(temp, &tb, a.ccount, coff, p.total, nullptr));
+  KMA_HIP(kma::prim_excl_sum_u32_u64(temp, &tb, a.ccount, coff, p.total, nullptr));
   uint64_t last_off = 0;
   uint32_t last_cnt = 0;
   if (p.total) {
@@ -2128,7 +2128,7 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
   for (uint64_t* q : {best_bits, a.best_bits}) KMA_HIP(hipMemset(q, 0, n_gp * 8ull));
   for (uint32_t* q : {best_proto, a.best_proto}) KMA_HIP(hipMemset(q, 0xFF, n_gp * 4ull));
   // Candidates are scored in slices of whole prototypes (file order) whose sort and run-length
-  // encoding stay below 2^31 elements (hipcub's int counts); a slice's best per protein
+  // encoding stay below 2^31 elements (the int counts of the CUB-style APIs this was first written against; rocPRIM's select and sort take size_t, its run-length encode still unsigned); a slice's best per protein
   // replaces the running best only when strictly higher, so earlier prototypes keep ties.
   // KMA_OPT_HASH_SLICE (tests) lowers the slice size.
   uint64_t slice_cap = (1ull << 31) - 1;
@@ -2162,8 +2162,8 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
     int pbits = 1;
     while (pbits < 32 && (1ull << pbits) < n_pt) ++pbits;
     size_t t2 = 0, t3 = 0;
-    KMA_HIP(kma::cub_sort_keys_u64(nullptr, &t2, cand, csorted, max_slice, 32 + pbits, nullptr));
-    KMA_HIP(kma::cub_rle_u64(nullptr, &t3, csorted, runs, run_len, d_n + 2, max_slice, nullptr));
+    KMA_HIP(kma::prim_sort_keys_u64(nullptr, &t2, cand, csorted, max_slice, 32 + pbits, nullptr));
+    KMA_HIP(kma::prim_rle_u64(nullptr, &t3, csorted, runs, run_len, d_n + 2, max_slice, nullptr));
     void* temp2;
     const size_t t23 = std::max(t2, t3);
     KMA_HIP(b.alloc(&temp2, t23 ? t23 : 1));
@@ -2181,9 +2181,9 @@ int kma_hash_annotate(const uint8_t* gres, const uint64_t* goff, uint32_t n_gp,
       a.cand_base = cum[cut[i]];
       KMA_HIP(kma::launch_cand_emit(a, nullptr));
       t2 = t23;
-      KMA_HIP(kma::cub_sort_keys_u64(temp2, &t2, cand, csorted, nc, 32 + pbits, nullptr));
+      KMA_HIP(kma::prim_sort_keys_u64(temp2, &t2, cand, csorted, nc, 32 + pbits, nullptr));
       t3 = t23;
-      KMA_HIP(kma::cub_rle_u64(temp2, &t3, csorted, runs, run_len, d_n + 2, nc, nullptr));
+      KMA_HIP(kma::prim_rle_u64(temp2, &t3, csorted, runs, run_len, d_n + 2, nc, nullptr));
       KMA_HIP(kma::launch_score(a, nc, nullptr));
       KMA_HIP(kma::launch_choose(a, nc, nullptr));
       KMA_HIP(kma::launch_merge_best(best_bits, best_proto, a.best_bits, a.best_proto, n_gp,

@@ -9,13 +9,14 @@
 // GPU form, for batches of proteins and any protein length:
 //   window_keys_kernel  every window of every protein packed to a 5K-bit key (K <= 12) at its
 //                       residue position; positions that start no window hold the sentinel
-//   (hipcub) segmented radix sort of each protein's positions
+//   (rocPRIM) segmented radix sort of each protein's positions
 //   distinct_kernel     |S| per protein: first occurrences of non-sentinel keys (wave per protein)
 //   pair_kernel         per (a, b) pair: the distinct keys of the smaller set, each looked up by
 //                       binary search in the other's sorted keys (wave per pair, lanes stride)
 // Integer work only; outputs are (|A|, |B|, |A n B|) per pair, the host forms the distance in
 // double exactly as the restated Java expression.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocprim.hpp uses memset without including it)
+#include <rocprim/rocprim.hpp>
 
 #include "kma_distance.h"
 
@@ -152,8 +153,8 @@ hipError_t launch_segmented_sort(void* temp, size_t* temp_bytes, const uint64_t*
                                  uint64_t* out, uint64_t n_items, uint32_t n_seg,
                                  const uint64_t* seg_begin, const uint64_t* seg_end, int bits,
                                  hipStream_t s) {
-  return hipcub::DeviceSegmentedRadixSort::SortKeys(temp, *temp_bytes, in, out, (int)n_items,
-                                                    (int)n_seg, seg_begin, seg_end, 0, bits, s);
+  return rocprim::segmented_radix_sort_keys(temp, *temp_bytes, in, out, (unsigned)n_items, n_seg,
+                                            seg_begin, seg_end, 0u, (unsigned)bits, s);
 }
 
 hipError_t launch_distinct(const uint64_t* sorted, const uint64_t* off, uint32_t n, uint32_t* size,

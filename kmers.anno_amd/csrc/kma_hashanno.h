@@ -53,18 +53,18 @@ hipError_t launch_proto_cum(const uint64_t* coff, const uint32_t* ccount, const 
 hipError_t launch_merge_best(uint64_t* best_bits, uint32_t* best_proto, uint64_t* slice_bits,
                              uint32_t* slice_proto, uint32_t n, hipStream_t s);
 hipError_t launch_choose(const HashArgs& a, uint64_t n_max, hipStream_t s);
-hipError_t cub_select_flagged_u64(void* temp, size_t* tb, const uint64_t* in, const uint8_t* f,
+hipError_t prim_select_flagged_u64(void* temp, size_t* tb, const uint64_t* in, const uint8_t* f,
                                   uint64_t* out, uint64_t* n_out, uint64_t n, hipStream_t s);
-hipError_t cub_select_flagged_u32(void* temp, size_t* tb, const uint32_t* in, const uint8_t* f,
+hipError_t prim_select_flagged_u32(void* temp, size_t* tb, const uint32_t* in, const uint8_t* f,
                                   uint32_t* out, uint64_t* n_out, uint64_t n, hipStream_t s);
-hipError_t cub_sort_pairs_u64_u32(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko,
+hipError_t prim_sort_pairs_u64_u32(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko,
                                   const uint32_t* vi, uint32_t* vo, uint64_t n, int bits,
                                   hipStream_t s);
-hipError_t cub_sort_keys_u64(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko, uint64_t n,
+hipError_t prim_sort_keys_u64(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko, uint64_t n,
                              int bits, hipStream_t s);
-hipError_t cub_excl_sum_u32_u64(void* temp, size_t* tb, const uint32_t* in, uint64_t* out,
+hipError_t prim_excl_sum_u32_u64(void* temp, size_t* tb, const uint32_t* in, uint64_t* out,
                                 uint64_t n, hipStream_t s);
-hipError_t cub_rle_u64(void* temp, size_t* tb, const uint64_t* in, uint64_t* uniq, uint32_t* len,
+hipError_t prim_rle_u64(void* temp, size_t* tb, const uint64_t* in, uint64_t* uniq, uint32_t* len,
                        uint64_t* n_runs, uint64_t n, hipStream_t s);
 
 }  // namespace kma

@@ -19,7 +19,8 @@
 //   score:      similarity per (prototype, protein) in double (the Java expression), match
 //               counts per prototype, best similarity per protein (u64 atomicMax on the
 //               non-negative double's bits), then the smallest prototype index at that value
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocprim.hpp uses memset without including it)
+#include <rocprim/rocprim.hpp>
 
 #include "kma_hashanno.h"
 
@@ -216,31 +217,32 @@ hipError_t launch_choose(const HashArgs& a, uint64_t n_max, hipStream_t s) {
   return hipGetLastError();
 }
 
-// hipcub wrappers (temp == nullptr: size query).
-hipError_t cub_select_flagged_u64(void* temp, size_t* tb, const uint64_t* in, const uint8_t* f,
+// rocPRIM wrappers (temp == nullptr: size query).
+hipError_t prim_select_flagged_u64(void* temp, size_t* tb, const uint64_t* in, const uint8_t* f,
                                   uint64_t* out, uint64_t* n_out, uint64_t n, hipStream_t s) {
-  return hipcub::DeviceSelect::Flagged(temp, *tb, in, f, out, n_out, (int)n, s);
+  return rocprim::select(temp, *tb, in, f, out, n_out, (size_t)n, s);
 }
-hipError_t cub_select_flagged_u32(void* temp, size_t* tb, const uint32_t* in, const uint8_t* f,
+hipError_t prim_select_flagged_u32(void* temp, size_t* tb, const uint32_t* in, const uint8_t* f,
                                   uint32_t* out, uint64_t* n_out, uint64_t n, hipStream_t s) {
-  return hipcub::DeviceSelect::Flagged(temp, *tb, in, f, out, n_out, (int)n, s);
+  return rocprim::select(temp, *tb, in, f, out, n_out, (size_t)n, s);
 }
-hipError_t cub_sort_pairs_u64_u32(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko,
+hipError_t prim_sort_pairs_u64_u32(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko,
                                   const uint32_t* vi, uint32_t* vo, uint64_t n, int bits,
                                   hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(temp, *tb, ki, ko, vi, vo, (int)n, 0, bits, s);
+  return rocprim::radix_sort_pairs(temp, *tb, ki, ko, vi, vo, (size_t)n, 0u, (unsigned)bits, s);
 }
-hipError_t cub_sort_keys_u64(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko, uint64_t n,
+hipError_t prim_sort_keys_u64(void* temp, size_t* tb, const uint64_t* ki, uint64_t* ko, uint64_t n,
                              int bits, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeys(temp, *tb, ki, ko, (int)n, 0, bits, s);
+  return rocprim::radix_sort_keys(temp, *tb, ki, ko, (size_t)n, 0u, (unsigned)bits, s);
 }
-hipError_t cub_excl_sum_u32_u64(void* temp, size_t* tb, const uint32_t* in, uint64_t* out,
+hipError_t prim_excl_sum_u32_u64(void* temp, size_t* tb, const uint32_t* in, uint64_t* out,
                                 uint64_t n, hipStream_t s) {
-  return hipcub::DeviceScan::ExclusiveSum(temp, *tb, in, out, (int)n, s);
+  return rocprim::exclusive_scan(temp, *tb, in, out, (uint64_t)0, (size_t)n,
+                                 rocprim::plus<uint64_t>(), s);
 }
-hipError_t cub_rle_u64(void* temp, size_t* tb, const uint64_t* in, uint64_t* uniq, uint32_t* len,
+hipError_t prim_rle_u64(void* temp, size_t* tb, const uint64_t* in, uint64_t* uniq, uint32_t* len,
                        uint64_t* n_runs, uint64_t n, hipStream_t s) {
-  return hipcub::DeviceRunLengthEncode::Encode(temp, *tb, in, uniq, len, n_runs, (int)n, s);
+  return rocprim::run_length_encode(temp, *tb, in, (unsigned)n, uniq, len, n_runs, s);
 }
 
 }  // namespace kma

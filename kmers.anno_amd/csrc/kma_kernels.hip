@@ -12,7 +12,8 @@
 //
 // Integer / byte work only: the bound is HBM (or Infinity-Cache) random access to 64-byte
 // buckets, not MFMA.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocprim.hpp uses memset without including it)
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -1148,7 +1149,7 @@ __global__ __launch_bounds__(1024) void contigs_group_scan_kernel(uint64_t* sums
 // block counts itself done (one agent-scope atomic, issued once its offsets are read) and the
 // block that finishes last zeroes the group sums and the counter for the next call (so calls
 // on one workspace may be graph-captured and replayed). Measured alternatives for the offsets
-// (c3, profiles/r03_ab/): hipcub's two-kernel scan ~10 us; a ticket letting the probe's last
+// (c3, profiles/r03_ab/): a library two-kernel scan ~10 us; a ticket letting the probe's last
 // block scan, 0.6 ms (20k atomics on one address serialize); a one-block scan kernel, ~18 us (a
 // single CU's dependent round trips); a group-sum kernel between probe and emit, and one emit
 // block per probe block (12.5 us for c3's 19.5k blocks of ~9 hits).
@@ -1340,8 +1341,8 @@ hipError_t launch_peg_windows(const uint8_t* residues, const uint64_t* offsets, 
 hipError_t launch_sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* keys_in,
                              uint64_t* keys_out, const uint32_t* vals_in, uint32_t* vals_out,
                              uint64_t n, int key_bits, hipStream_t stream) {
-  return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_in, keys_out, vals_in,
-                                            vals_out, (int)n, 0, key_bits, stream);
+  return rocprim::radix_sort_pairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                   (size_t)n, 0u, (unsigned)key_bits, stream);
 }
 
 hipError_t launch_singleton_flags(const uint64_t* sorted_keys, uint64_t n, uint8_t* flags,
@@ -1357,22 +1358,20 @@ hipError_t launch_select_flagged(void* temp, size_t* temp_bytes, const uint64_t*
                                  hipStream_t stream) {
   // Keys and values: two passes over the same flags keep the order identical.
   size_t need = 0;
-  hipError_t e = hipcub::DeviceSelect::Flagged(nullptr, need, keys_in, flags, keys_out, n_out,
-                                               (int)n, stream);
+  hipError_t e = rocprim::select(nullptr, need, keys_in, flags, keys_out, n_out, (size_t)n,
+                                 stream);
   if (e != hipSuccess) return e;
   size_t need2 = 0;
-  e = hipcub::DeviceSelect::Flagged(nullptr, need2, vals_in, flags, vals_out, n_out, (int)n,
-                                    stream);
+  e = rocprim::select(nullptr, need2, vals_in, flags, vals_out, n_out, (size_t)n, stream);
   if (e != hipSuccess) return e;
   need = std::max(need, need2);
   if (!temp) {
     *temp_bytes = need;
     return hipSuccess;
   }
-  e = hipcub::DeviceSelect::Flagged(temp, need, keys_in, flags, keys_out, n_out, (int)n, stream);
+  e = rocprim::select(temp, need, keys_in, flags, keys_out, n_out, (size_t)n, stream);
   if (e != hipSuccess) return e;
-  return hipcub::DeviceSelect::Flagged(temp, need, vals_in, flags, vals_out, n_out, (int)n,
-                                       stream);
+  return rocprim::select(temp, need, vals_in, flags, vals_out, n_out, (size_t)n, stream);
 }
 
 hipError_t launch_build_windows(const uint8_t* residues, const uint64_t* offsets, uint32_t n_seq,
@@ -1389,14 +1388,14 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
                                   uint8_t* flags, uint32_t* head_idx, uint32_t* run, void* temp,
                                   size_t* temp_bytes, hipStream_t stream) {
   if (!temp)
-    return hipcub::DeviceScan::InclusiveScan(nullptr, *temp_bytes, head_idx, run, hipcub::Max(),
-                                             (int)n, stream);
+    return rocprim::inclusive_scan(nullptr, *temp_bytes, head_idx, run, (size_t)n,
+                                   rocprim::maximum<uint32_t>(), stream);
   hipLaunchKernelGGL(sig_heads_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, n, flags,
                      head_idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::InclusiveScan(temp, *temp_bytes, head_idx, run, hipcub::Max(), (int)n,
-                                        stream);
+  e = rocprim::inclusive_scan(temp, *temp_bytes, head_idx, run, (size_t)n,
+                              rocprim::maximum<uint32_t>(), stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(sig_clear_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, tags, run,
                      n, flags);

@@ -18,7 +18,8 @@
 //
 // Restated external semantics (Location, Frame, SortedLocationList are not in the reference)
 // are those of oracle/kma_oracle.c orc_propose.
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // (rocprim.hpp uses memset without including it)
+#include <rocprim/rocprim.hpp>
 
 #include "../../include/kmeranno.h"
 #include "kma_internal.h"
@@ -148,15 +149,16 @@ unsigned grid_of(uint64_t n) {
 // The whole sweep on `stream`; a.stats (4 u64) must be zeroed before. Scratch sizes: see
 // kma_abi.cpp (kma_propose_pegs). temp == nullptr: *temp_bytes = the sort / scan scratch.
 hipError_t launch_propose(PropArgs a, void* temp, size_t* temp_bytes, hipStream_t stream) {
-  const int n = (int)a.n;
+  const size_t n = a.n;
+  const rocprim::plus<uint32_t> add;
   if (!temp) {
     size_t s1 = 0, s2 = 0, s3 = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, s1, a.keys, a.skeys, a.idx, a.sidx,
-                                                      n, 0, 32, stream);
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, s1, a.keys, a.skeys, a.idx, a.sidx, n, 0u,
+                                             32u, stream);
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::InclusiveSum(nullptr, s2, a.head, a.list_no, n, stream);
+    e = rocprim::inclusive_scan(nullptr, s2, a.head, a.list_no, n, add, stream);
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(nullptr, s3, a.keep, a.out_pos, n, stream);
+    e = rocprim::exclusive_scan(nullptr, s3, a.keep, a.out_pos, 0u, n, add, stream);
     if (e != hipSuccess) return e;
     *temp_bytes = std::max(s1, std::max(s2, s3));
     return hipSuccess;
@@ -164,17 +166,17 @@ hipError_t launch_propose(PropArgs a, void* temp, size_t* temp_bytes, hipStream_
   const unsigned g = grid_of(a.n);
   hipLaunchKernelGGL(prop_keys_kernel, dim3(g), dim3(256), 0, stream, a);
   size_t tb = *temp_bytes;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, tb, a.keys, a.skeys, a.idx, a.sidx, n,
-                                                    0, 32, stream);
+  hipError_t e = rocprim::radix_sort_pairs(temp, tb, a.keys, a.skeys, a.idx, a.sidx, n, 0u, 32u,
+                                           stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(prop_heads_kernel, dim3(g), dim3(256), 0, stream, a);
   tb = *temp_bytes;
-  e = hipcub::DeviceScan::InclusiveSum(temp, tb, a.head, a.list_no, n, stream);
+  e = rocprim::inclusive_scan(temp, tb, a.head, a.list_no, n, add, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(prop_starts_kernel, dim3(g), dim3(256), 0, stream, a);
   hipLaunchKernelGGL(prop_sweep_kernel, dim3(g), dim3(256), 0, stream, a);
   tb = *temp_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(temp, tb, a.keep, a.out_pos, n, stream);
+  e = rocprim::exclusive_scan(temp, tb, a.keep, a.out_pos, 0u, n, add, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(prop_emit_kernel, dim3(g), dim3(256), 0, stream, a);
   return hipGetLastError();
