@@ -160,19 +160,17 @@ __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
 // m = 0 is the flat layout (a hash of the whole key): the fallback for tables whose keys pile
 // onto few minimizers (low-complexity or adversarial kmer sets).
 //
-// Paired homes (KMA_PAIR_HOME = 1, the default; minimizer layouts): the minimizer hash picks a
-// PAIR of adjacent 64-byte buckets — one 128-byte L2 line — and one bit of a hash of the key
-// picks the bucket in it. A probe still reads 64 bytes, windows sharing a minimizer still share
-// a line, and a minimizer's keys spread over two buckets instead of piling into one: displaced
-// keys at c5 (m = 7) 3.55% -> 2.45%, c2 3.60% -> 2.18%; c5 4.54 -> 4.50 ms and 4.56 -> 4.52 ms
-// on two boxes, c3 / c2 even (profiles/r02q_pair/). 0 = one bucket per minimizer (round 2's
-// first layout).
-#ifndef KMA_PAIR_HOME
-#define KMA_PAIR_HOME 1
-#endif
+// Paired homes (minimizer layouts): the minimizer hash picks a PAIR of adjacent 64-byte buckets
+// — one 128-byte L2 line — and one bit of a hash of the key picks the bucket in it. A probe
+// still reads 64 bytes, windows sharing a minimizer still share a line, and a minimizer's keys
+// spread over two buckets instead of piling into one: displaced keys at c5 (m = 7) 3.55% ->
+// 2.45%, c2 3.60% -> 2.18%; c5 4.54 -> 4.50 ms and 4.56 -> 4.52 ms on two boxes, c3 / c2 even
+// (profiles/r02q_pair/). Round 2's first layout (one bucket per minimizer) was kept as a tuning
+// variant until round 4 and is gone: it measured slower at every load but one
+// (profiles/r03_layout/) and its adversarial sweep never produced a record.
 __host__ __device__ inline uint32_t home_from_hash(uint32_t h, uint64_t key, int m,
                                                    uint32_t n_buckets) {
-  if (KMA_PAIR_HOME && m != 0 && n_buckets >= 2) {
+  if (m != 0 && n_buckets >= 2) {
     const uint32_t pair = (uint32_t)(((uint64_t)h * (n_buckets >> 1)) >> 32);
 #if KMA_HASH_LITE
     return 2u * pair + parity32((uint32_t)key);

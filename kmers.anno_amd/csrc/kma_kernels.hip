@@ -492,9 +492,9 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       const uint32_t p = protein_at<P>(pb, x);
       uint64_t key;
       bool ok;
-      if (Packed) {
+      if (Packed) {  // (key 0: every residue without a code; it would match an empty slot)
         key = packed_key<K>(ww[j]);
-        ok = x < span && window_at<P>(pe, x, p);
+        ok = key != 0 && x < span && window_at<P>(pe, x, p);
       } else {
         ok = pack_window<K>(lut, win_bytes(ww[j]), key) && x < span && window_at<P>(pe, x, p);
       }

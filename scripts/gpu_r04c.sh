@@ -21,3 +21,6 @@ for f in sorted(glob.glob('gpurun_out/r04c/c*_p*_r*.json')):
     e=d.get('e2e_host_call',{})
     print(f.split('/')[-1], round(d['ms_per_step'],4), d['phases_ms'], 'e2e', round(e.get('ms',0),3))
 PY
+# the adversarial layout sweep (2,000 shared minimizers) on the shipped build, once
+timeout -k 10 300 python3 scripts/layout_sweep.py --adversarial --lfs 0.5,0.9 > $OUT/adversarial.jsonl 2> $OUT/adversarial.log
+echo "adversarial rc=$?" >> $OUT/steps.log

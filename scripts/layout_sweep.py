@@ -114,7 +114,7 @@ def main():
                    "displaced_frac": st[3] / max(st[1], 1), "ms": ms,
                    "lookups_per_s": n_win / (ms * 1e-3), "windows": n_win,
                    "launches": args.warmup + args.steps, "outputs_equal_first_case": bool(same),
-                   "pair_home_build": os.environ.get("KMERANNO_LIB", "default")}
+                   "library": os.environ.get("KMERANNO_LIB", "default")}
             print(json.dumps(rec), flush=True)
         # which layout the creators keep (kma_abi.cpp create_from_device_keys)
         msize = kmeranno.layout_for(K, nb)
@@ -128,22 +128,17 @@ def main():
 
 
 def adversarial_workload():
-    """2.4M keys built to share 2,000 minimizers (scripts/robustness.py's set) and 200k
-    proteins assembled from them."""
+    """~1.5M keys built to share 2,000 minimizers and 200k proteins assembled from them: the
+    cores are the 2,000 6-mers of lowest m-mer hash (kma_internal.h mmer_hash, KMA_HASH_LITE:
+    the 32-bit product with 0x9E3779B1) among 2M random ones, so every key built around one has
+    it as its minimizer at m = 6."""
     rng = np.random.default_rng(23)
     aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
-
-    def mix32(h):
-        h = h ^ (h >> np.uint64(16))
-        h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
-        h = h ^ (h >> np.uint64(13))
-        h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
-        return h ^ (h >> np.uint64(16))
     cand = aa[rng.integers(0, 20, (2_000_000, 6))]
     packed = np.zeros(len(cand), np.uint64)
     for j in range(6):
         packed = (packed << np.uint64(5)) | (cand[:, j].astype(np.uint64) - np.uint64(64))
-    h = mix32((packed * np.uint64(0x9E3779B1) + np.uint64(0x7F4A7C15)) & np.uint64(0xFFFFFFFF))
+    h = (packed * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
     cores = packed[np.argsort(h)[:2000]]
     codes = np.arange(1, 21, dtype=np.uint64)[rng.integers(0, 20, (2000, 3, 400, 2))]
     ks = []

@@ -455,7 +455,8 @@ def test_device_api_with_torch_buffers(kma):
 
 
 def test_workspace_timing(kma):
-    """kma_workspace_timing: hipEvent durations of device calls (the protein kernel)."""
+    """kma_workspace_timing: hipEvent durations of device calls (the pack kernel and the
+    protein kernel; the protein kernel alone on ASCII input)."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_workload(500, 20_000, 200, seed=31)
@@ -478,8 +479,14 @@ def test_workspace_timing(kma):
         for _ in range(2):
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
                                          *[o.data_ptr() for o in outs], 0, 0, stream)
+        calls, ph = ws.phases_read()  # the pack kernel, then the probe (KMA_OPT_PACKED_INPUT)
+        assert calls == 2 and list(ph) == ["pack_kernel", "annotate_kernel"]
+        assert ph["annotate_kernel"] > 0 and ph["pack_kernel"] > 0
+        kma.set_option(kma.OPT_PACKED_INPUT, 0)
+        kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
+                                     *[o.data_ptr() for o in outs], 0, 0, stream)
         calls, ph = ws.phases_read()
-        assert calls == 2 and list(ph) == ["annotate_kernel"] and ph["annotate_kernel"] > 0
+        assert calls == 1 and list(ph) == ["annotate_kernel"] and ph["annotate_kernel"] > 0
         with pytest.raises(kma.KmerAnnoError) as e:  # reservation too small
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res + 1, 5,
                                          0, *[o.data_ptr() for o in outs], 0, 0, stream)
