@@ -12,12 +12,14 @@
 // Every kmer probe and vote runs on the GPU through libkmeranno.so; this file only parses
 // arguments, reads files, and formats reports exactly as the Java reporters do.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -130,13 +132,27 @@ double seconds(Clock::time_point t0) {
   return std::chrono::duration<double>(Clock::now() - t0).count();
 }
 
+// One genome of the directory as the apply loop consumes it: the parsed GTO, its pegs
+// (Genome.getPegs order) and, when a parse worker annotated it, the native call's outputs.
+struct ParsedGenome {
+  std::unique_ptr<Genome> genome;
+  std::vector<const Feature*> pegs;
+  std::vector<int32_t> fid, count;
+  std::vector<uint8_t> status;
+  bool annotated = false;
+  double call_s = 0;  // the worker's native call
+};
+
 // GenomeDirectory iteration with the GTOs parsed ahead by a thread pool (load_genome_pegs),
-// at most `lookahead` genomes past the consumer; genomes are taken in file order.
+// at most `lookahead` genomes past the consumer; genomes are taken in file order. `after`
+// (optional) runs on the worker once a genome is parsed (the per-genome native call).
 class GenomeFeed {
  public:
-  GenomeFeed(const std::vector<std::string>& files, int threads, size_t lookahead)
+  using After = std::function<void(ParsedGenome&)>;
+  GenomeFeed(const std::vector<std::string>& files, int threads, size_t lookahead,
+             After after = nullptr)
       : files_(files), slots_(files.size()), errors_(files.size()), ready_(files.size(), 0),
-        lookahead_(std::max<size_t>(lookahead, 1)) {
+        lookahead_(std::max<size_t>(lookahead, 1)), after_(std::move(after)) {
     const int n = (int)std::max<size_t>(1, std::min<size_t>(threads, files.size()));
     for (int i = 0; i < n; ++i) pool_.emplace_back([this] { work(); });
   }
@@ -148,8 +164,8 @@ class GenomeFeed {
     cv_.notify_all();
     for (auto& t : pool_) t.join();
   }
-  std::unique_ptr<Genome> take(size_t i) {
-    std::unique_ptr<Genome> out;
+  ParsedGenome take(size_t i) {
+    ParsedGenome out;
     std::string err;
     {
       std::unique_lock<std::mutex> g(mu_);
@@ -174,17 +190,19 @@ class GenomeFeed {
         if (stop_ || next_ >= files_.size()) return;
         i = next_++;
       }
-      std::unique_ptr<Genome> gen;
+      ParsedGenome pg;
       std::string err;
       try {
-        gen.reset(new Genome(load_genome_pegs(files_[i])));
+        pg.genome.reset(new Genome(load_genome_pegs(files_[i])));
+        pg.pegs = pg.genome->pegs();
+        if (after_) after_(pg);
       } catch (const std::exception& e) {
         err = e.what();
-        if (err.empty()) err = "parse failure";
+        if (err.empty()) err = "failure";
       }
       {
         std::lock_guard<std::mutex> g(mu_);
-        slots_[i] = std::move(gen);
+        slots_[i] = std::move(pg);
         errors_[i] = std::move(err);
         ready_[i] = 1;
       }
@@ -192,42 +210,32 @@ class GenomeFeed {
     }
   }
   const std::vector<std::string>& files_;
-  std::vector<std::unique_ptr<Genome>> slots_;
+  std::vector<ParsedGenome> slots_;
   std::vector<std::string> errors_;
   std::vector<char> ready_;
   size_t lookahead_, next_ = 0, taken_ = 0;
   bool stop_ = false;
+  After after_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<std::thread> pool_;
 };
 
-// Consecutive genomes concatenated for one native call; pegs[first[g] .. first[g + 1]) are
-// genome g's (Genome.getPegs order).
-struct Batch {
-  std::vector<std::unique_ptr<Genome>> genomes;
-  std::vector<const Feature*> pegs;
-  std::vector<uint32_t> first{0};
+// Concatenated proteins of one or more genomes for one native call.
+struct ProteinBatch {
   std::string residues;
   std::vector<uint64_t> offsets{0};
-  std::vector<int32_t> fid, count;
-  std::vector<uint8_t> status;
   void clear() {
-    genomes.clear();
-    pegs.clear();
-    first.assign(1, 0);
     residues.clear();
     offsets.assign(1, 0);
   }
-  void add(std::unique_ptr<Genome> g) {
-    for (const Feature* f : g->pegs()) {
+  void add(const std::vector<const Feature*>& pegs) {
+    for (const Feature* f : pegs) {
       residues += f->protein;
       offsets.push_back(residues.size());
-      pegs.push_back(f);
     }
-    first.push_back((uint32_t)pegs.size());
-    genomes.push_back(std::move(g));
   }
+  uint32_t size() const { return (uint32_t)(offsets.size() - 1); }
 };
 
 // ---- ApplyKmerProcessor -----------------------------------------------------------------------
@@ -313,48 +321,70 @@ class ApplyKmerProcessor {
   }
 
   // :114-155. The reference loops genome by genome: parse a GTO, run every peg's ProteinKmers
-  // through the map, report. Here the same reports come out in the same order, but
+  // through the map, report. Here the same reports come out in the same order, while
   //   - GTOs are parsed ahead by a pool of threads (GenomeFeed: the loader skips contig DNA),
-  //   - consecutive genomes are batched into one native call of >= batch_residues residues
-  //     (a 4k-peg genome is ~1.2M residues: a launch that small leaves most of the GPU idle),
-  //   - the call runs while the pool parses the next genomes.
+  //   - the native calls run off the report thread: by default each parse worker makes its
+  //     genome's call (concurrent host calls on one table: a pooled context and stream each,
+  //     include/kmeranno.h), so parsing, staging and the GPU overlap across genomes;
+  //     --batch R > 0 instead concatenates consecutive genomes into one call of >= R residues
+  //     on the report thread (fewer, larger launches),
+  //   - the report thread only waits for genome i, then writes its report.
   void runCommand() {
     const std::vector<std::string> files = genome_files(inDir_);
     log_info("%zu genomes found in input directory.", files.size());
     const auto t0 = Clock::now();
-    GenomeFeed feed(files, parseThreads_, 4 * batchGenomesHint());
-    Batch b;
-    uint64_t n_prot = 0, n_res = 0, n_calls = 0;
-    double gpu_s = 0;
-    for (size_t i = 0; i < files.size();) {
+    std::atomic<uint64_t> calls{0}, call_us{0};
+    const bool on_workers = batchResidues_ == 0;
+    GenomeFeed::After annotate = [&](ParsedGenome& pg) {
+      thread_local ProteinBatch b;
       b.clear();
-      while (i < files.size() && (b.residues.size() < batchResidues_ || b.genomes.empty())) {
-        b.add(feed.take(i++));
-        if (!b.genomes.empty() && b.residues.size() >= batchResidues_) break;
+      b.add(pg.pegs);
+      call(b, pg, calls, call_us);
+    };
+    GenomeFeed feed(files, parseThreads_, on_workers ? 4 * (size_t)parseThreads_ : 4 * batchGenomesHint(),
+                    on_workers ? annotate : nullptr);
+    std::vector<ParsedGenome> pending;  // batched mode: genomes of the current batch
+    ProteinBatch b;
+    uint64_t n_prot = 0, n_res = 0;
+    double wait_s = 0, report_s = 0;
+    for (size_t i = 0; i < files.size();) {
+      pending.clear();
+      const auto w0 = Clock::now();
+      if (on_workers) {
+        pending.push_back(feed.take(i++));
+      } else {
+        b.clear();
+        while (i < files.size() && (pending.empty() || b.residues.size() < batchResidues_)) {
+          pending.push_back(feed.take(i++));
+          b.add(pending.back().pegs);
+        }
       }
-      const uint32_t n = (uint32_t)b.pegs.size();
-      b.fid.resize(n);
-      b.count.resize(n);
-      b.status.resize(n);
-      const auto c0 = Clock::now();
-      if (n)  // one batched native call replaces the per-feature ProteinKmers + probe loop
-        check(kma_annotate_proteins(table_, reinterpret_cast<const uint8_t*>(b.residues.data()),
-                                    b.offsets.data(), n, minHits_, 0, b.fid.data(),
-                                    b.count.data(), b.status.data(), nullptr, 0),
-              "kma_annotate_proteins");
-      gpu_s += seconds(c0);
-      n_calls += n > 0;
-      n_prot += n;
-      n_res += b.residues.size();
-      for (size_t g = 0; g < b.genomes.size(); ++g) {
-        const Genome& genome = *b.genomes[g];
+      wait_s += seconds(w0);
+      if (!on_workers) {
+        ParsedGenome all;  // the batch's outputs, split back per genome below
+        call(b, all, calls, call_us);
+        size_t at = 0;
+        for (ParsedGenome& pg : pending) {
+          const size_t n = pg.pegs.size();
+          pg.fid.assign(all.fid.begin() + at, all.fid.begin() + at + n);
+          pg.count.assign(all.count.begin() + at, all.count.begin() + at + n);
+          pg.status.assign(all.status.begin() + at, all.status.begin() + at + n);
+          at += n;
+        }
+      }
+      const auto r0 = Clock::now();
+      for (const ParsedGenome& pg : pending) {
+        const Genome& genome = *pg.genome;
         log_info("Processing genome %s (%s).", genome.id.c_str(), genome.name.c_str());
         reporter_->openGenome(genome);
-        for (uint32_t j = b.first[g]; j < b.first[g + 1]; ++j)
-          if (b.status[j] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
-            reporter_->recordFeature(*b.pegs[j], db_.roles[b.fid[j]], b.count[j]);
+        for (size_t j = 0; j < pg.pegs.size(); ++j)
+          if (pg.status[j] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
+            reporter_->recordFeature(*pg.pegs[j], db_.roles[pg.fid[j]], pg.count[j]);
         reporter_->closeGenome();
+        n_prot += pg.pegs.size();
+        for (const Feature* f : pg.pegs) n_res += f->protein.size();
       }
+      report_s += seconds(r0);
     }
     reporter_->closeReport();
     std::fflush(stdout);
@@ -363,10 +393,31 @@ class ApplyKmerProcessor {
     std::fprintf(stderr,
                  "[kma] apply-stats {\"genomes\": %zu, \"proteins\": %llu, \"residues\": %llu, "
                  "\"calls\": %llu, \"loop_s\": %.6f, \"native_call_s\": %.6f, "
+                 "\"report_wait_s\": %.6f, \"report_s\": %.6f, \"calls_on\": \"%s\", "
                  "\"parse_threads\": %d, \"batch_residues\": %llu, \"table_load_s\": %.6f}\n",
                  files.size(), (unsigned long long)n_prot, (unsigned long long)n_res,
-                 (unsigned long long)n_calls, wall, gpu_s, feed.threads(),
+                 (unsigned long long)calls.load(), wall, call_us.load() * 1e-6, wait_s, report_s,
+                 on_workers ? "parse workers" : "report thread", feed.threads(),
                  (unsigned long long)batchResidues_, tableLoadS_);
+  }
+
+  // One native call on the proteins of `b`; outputs into pg (fid, count, status).
+  void call(const ProteinBatch& b, ParsedGenome& pg, std::atomic<uint64_t>& calls,
+            std::atomic<uint64_t>& call_us) const {
+    const uint32_t n = b.size();
+    pg.fid.resize(n);
+    pg.count.resize(n);
+    pg.status.resize(n);
+    if (n == 0) return;
+    const auto c0 = Clock::now();
+    check(kma_annotate_proteins(table_, reinterpret_cast<const uint8_t*>(b.residues.data()),
+                                b.offsets.data(), n, minHits_, 0, pg.fid.data(), pg.count.data(),
+                                pg.status.data(), nullptr, 0),
+          "kma_annotate_proteins");
+    pg.annotated = true;
+    pg.call_s = seconds(c0);
+    calls += 1;
+    call_us += (uint64_t)(pg.call_s * 1e6);
   }
 
   bool help() const { return help_; }
@@ -384,8 +435,8 @@ class ApplyKmerProcessor {
   int minHits_ = 5;
   int device_ = 0;
   bool help_ = false;
-  int parseThreads_ = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  uint64_t batchResidues_ = 16ull << 20;  // residues per native call (several genomes)
+  int parseThreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  uint64_t batchResidues_ = 0;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
   std::unique_ptr<ApplyKmerReporter> reporter_;
@@ -401,8 +452,9 @@ const char* kApplyUsage =
     " -m, --min N       minimum number of hits required to call a role (default 5)\n"
     " --format FMT      reporting format: APPLY (default) or VERIFY\n"
     " --device D        HIP device ordinal (default 0)\n"
-    " --threads N       GTO parser threads (default min(8, cores))\n"
-    " --batch R         residues per native call, whole genomes (default 16777216)\n";
+    " --threads N       GTO parser threads (default min(16, cores))\n"
+    " --batch R         0 (default): each parser thread makes its genome's native call;\n"
+    "                   R > 0: consecutive genomes batched into calls of >= R residues\n";
 
 int run_apply(const std::vector<std::string>& args) {
   ApplyKmerProcessor p;

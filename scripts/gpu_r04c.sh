@@ -24,3 +24,5 @@ PY
 # the adversarial layout sweep (2,000 shared minimizers) on the shipped build, once
 timeout -k 10 300 python3 scripts/layout_sweep.py --adversarial --lfs 0.5,0.9 > $OUT/adversarial.jsonl 2> $OUT/adversarial.log
 echo "adversarial rc=$?" >> $OUT/steps.log
+timeout -k 10 700 python bench.py --workload genomes > $OUT/genomes.json 2> $OUT/genomes.log
+echo "genomes rc=$?" >> $OUT/steps.log

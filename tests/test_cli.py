@@ -88,13 +88,15 @@ def test_kma_apply_reports(kma_bin, oracle_c, small_gto, apply_inputs, min_hits)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads,batch", [(1, 1), (4, 500_000), (8, 1 << 40)])
+@pytest.mark.parametrize("threads,batch", [(6, 0), (1, 1), (4, 500_000), (8, 1 << 40)])
 def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads, batch):
     """`kma apply` over a directory of 14 synthetic GTOs (600 pegs each, a contig of DNA the
-    loader skips): GTOs parsed ahead by a thread pool, consecutive genomes batched into one
-    native call of >= `batch` residues (1: a call per genome, as round 3; 500k: several
-    genomes per call; 2^40: one call for the directory). APPLY and VERIFY reports equal the
-    oracle-derived reports line for line, genomes in file-name order
+    loader skips): GTOs parsed ahead by a thread pool; batch 0 (the default): every parse
+    worker makes its own genome's native call (concurrent host calls on one table); batch > 0:
+    consecutive genomes batched on the report thread into one native call of >= `batch`
+    residues (1: a call per genome, as round 3; 500k: several genomes per call; 2^40: one
+    call for the directory). APPLY and VERIFY reports equal the oracle-derived reports line
+    for line, genomes in file-name order
     (ApplyKmerProcessor.java:116-151, rep/DefaultApplyKmerReporter.java:43-55)."""
     from kmeranno import synth
     sig = synth.make_table(200_000, 400, 5, 8)
@@ -128,8 +130,9 @@ def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads
     assert len(stats) == 1
     st = json.loads(stats[0].split("apply-stats ", 1)[1])
     assert st["genomes"] == 14 and st["proteins"] == 14 * 600
-    if batch == 1:
+    if batch in (0, 1):
         assert st["calls"] == 14
+        assert st["calls_on"] == ("parse workers" if batch == 0 else "report thread")
     elif batch == 1 << 40:
         assert st["calls"] == 1
     else:
