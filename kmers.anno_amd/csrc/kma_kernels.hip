@@ -201,6 +201,7 @@ struct ProteinSmem {
   uint32_t pset[P];      // set base in `pool`, or kGlobalSet
   uint32_t pcap[P];      // set capacity (0: no set)
   uint32_t pmin[P], pmax[P], pcnt[P];  // smallest / largest fid hit; distinct keys (or hits)
+  uint32_t plist[P];                   // kGlobalSet proteins: hits appended to their list
   uint32_t skip;                       // two-pass grid: the group belongs to the other pass
   uint8_t lut[256];
 };
@@ -229,7 +230,12 @@ __device__ __forceinline__ bool global_set_insert(uint32_t* set, uint32_t cap, u
   }
 }
 
-// A hit of protein p (of the block) on the key with slot id `sid` and function `fid`.
+// A hit of protein p (of the block) on the key with slot id `sid` and function `fid`. A protein
+// whose set is in LDS inserts the slot id there (a fresh key counts); a protein whose set did not
+// fit (kGlobalSet) appends it to its list in workspace memory (its own residues' region: 2 u32
+// per residue), deduplicated after the probe steps (dedupe_lists). Round 3 kept a hash set
+// there, zeroed by the block and filled by agent-scope CAS: at c5 0.23 GB of writes per launch
+// for 9 MB of outputs, the set lines being evicted from L2 between hits under the gather load.
 template <int P>
 __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs& a,
                                            uint64_t span_lo, bool multiset, uint32_t p,
@@ -243,12 +249,50 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs
 #else
   if (!multiset) {
 #endif
-    const uint32_t base = sm.pset[p], cap = sm.pcap[p];
-    fresh = base != kGlobalSet
-                ? lds_set_insert(sm.pool + base, cap, sid + 1u)
-                : global_set_insert(a.gset + 2 * (span_lo + sm.pbeg[p]), cap, sid + 1u);
+    const uint32_t base = sm.pset[p];
+    if (base != kGlobalSet) {
+      fresh = lds_set_insert(sm.pool + base, sm.pcap[p], sid + 1u);
+    } else {
+      a.gset[2 * (span_lo + sm.pbeg[p]) + atomicAdd(&sm.plist[p], 1u)] = sid + 1u;
+      fresh = false;
+    }
   }
   if (fresh) atomicAdd(&sm.pcnt[p], 1u);
+}
+
+// After the probe steps (the LDS sets are final, the pool is free): the distinct slot ids of
+// every kGlobalSet protein's list, counted into pcnt. A list of fewer than kSetPool hits is
+// deduplicated in the pool (the usual case: it needs 2,730+ windows to have that many); a
+// longer one (giant proteins) in a hash set of L entries in the second half of its region,
+// zeroed here (agent-scope stores, the CAS inserts are agent-scope). Block-uniform loop.
+template <int P>
+__device__ __forceinline__ void dedupe_lists(ProteinSmem<P>& sm, const ProteinArgs& a,
+                                             uint64_t span_lo, const uint32_t (&pb)[P + 1]) {
+  const int t = threadIdx.x;
+  for (int p = 0; p < P; ++p) {
+    if (sm.pset[p] != kGlobalSet) continue;
+    const uint32_t h = sm.plist[p];
+    if (h == 0) continue;
+    const uint32_t* list = a.gset + 2 * (span_lo + pb[p]);
+    uint32_t fresh = 0;
+    if (h < (uint32_t)kSetPool) {
+      uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
+      for (uint32_t i = t; i < (uint32_t)kSetPool / 4; i += 256) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+      __syncthreads();
+      for (uint32_t i = t; i < h; i += 256) fresh += lds_set_insert(sm.pool, kSetPool, list[i]);
+    } else {
+      const uint32_t L = pb[p + 1] - pb[p];  // > windows >= h: the set never fills
+      uint32_t* set = a.gset + 2 * (span_lo + pb[p]) + L;
+      for (uint32_t i = t; i < L; i += 256)
+        __hip_atomic_store(set + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      __syncthreads();
+      for (uint32_t i = t; i < h; i += 256) fresh += global_set_insert(set, L, list[i]);
+    }
+    fresh = wave_sum(fresh);
+    if ((t & 63) == 0 && fresh) atomicAdd(&sm.pcnt[p], fresh);
+    __syncthreads();  // the pool (or the set) is free for the next list
+  }
 }
 
 // Which of the block's proteins holds span position x (pb: the block-uniform starts, in
@@ -392,6 +436,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       sm.pmin[lane] = 0xFFFFFFFFu;
       sm.pmax[lane] = 0u;
       sm.pcnt[lane] = 0u;
+      sm.plist[lane] = 0u;
     }
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {  // LDS pool for the sets; workspace memory for those that do not fit
@@ -414,8 +459,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
           done |= 1u << best;
           const uint32_t cap = sm.pcap[best];
           const bool fits = top + cap <= (uint32_t)kSetPool;
-          sm.pset[best] = fits ? top : kGlobalSet;
-          if (!fits) sm.pcap[best] = 2u * sm.pwin[best];  // <= 2 entries per residue
+          sm.pset[best] = fits ? top : kGlobalSet;  // (a list: appended, never zeroed)
           top += fits ? cap : 0u;
         }
       }
@@ -435,12 +479,6 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
   KMA_CLK(1);
   for (uint32_t i = t; i < used / 4; i += 256) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int p = 0; p < P; ++p) {  // block-uniform: sets in workspace memory (long proteins)
-    if (sm.pset[p] != kGlobalSet || sm.pcap[p] == 0) continue;
-    uint32_t* gs = a.gset + 2 * (span_lo + pb[p]);
-    for (uint32_t i = t; i < sm.pcap[p]; i += 256)
-      __hip_atomic_store(gs + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   __syncthreads();
 
   const uint64_t* __restrict__ slots = a.slots;
@@ -602,7 +640,8 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   KMA_CLK_SET(7, (span + stride - 1) / stride);
   if (cn) chain_flush();
   KMA_CLK(4);
-  __syncthreads();  // every record is final
+  __syncthreads();  // every LDS set is final; the lists are complete
+  if (!multiset) dedupe_lists<P>(sm, a, span_lo, pb);
   if (t < (int)np) {
     const uint32_t mn = sm.pmin[t], mx = sm.pmax[t], cnt = sm.pcnt[t];
     int32_t fid_out = -1, cnt_out = 0;
