@@ -265,15 +265,17 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs
 // deduplicated in the pool (the usual case: it needs 2,730+ windows to have that many); a
 // longer one (giant proteins) in a hash set of L entries in the second half of its region,
 // zeroed here (agent-scope stores, the CAS inserts are agent-scope). Block-uniform loop.
+// (Protein bounds from LDS: indexing the kernel's register copy pb[] by the loop counter makes
+// the compiler spill it to scratch.)
 template <int P>
 __device__ __forceinline__ void dedupe_lists(ProteinSmem<P>& sm, const ProteinArgs& a,
-                                             uint64_t span_lo, const uint32_t (&pb)[P + 1]) {
+                                             uint64_t span_lo) {
   const int t = threadIdx.x;
   for (int p = 0; p < P; ++p) {
     if (sm.pset[p] != kGlobalSet) continue;
-    const uint32_t h = sm.plist[p];
+    const uint32_t h = sm.plist[p], b0 = sm.pbeg[p];
     if (h == 0) continue;
-    const uint32_t* list = a.gset + 2 * (span_lo + pb[p]);
+    const uint32_t* list = a.gset + 2 * (span_lo + b0);
     uint32_t fresh = 0;
     if (h < (uint32_t)kSetPool) {
       uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
@@ -281,8 +283,8 @@ __device__ __forceinline__ void dedupe_lists(ProteinSmem<P>& sm, const ProteinAr
       __syncthreads();
       for (uint32_t i = t; i < h; i += 256) fresh += lds_set_insert(sm.pool, kSetPool, list[i]);
     } else {
-      const uint32_t L = pb[p + 1] - pb[p];  // > windows >= h: the set never fills
-      uint32_t* set = a.gset + 2 * (span_lo + pb[p]) + L;
+      const uint32_t L = sm.pbeg[p + 1] - b0;  // > windows >= h: the set never fills
+      uint32_t* set = a.gset + 2 * (span_lo + b0) + L;
       for (uint32_t i = t; i < L; i += 256)
         __hip_atomic_store(set + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence();
@@ -641,7 +643,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   if (cn) chain_flush();
   KMA_CLK(4);
   __syncthreads();  // every LDS set is final; the lists are complete
-  if (!multiset) dedupe_lists<P>(sm, a, span_lo, pb);
+  if (!multiset) dedupe_lists<P>(sm, a, span_lo);
   if (t < (int)np) {
     const uint32_t mn = sm.pmin[t], mx = sm.pmax[t], cnt = sm.pcnt[t];
     int32_t fid_out = -1, cnt_out = 0;
@@ -662,8 +664,13 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   }
 }
 
+// Occupancy: kProteinOcc waves per SIMD (its LDS and VGPR budget); the flat layout's packed
+// variant (a fallback for crowded tables: two full-key mixes per window) needs 6 to stay clear
+// of scratch.
+template <int K, int M, bool Packed>
+constexpr int protein_occ() { return M == 0 && Packed ? 6 : kProteinOcc; }
 template <int K, int M, int P, bool Packed>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kProteinOcc, 8))) void annotate_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(protein_occ<K, M, Packed>(), 8))) void annotate_kernel(
     ProteinArgs a) {
   __shared__ ProteinSmem<P> sm;
   KMA_CLK(0);
