@@ -16,12 +16,13 @@ Workloads (BASELINE.json configs; the default is c5, the north-star configuratio
   c3  6-frame pass (KmerReference.java:157-203) over a rank's 5 Mbp synthetic genome.
 
 Beside the timed steps, rank 0 of a 1-GPU run also reports
-  roofline      the dominant kernel's HBM bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE
-                passes of this build, committed under profiles/, calibrated per the guide) over
-                its hipEvent-timed duration against 8 TB/s (`achieved`, `frac`); beside it the
-                SURVEY §8(d) algorithmic equivalent (64 B per probed window + 1 B per residue,
-                `alg_equiv_GBps`) and the fabric line-request rate against the random-64-B
-                ceiling measured live on a buffer of the table's size (kma_gather_bench);
+  roofline      the dominant kernel's SURVEY §8(d) algorithmic bytes per launch (64 B per
+                probed window + its input) over its hipEvent-timed duration against 8 TB/s
+                (`achieved`, `frac`); beside it the HBM bytes it really moves (`traffic`,
+                `pmc_frac`: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of these kernel sources,
+                committed under profiles/, calibrated per the guide) and the fabric line-request
+                rate against the random-64-B ceiling measured live on a buffer of the table's
+                size (kma_gather_bench);
   e2e           the host entry point kma_annotate_proteins on the same batch from host memory
                 (H2D + kernel + D2H through pinned staging): the PCIe-inclusive rate;
   cpu_baseline  the C restatement of the reference loop (oracle/kma_oracle.c) on all the box's
@@ -60,7 +61,7 @@ MALL_BYTES = 256 << 20  # Infinity Cache: a table below it is served on-die (MI3
 GATHER_BIN = os.path.join(ROOT, "kmers.anno_amd", "build", "kma_gather_bench")
 # Per-launch PMC traffic of the dominant kernels of this build (scripts/gpu_traffic.sh +
 # scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_traffic.json")
 METRIC = "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs roofline"
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
@@ -198,124 +199,46 @@ def gather_ceiling(table_bytes: int):
 
 
 def pmc_traffic(workload: str, kernel: str):
-    """(traffic bytes per launch, fabric line requests per launch, source) from the committed
-    PMC summary, or (None, None, None)."""
+    """(traffic bytes per launch, fabric line requests per launch, source, stale) from the
+    committed PMC summary, or Nones. stale: the summary was measured on other kernel sources
+    than this tree's (its source_sha16 differs): its numbers are then not reported."""
     try:
-        d = json.load(open(TRAFFIC_FILE))["workloads"][workload][kernel]
-        return d["traffic_bytes"], d.get("read_requests"), os.path.relpath(TRAFFIC_FILE, ROOT)
+        d = json.load(open(TRAFFIC_FILE))
+        rec = d["workloads"][workload][kernel]
     except (OSError, KeyError, ValueError):
-        return None, None, None
-
-
-def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
-    """Signature table built on rank 0's GPU with the library creators' layout rule
-    (kmeranno.choose_layout), replicated over RCCL (xGMI) to the other ranks."""
-    nb = kmeranno.buckets_for(t_size, load_factor)
-    slots = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int64, device=dev)
-    layout = torch.zeros(1, dtype=torch.int32, device=dev)
-    if rank == 0:
-        winner = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int32, device=dev)
-        status = torch.zeros(4, dtype=torch.int32, device=dev)
-        keys = torch.from_numpy(keys_np.view(np.int64)).to(dev)
-        fids = torch.from_numpy(fids_np.view(np.int32)).to(dev)
-
-        times = {}
-
-        def build(m):
-            tb, te = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            tb.record()
-            kmeranno.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
-                                  fids.data_ptr(), len(keys_np), status.data_ptr(), sp, k=K,
-                                  layout=m)
-            te.record()
-            torch.cuda.synchronize()
-            st = status.cpu().numpy().astype(np.int64)
-            assert st[0] == 0, "table full"
-            times[m] = tb.elapsed_time(te)
-            return st
-
-        # the library creators' rule (size rule, then m = 7 / flat rebuilds by measurement)
-        m, st = kmeranno.choose_layout(K, nb, build)
-        ms = times[m]
-        layout.fill_(m)
-        log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 8 * kmeranno.bucket_slots() / 2**20:.0f} MiB), "
-            f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
-            f"built in {ms:.1f} ms")
-        del winner, keys, fids
-    if world > 1:
-        kdist.broadcast_table(slots, src=0)  # RCCL over xGMI (host-staged under gloo)
-        kdist.broadcast(layout, src=0)
-        torch.cuda.synchronize()
-    m = int(layout.item())
-    return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m), slots
-
-
-def timed(step, ws, args, world, stream, dev, before=None, after=None):
-    """W warmup steps, then exactly K steps between barrier + synchronize; then the same K steps
-    again with the library's hipEvents around its kernels. Max over ranks of (wall s, GPU ms,
-    main-kernel ms per call, rest ms per call)."""
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if before is not None:
-        before()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    if after is not None:
-        after()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    ws.timing(True)
-    for _ in range(args.steps):
-        step()
-    n_t, phases = ws.phases_read()
-    ws.timing(False)
-    names = list(phases)
-    stats = torch.tensor([elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names],
-                         dtype=torch.float64, device=dev)
-    if world > 1:
-        kdist.all_reduce_max(stats)
-    v = stats.tolist()
-    return v[0], v[1], dict(zip(names, v[2:]))
+        return None, None, None, False
+    src = os.path.relpath(TRAFFIC_FILE, ROOT)
+    if d.get("source_sha16") != kmeranno.source_digest():
+        return None, None, src, True
+    return rec["traffic_bytes"], rec.get("read_requests"), src, False
 
 
 def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
-    """The dominant kernel's line. achieved = the HBM bytes it moves per launch (PMC counters
-    of this build, committed in profiles/) / its hipEvent-timed mean duration, against the
-    8 TB/s spec; when no counter summary names the kernel, the algorithmic bytes stand in (and
-    achieved_basis says so). The SURVEY §8(d) algorithmic figure (one 64-B line per probed
-    window + the input) is kept as alg_equiv_GBps: minimizer buckets let consecutive windows
-    share a line, so it exceeds the bytes actually moved and its ratio to the random-line
-    ceiling can pass 1. The request-rate view: fabric line requests per launch (PMC) per
-    second against the live random-64-B ceiling."""
+    """The dominant kernel's line, by the SURVEY §8(d) rule: achieved = its algorithmic bytes
+    per launch (one 64-B bucket line per probed window + the input it streams) / its
+    hipEvent-timed mean duration, against the 8 TB/s HBM peak (frac). Minimizer buckets let
+    consecutive windows share a line, so the algorithmic figure exceeds the bytes moved.
+    traffic = the HBM bytes the kernel really moves per launch (rocprofv3 FETCH_SIZE +
+    WRITE_SIZE passes of these kernel sources, committed under profiles/), with pmc_frac =
+    traffic / time / peak beside it; the request view: fabric line requests per launch (PMC)
+    per second against the random-64-B ceiling measured live on a buffer of the table's size."""
     name = kernel.split(" (")[0]
-    traffic, reqs, src = pmc_traffic(workload, name)
-    alg_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    if traffic:
-        achieved, basis = traffic / (kernel_ms * 1e-3) / 1e9, (
-            f"PMC bytes per launch ({src}) / hipEvent kernel time")
-    else:
-        achieved, basis = alg_gbps, "algorithmic bytes (no PMC summary for this kernel)"
+    traffic, reqs, src, stale = pmc_traffic(workload, name)
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     ceil = gather_ceiling(table_bytes) if live else None
     out = {"bound": "hbm" if table_bytes > MALL_BYTES else "infinity-cache",
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "achieved_basis": basis,
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+           "achieved_basis": f"algorithmic bytes per launch ({kind}) / hipEvent kernel time",
            "traffic_source": (f"{src}: rocprofv3 FETCH_SIZE + WRITE_SIZE passes of this kernel "
                               "(MI355X_MICROARCH.md HBM section; Infinity-Cache hits included)")
-           if src else None,
-           "kernel": kernel, "kernel_ms": kernel_ms,
-           "alg_equiv_GBps": alg_gbps, "alg_bytes_per_launch": alg_bytes,
-           "alg_bytes_rule": kind, "windows_per_launch": windows, "table_bytes": table_bytes}
+           if src and not stale else (f"{src} describes other kernel sources: not used"
+                                      if stale else None),
+           "kernel": kernel, "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
+           "windows_per_launch": windows, "table_bytes": table_bytes}
+    if traffic:
+        out["pmc_GBps"] = traffic / (kernel_ms * 1e-3) / 1e9
+        out["pmc_frac"] = out["pmc_GBps"] / HBM_PEAK_GBS
     if reqs:
         out["line_requests_per_launch"] = reqs
         out["line_requests_per_window"] = reqs / windows
@@ -332,11 +255,15 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
 
 
 def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
-    """Roofline of the protein path (one kernel; rank 0's shard, times max over ranks)."""
-    return roofline("windows x 64 B + residues", workload,
-                    f"annotate_kernel<{K}, {m}, 8> (probe + sets + vote)",
-                    ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP + n_res, table_bytes, n_win,
-                    live=live)
+    """Roofline of the protein path's probe kernel (rank 0's shard, times max over ranks)."""
+    packed = kmeranno.get_option(kmeranno.OPT_PACKED_INPUT) == 1
+    return roofline("windows x 64 B + residues (" + ("packed: 0.625 B" if packed else "1 B") +
+                    " each)", workload,
+                    f"annotate_kernel<{K}, {m}, 8, {'true' if packed else 'false'}> "
+                    "(probe + sets + vote)",
+                    ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP +
+                    (n_res * 5 + 7) // 8 if packed else n_win * BYTES_PER_LOOKUP + n_res,
+                    table_bytes, n_win, live=live)
 
 
 def bench_contigs(args, rank, world, dev, stream, sp):
@@ -385,9 +312,9 @@ def bench_contigs(args, rank, world, dev, stream, sp):
             "gpu_ms_per_step": gpu_ms / args.steps,
             "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
             # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 8 B per staged hit
-            "roofline": roofline("probed windows x 64 B + bases + hits x 8 B", "c3",
+            "roofline": roofline("probed windows x 64 B + bases + hits x 16 B", "c3",
                                  f"{kname} (6-frame translate + 2 probes per base)", k_ms,
-                                 n_probe * BYTES_PER_LOOKUP + n_bases + 8 * n_hits,
+                                 n_probe * BYTES_PER_LOOKUP + n_bases + 16 * n_hits,
                                  table.info.bytes, n_probe),
         }
         if world == 1 and not args.no_cpu_baseline:

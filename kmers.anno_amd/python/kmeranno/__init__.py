@@ -193,6 +193,21 @@ def options(**kw):
             set_option(o, v)
 
 
+def source_digest() -> str:
+    """sha256[:16] of the native sources (csrc/ and the ABI header): stamps counter summaries
+    under profiles/ so that a bench run can tell whether they describe the kernels it runs."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG_ROOT, "csrc")
+    hdr = os.path.join(os.path.dirname(PKG_ROOT), "include", "kmeranno.h")
+    for f in sorted(os.listdir(csrc)) + [hdr]:
+        path = f if os.path.isabs(f) else os.path.join(csrc, f)
+        if os.path.isfile(path):
+            h.update(os.path.basename(path).encode())
+            h.update(open(path, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def device_count() -> int:
     n = C.c_int(0)
     _check(load().kma_device_count(C.byref(n)))

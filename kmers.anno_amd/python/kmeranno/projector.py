@@ -287,14 +287,17 @@ class PegProposalList:
 
 
 def annotate_proposals(proposals, functions: list[str], contigs: list[str], genome_id: str,
-                       min_strength: float = 0.5, min_evidence: int = 10, gcode: int = 11,
-                       contig_ids: list[str] | None = None):
+                       contig_ids: list[str], min_strength: float = 0.5, min_evidence: int = 10,
+                       gcode: int = 11):
     """KmerProcessor.annotateGenome's tail (:250-284): the sweep's proposals (PROPOSAL_DTYPE, in
     list order; peg index -> functions[peg]) through PegProposalList with the DNA strength
     min_strength / 3 (:170), then makeFeature (:295-312): [(fid, function, Location, evidence,
-    strength)] in the list's order. contig_ids: the contigs' ids (compareTo orders by them;
-    default: zero-padded indices, i.e. index order)."""
-    ids = contig_ids or [f"{i:010d}" for i in range(len(contigs))]
+    strength)] in the list's order. contig_ids: the genome's contig ids, in contig-index order
+    (required: PegProposal.compareTo orders by Location.getContigId, so the TreeSet's order and
+    the fig|...peg.N numbering depend on them)."""
+    ids = list(contig_ids)
+    if len(ids) != len(contigs):
+        raise ValueError(f"{len(ids)} contig ids for {len(contigs)} contigs")
     plist = PegProposalList(contigs, min_strength / 3, min_evidence, gcode)
     for p in proposals:
         c = int(p["contig"])

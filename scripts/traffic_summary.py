@@ -10,8 +10,13 @@ import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "kmers.anno_amd", "python"))
+import kmeranno  # noqa: E402  (source_digest only: no library load)
 
 
 def load(d):
@@ -20,7 +25,8 @@ def load(d):
         return {}
     per = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in csv.DictReader(open(files[0])):
-        m = re.search(r"(annotate_kernel<[^>]*>|contigs_\w+_kernel(?:<[^>]*>)?|gather_\w+)",
+        m = re.search(r"(annotate_kernel<[^>]*>|contigs_\w+_kernel(?:<[^>]*>)?|pack_residues_kernel|"
+                      r"gather_\w+)",
                       r["Kernel_Name"])
         if not m:
             continue
@@ -32,7 +38,8 @@ root, lines = sys.argv[1], float(sys.argv[2])
 g = load(f"{root}/pmc_gather_FETCH_SIZE")
 gk = next(iter(g))
 corr = lines * 64 / (g[gk]["FETCH_SIZE"] * 1024)
-out = {"calibration": {"kernel": gk, "lines_per_launch": lines,
+out = {"source_sha16": kmeranno.source_digest(),
+       "calibration": {"kernel": gk, "lines_per_launch": lines,
                        "fetch_bytes": g[gk]["FETCH_SIZE"] * 1024, "factor": corr},
        "workloads": {}}
 for wl in ("c2", "c3", "c4", "c5"):

@@ -40,7 +40,8 @@ def test_projection_of_small_gto_onto_itself(oracle_c, small_gto):
     for key in ("peg", "contig", "left", "right", "evidence", "strand", "frame"):
         arr[key] = prop[key]
     funcs = [f.get("function", "") for f in pegs]
-    feats, plist = projector.annotate_proposals(arr, funcs, contigs, small_gto["id"])
+    feats, plist = projector.annotate_proposals(arr, funcs, contigs, small_gto["id"],
+                                                [c["id"] for c in small_gto["contigs"]])
     assert plist.made == len(arr) and len(feats) == len(plist) > 0.6 * len(pegs)
     assert plist.rejected + plist.weak + plist.small + len(plist) + plist.merged <= plist.made + len(plist)
     comp = str.maketrans("ACGTacgt", "TGCAtgca")
@@ -147,8 +148,8 @@ def test_proposal_list_is_the_java_treeset():
     for i, (c, s, lft, rgt, ev) in enumerate(props):
         arr[i] = (i % 4, c, lft, rgt, ev, ord(s), 0, 0)
     funcs = [f"F{i}" for i in range(4)]
-    feats, plist = projector.annotate_proposals(arr, funcs, [contig], "g", min_evidence=10,
-                                                contig_ids=ids)
+    feats, plist = projector.annotate_proposals(arr, funcs, [contig], "g", ids,
+                                                min_evidence=10)
     exp, oplist = _oracle_features(arr, funcs, [contig], ids)
     got = [(f[1], ids[f[2].contig], f[2].strand, f[2].left, f[2].right, f[3]) for f in feats]
     assert got == exp and len(got) > 2
@@ -190,3 +191,34 @@ def test_projection_of_small_gto_vs_oracle_list(oracle_c, small_gto):
     assert len(got) > 400 and got == exp
     assert (plist.made, plist.rejected, plist.merged) == (oplist.made, oplist.rejected,
                                                           oplist.merged)
+
+
+def test_proposal_order_follows_contig_ids_not_indices():
+    """PegProposal.compareTo orders by Location.getContigId: the same proposals on two contigs
+    whose ids sort against their index order ("zeta" is contig 0, "alpha" contig 1) come out
+    with contig 1's first, numbered fig|g.peg.1.., exactly as the oracle's literal TreeSet
+    orders them; swapping the ids swaps the order."""
+    rng = np.random.default_rng(5)
+    orf = "ATG" + "".join(rng.choice(["GCT", "AAA", "CTG", "GAT"], 60)) + "TAA"
+    contig = "CCC" + orf + "CCCGGG" + orf + "CC"
+    props = []
+    for c in (0, 1):
+        for start in (4, 4 + len(orf) + 6):  # 1-based ORF starts (in frame)
+            for shift in (0, 30, 60):
+                props.append((c, "+", start + shift, start + shift + 23, 50 + 3 * c + shift % 7))
+    arr = np.zeros(len(props), [("peg", "<u4"), ("contig", "<u4"), ("left", "<i4"),
+                                ("right", "<i4"), ("evidence", "<u4"), ("strand", "u1"),
+                                ("frame", "u1"), ("pad", "<u2")])
+    for i, (c, st, lft, rgt, ev) in enumerate(props):
+        arr[i] = (i % 3, c, lft, rgt, ev, ord(st), 0, 0)
+    funcs = ["F0", "F1", "F2"]
+    orders = []
+    for ids in (["zeta", "alpha"], ["alpha", "zeta"]):
+        feats, _ = projector.annotate_proposals(arr, funcs, [contig, contig], "g", ids,
+                                                min_evidence=10)
+        exp, _ = _oracle_features(arr, funcs, [contig, contig], ids)
+        got = [(f[1], ids[f[2].contig], f[2].strand, f[2].left, f[2].right, f[3]) for f in feats]
+        assert got == exp and len(got) >= 4
+        orders.append([ids[f[2].contig] for f in feats])
+        assert orders[-1] == sorted(orders[-1])  # contig-id order, whatever the index
+    assert orders[0][0] == "alpha" and [f[2].contig for f in feats][0] == 0
