@@ -141,10 +141,10 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 // served by the CU's L1/L2 instead of HBM. Overflow chains (~1% of probes) are deferred to a
 // per-wave LDS queue and walked 64 at a time.
 //
-// A hit updates its protein's record in LDS: smallest / largest fid (non-returning atomics)
-// and the set of distinct keys hit (ProteinKmers is a set: a kmer occurring twice counts
+// A hit updates its protein's record in LDS: the first fid hit and a flag for a second one
+// (record_fid) and the set of distinct keys hit (ProteinKmers is a set: a kmer occurring twice counts
 // once; a key's slot id is its identity in the table). After one barrier the vote is read off
-// the record, order-free: no hit -> NONE (roleId == null); smallest != largest -> AMBIGUOUS
+// the record, order-free: no hit -> NONE (roleId == null); two distinct fids -> AMBIGUOUS
 // (badPeg); else the role with count = |set|, CALLED iff count >= minHits (:146). The Java
 // loop's early break at the second role changes nothing it reports.
 //
@@ -200,7 +200,9 @@ struct ProteinSmem {
   uint32_t pwin[P];      // windows of the protein (ProteinKmers: L - K + 1, or L - K)
   uint32_t pset[P];      // set base in `pool`, or kGlobalSet
   uint32_t pcap[P];      // set capacity (0: no set)
-  uint32_t pmin[P], pmax[P], pcnt[P];  // smallest / largest fid hit; distinct keys (or hits)
+  uint32_t pfid[P];   // the first fid hit (kNoFid: none yet)
+  uint32_t pbad[P];   // a second, different fid was hit (badPeg)
+  uint32_t pcnt[P];   // distinct keys hit (multiset: hits)
   uint32_t plist[P];                   // kGlobalSet proteins: hits appended to their list
   uint32_t skip;                       // two-pass grid: the group belongs to the other pass
   uint8_t lut[256];
@@ -236,12 +238,25 @@ __device__ __forceinline__ bool global_set_insert(uint32_t* set, uint32_t cap, u
 // per residue), deduplicated after the probe steps (dedupe_lists). Round 3 kept a hash set
 // there, zeroed by the block and filled by agent-scope CAS: at c5 0.23 GB of writes per launch
 // for 9 MB of outputs, the set lines being evicted from L2 between hits under the gather load.
+// The vote record: the first fid lands by CAS; a hit whose fid differs from the recorded one
+// marks the protein bad. A hit reads the record first (a broadcast read when the wave's hits
+// share a protein) and writes only on its first fid or a conflict: round 3's atomicMin /
+// atomicMax per hit serialized on the protein's address (c5: 215M LDS bank-conflict cycles
+// against 151M LDS instruction cycles, profiles/r03_end/sq_summary.json). Bad iff two distinct
+// fids were hit; the fid is then irrelevant (AMBIGUOUS reports -1).
+constexpr uint32_t kNoFid = 0xFFFFFFFFu;
 template <int P>
-__device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs& a,
+__device__ __forceinline__ void record_fid(ProteinSmem<P>& sm, uint32_t p, uint32_t fid) {
+  const uint32_t cur = sm.pfid[p];
+  if (cur == fid) return;
+  const uint32_t old = cur == kNoFid ? atomicCAS(&sm.pfid[p], kNoFid, fid) : cur;
+  if (old != kNoFid && old != fid) sm.pbad[p] = 1u;
+}
+// The hit's set insert (returns whether it counts: a fresh key, or every hit in multiset mode).
+template <int P>
+__device__ __forceinline__ bool record_set(ProteinSmem<P>& sm, const ProteinArgs& a,
                                            uint64_t span_lo, bool multiset, uint32_t p,
-                                           uint32_t fid, uint32_t sid) {
-  atomicMin(&sm.pmin[p], fid);
-  atomicMax(&sm.pmax[p], fid);
+                                           uint32_t sid) {
   bool fresh = true;  // multiset: every hit counts
 #ifdef KMA_TUNE_NO_SET  // tuning builds only (cost bound of the distinct-key sets; wrong counts)
   fresh = false;
@@ -257,7 +272,29 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs
       fresh = false;
     }
   }
-  if (fresh) atomicAdd(&sm.pcnt[p], 1u);
+  return fresh;
+}
+// Counts of a wave's fresh hits (wave-uniform call): one add per wave when they share a protein
+// (the usual case: a step's windows span one or two proteins), per lane otherwise.
+template <int P>
+__device__ __forceinline__ void count_fresh(ProteinSmem<P>& sm, bool fresh, uint32_t p) {
+  const uint64_t fm = __ballot(fresh);
+  if (!fm) return;
+  const int first = __builtin_ctzll(fm);
+  const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)p, first);
+  if (__ballot(fresh && p == p0) == fm) {
+    if ((int)(threadIdx.x & 63) == first) atomicAdd(&sm.pcnt[p0], (uint32_t)__popcll(fm));
+  } else if (fresh) {
+    atomicAdd(&sm.pcnt[p], 1u);
+  }
+}
+// One lane's hit (the deferred chain walks; the probe steps use the parts above directly).
+template <int P>
+__device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs& a,
+                                           uint64_t span_lo, bool multiset, uint32_t p,
+                                           uint32_t fid, uint32_t sid) {
+  record_fid<P>(sm, p, fid);
+  if (record_set<P>(sm, a, span_lo, multiset, p, sid)) atomicAdd(&sm.pcnt[p], 1u);
 }
 
 // After the probe steps (the LDS sets are final, the pool is free): the distinct slot ids of
@@ -435,8 +472,8 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       }
       sm.pwin[lane] = nw;
       sm.pcap[lane] = (nw == 0 || multiset) ? 0u : ((nw + (nw >> 1) + 4u) & ~3u);
-      sm.pmin[lane] = 0xFFFFFFFFu;
-      sm.pmax[lane] = 0u;
+      sm.pfid[lane] = kNoFid;
+      sm.pbad[lane] = 0u;
       sm.pcnt[lane] = 0u;
       sm.plist[lane] = 0u;
     }
@@ -604,9 +641,15 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       KMA_COUNT(2, __popcll(__ballot(probed)));
       KMA_COUNT(3, __popcll(__ballot((w & kWordHit) != 0u)));
 #endif
-      if (w & kWordHit)
-        record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, w & kFidMask,
-                      (c.bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
+      const uint32_t hp = c.bk[j] >> kBucketBits;
+      bool fresh = false;
+      if (w & kWordHit) {
+        record_fid<P>(sm, hp, w & kFidMask);
+        fresh = record_set<P>(sm, a, span_lo, multiset, hp,
+                              (c.bk[j] & kBucketIdx) * kSlotsPerBucket +
+                                  ((w >> kSlotShift) & kSlotMask));
+      }
+      count_fresh<P>(sm, fresh, hp);
       // rare: the home bucket missed and the key's filter positions are set -> deferred walk
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
       const bool pend = false;
@@ -645,12 +688,12 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   __syncthreads();  // every LDS set is final; the lists are complete
   if (!multiset) dedupe_lists<P>(sm, a, span_lo);
   if (t < (int)np) {
-    const uint32_t mn = sm.pmin[t], mx = sm.pmax[t], cnt = sm.pcnt[t];
+    const uint32_t mn = sm.pfid[t], cnt = sm.pcnt[t];
     int32_t fid_out = -1, cnt_out = 0;
     uint8_t st;
-    if (mn == 0xFFFFFFFFu) {
+    if (mn == kNoFid) {
       st = KMA_STATUS_NONE;  // roleId == null
-    } else if (mn != mx) {
+    } else if (sm.pbad[t]) {
       st = KMA_STATUS_AMBIGUOUS;  // badPeg
     } else {
       fid_out = (int32_t)mn;
