@@ -1,28 +1,24 @@
 #!/bin/bash
-# Round 4: packed residue input. Full GPU tests, then an interleaved A/B of the protein step
-# with the pack kernel + packed probe (1) against the ASCII probe (0) at c5 / c4 / c2.
+# Round 4: full GPU tests; interleaved A/B of the protein step (packed input on / off) on this
+# build and on the previous commit's library (build/prev: before the vote-record change); the
+# adversarial layout sweep; the genome-directory workload.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out/r04c; mkdir -p $OUT
 bash scripts/gpu_tests.sh r04c || exit $?
-for rep in 1 2; do
-  for wl in c5 c4 c2; do
-    for pk in 1 0; do
-      timeout -k 10 300 python bench.py --workload $wl --packed-input $pk --no-cpu-baseline \
-        $( [ $rep = 2 ] && echo --no-extras ) > $OUT/${wl}_p${pk}_r${rep}.json 2> $OUT/${wl}_p${pk}_r${rep}.log
-      rc=$?; echo "$wl p$pk r$rep rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
-    done
-  done
-done
-python3 - <<'PY'
-import json,glob
-for f in sorted(glob.glob('gpurun_out/r04c/c*_p*_r*.json')):
-    d=json.loads(open(f).read().strip().splitlines()[-1])
-    e=d.get('e2e_host_call',{})
-    print(f.split('/')[-1], round(d['ms_per_step'],4), d['phases_ms'], 'e2e', round(e.get('ms',0),3))
-PY
-# the adversarial layout sweep (2,000 shared minimizers) on the shipped build, once
+timeout -k 10 400 python scripts/ab_protein.py > $OUT/ab_cur.jsonl 2> $OUT/ab_cur.log
+rc=$?; echo "ab cur rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
+KMERANNO_LIB=kmers.anno_amd/build/prev/libkmeranno.so timeout -k 10 400 python scripts/ab_protein.py \
+  --configs "packed=1" > $OUT/ab_prev.jsonl 2> $OUT/ab_prev.log
+rc=$?; echo "ab prev rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 300 python3 scripts/layout_sweep.py --adversarial --lfs 0.5,0.9 > $OUT/adversarial.jsonl 2> $OUT/adversarial.log
 echo "adversarial rc=$?" >> $OUT/steps.log
-timeout -k 10 700 python bench.py --workload genomes > $OUT/genomes.json 2> $OUT/genomes.log
+timeout -k 10 600 python bench.py --workload genomes > $OUT/genomes.json 2> $OUT/genomes.log
 echo "genomes rc=$?" >> $OUT/steps.log
+python3 - <<'PY'
+import json
+for f in ("ab_cur", "ab_prev"):
+    for line in open(f"gpurun_out/r04c/{f}.jsonl"):
+        d = json.loads(line)
+        print(f, d["workload"], d["config"], d["rep"], round(d["ms"], 4), {k: round(v, 4) for k, v in d["phases_ms"].items()}, d["outputs_equal_first_arm"])
+PY
