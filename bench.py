@@ -634,11 +634,17 @@ def main():
         if world == 1:
             if not args.no_extras:
                 ms = e2e_host(table, residues, offsets, n_fid)
+                with kmeranno.options(packed_input=0):
+                    ms_ascii = e2e_host(table, residues, offsets, n_fid)
                 out["e2e_host_call"] = {
                     "entry": "kma_annotate_proteins (host buffers: pinned staging, H2D, kernel, "
                              "D2H, on the table's pooled stream)",
+                    "packed_input": kmeranno.get_option(kmeranno.OPT_PACKED_INPUT),
+                    "staging_threads": kmeranno.get_option(kmeranno.OPT_HOST_THREADS) or
+                    "min(16, cores)",
                     "ms": ms, "lookups_per_s": n_win / (ms * 1e-3),
-                    "seqs_per_s": n_seq / (ms * 1e-3)}
+                    "seqs_per_s": n_seq / (ms * 1e-3), "kernel_ratio": ms / ph["annotate_kernel"],
+                    "ascii_staging_ms": ms_ascii}
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(sig.keys, sig.fids, residues, offsets)
         if verify is not None:

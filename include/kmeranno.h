@@ -156,6 +156,8 @@ int kma_device_count(int* out_n);
  *                           (host calls while staging: the H2D moves 0.625 B per residue;
  *                           device calls with a pack kernel into the workspace) and the probe
  *                           reads the packed stream; 0 = the probe packs ASCII itself
+ *   KMA_OPT_HOST_THREADS    host calls: threads staging (copying / packing) the input
+ *                           [0: min(16, cores)]; 1..64
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -164,6 +166,7 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_HOST_PIECES 4
 #define KMA_OPT_HASH_SLICE 5
 #define KMA_OPT_PACKED_INPUT 6
+#define KMA_OPT_HOST_THREADS 7
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);
@@ -267,8 +270,9 @@ int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phase
  * min_hits >= 1 (ApplyKmerProcessor.java:91-92). out_tally (optional, length n_fid) receives
  * += 1 per CALLED protein at its fid (the APPLY report's role counts before column mapping).
  * Host form: synchronous, host buffers. A batch of >= 32 MiB of residues is cut into pieces of
- * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16) whose staging and H2D run on
- * the context's copy stream under the previous piece's kernel.                                */
+ * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16) whose staging (packing, under
+ * KMA_OPT_PACKED_INPUT, on KMA_OPT_HOST_THREADS threads) and H2D run on the context's copy
+ * stream under the previous piece's kernel.                                                   */
 int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,

@@ -35,8 +35,8 @@ namespace {
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 7;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}};
+constexpr int kNumOpts = 8;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
@@ -47,6 +47,7 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_HOST_PIECES: return v >= 0 && v <= 16;
     case KMA_OPT_HASH_SLICE: return v >= 0;
     case KMA_OPT_PACKED_INPUT: return v == 0 || v == 1;
+    case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
     default: return false;
   }
 }
@@ -57,7 +58,8 @@ struct EnvOptions {  // tuning builds: the A/B scripts' variables seed the defau
     const std::pair<const char*, int> vars[] = {
         {"KMA_MINIMIZER", KMA_OPT_LAYOUT}, {"KMA_BLOCK_PROTEINS", KMA_OPT_BLOCK_PROTEINS},
         {"KMA_DEFER", KMA_OPT_DEFER}, {"KMA_HOST_PIECES", KMA_OPT_HOST_PIECES},
-        {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}, {"KMA_PACKED_INPUT", KMA_OPT_PACKED_INPUT}};
+        {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}, {"KMA_PACKED_INPUT", KMA_OPT_PACKED_INPUT},
+        {"KMA_HOST_THREADS", KMA_OPT_HOST_THREADS}};
     for (const auto& [name, opt] : vars)
       if (const char* e = getenv(name); e && *e) {
         const int64_t v = strtoll(e, nullptr, 10);
@@ -71,6 +73,13 @@ int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 // The forced table layout (KMA_OPT_LAYOUT): -1 = not forced.
 int forced_layout() { return (int)opt(KMA_OPT_LAYOUT); }
+
+// Host threads a host call stages (copies or packs) its input with (KMA_OPT_HOST_THREADS; 0:
+// min(16, cores)). Packing 5 bits per residue keeps up with the PCIe link only on ~16 threads.
+size_t staging_threads() {
+  const int64_t o = opt(KMA_OPT_HOST_THREADS);
+  return o > 0 ? (size_t)o : std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+}
 }  // namespace
 
 int kma::minimizer_len(int k, uint64_t n_buckets) {
@@ -1022,7 +1031,7 @@ hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size
     return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
   }
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t n_threads = std::min<size_t>({8, hw, n_chunks});
+  const size_t n_threads = std::min<size_t>({staging_threads(), hw, n_chunks});
   std::atomic<size_t> next{0};
   std::atomic<int> err{(int)hipSuccess};
   auto work = [&]() {
@@ -1069,7 +1078,7 @@ hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* l
     return hipSuccess;
   }
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t n_threads = std::min<size_t>({8, hw, n_chunks});
+  const size_t n_threads = std::min<size_t>({staging_threads(), hw, n_chunks});
   std::atomic<uint64_t> next{0};
   std::atomic<int> err{(int)hipSuccess};
   auto work = [&]() {

@@ -43,13 +43,13 @@ EXPORTS = (
 
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
-OPT_PACKED_INPUT = 6
+OPT_PACKED_INPUT, OPT_HOST_THREADS = 6, 7
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
-                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1}
+                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0}
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
 _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
               "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
-              "packed_input": OPT_PACKED_INPUT}
+              "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS}
 
 
 class KmerAnnoError(RuntimeError):
