@@ -11,6 +11,8 @@ rc=$?; echo "ab cur rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
 KMERANNO_LIB=kmers.anno_amd/build/prev/libkmeranno.so timeout -k 10 400 python scripts/ab_protein.py \
   --configs "packed=1" > $OUT/ab_prev.jsonl 2> $OUT/ab_prev.log
 rc=$?; echo "ab prev rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/c5.json 2> $OUT/c5.log
+echo "bench c5 rc=$?" >> $OUT/steps.log
 timeout -k 10 300 python3 scripts/layout_sweep.py --adversarial --lfs 0.5,0.9 > $OUT/adversarial.jsonl 2> $OUT/adversarial.log
 echo "adversarial rc=$?" >> $OUT/steps.log
 timeout -k 10 600 python bench.py --workload genomes > $OUT/genomes.json 2> $OUT/genomes.log
