@@ -373,7 +373,18 @@ struct ContigArgs {
 // Forward positions per lane of the 6-frame probe (2 windows each). 2 raises the kernel to 97
 // VGPRs (4 waves/SIMD) and measured slower at c3 (0.139 vs 0.124 ms, profiles/r02i_variants.log).
 constexpr int kContigPos = KMA_CONTIG_POS;
-constexpr int kContigTile = 256 * kContigPos;  // forward positions per block
+// 256-position slices a 6-frame probe block works through one after the other (round 3: 1).
+// The block's fixed work — contig search, DNA tile load, translation, compaction, its group-sum
+// atomic — is paid once for all of them, and the slices' gathers follow each other while the
+// other blocks of the CU overlap them; a lane keeps one slice's loads in flight, so VGPRs stay
+// those of one slice (kContigPos = 2 holds two slices' loads at once: 97 VGPRs, 4 waves/SIMD,
+// measured slower).
+#ifndef KMA_CONTIG_SEQ
+#define KMA_CONTIG_SEQ 2
+#endif
+constexpr int kContigSeq = KMA_CONTIG_SEQ;
+static_assert(kContigSeq == 1 || kContigPos == 1, "sequential slices take one position per lane");
+constexpr int kContigTile = 256 * kContigPos * kContigSeq;  // forward positions per block
 constexpr uint32_t kScanGroup = 256;  // probe blocks per emit-offset group sum
 // Up to this many groups (16 loads per lane, one round trip) an emit block sums the group sums
 // before its own; beyond, a one-block scan turns them into prefixes first.

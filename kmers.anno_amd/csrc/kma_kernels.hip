@@ -819,8 +819,14 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
   return lo;
 }
 
+// Waves per SIMD of the 6-frame probe: 8 with one slice per block (64 VGPRs); the sequential
+// slices' loop carries a few more scalar and vector values (SGPR spills land in VGPR lanes) and
+// takes 7 to stay clear of scratch.
+#ifndef KMA_CONTIG_OCC
+#define KMA_CONTIG_OCC (KMA_CONTIG_SEQ > 1 ? 7 : 8)
+#endif
 template <int K, int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void contigs_probe_quad_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_OCC, 8))) void contigs_probe_quad_kernel(
     ContigArgs a) {
   // K > 8: a wide table (16-byte slots, kma_internal.h): one slot per lane of the quad.
   constexpr bool kWide = wide_k(K);
@@ -833,7 +839,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   __shared__ uint8_t aa_p[kSpan], aa_m[kSpan];
   __shared__ uint64_t offc[kOffCache + 1];
   __shared__ uint32_t crange[2];
-  __shared__ uint32_t wave_tot[kWavesPerBlock * kContigPos];
+  constexpr int CP = kContigPos * kContigSeq;  // slices of 256 positions per block
+  __shared__ uint32_t wave_tot[kWavesPerBlock * CP];
   __shared__ uint8_t codon[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   // offsets[0] through the constant address space: a scalar load (every block reads it, so the
@@ -895,7 +902,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   // p takes position 16 p + q of its wave, so that one load instruction covers 16 consecutive
   // positions (same-frame windows 3 apart share minimizers, hence lines); the results go back
   // to position order through LDS before the compaction.
-  constexpr int CP = kContigPos;
+  constexpr int CL = kContigPos;  // positions per lane held at once (per sequential slice)
 #if KMA_LANE_PERM
   const uint32_t tp = (uint32_t)(wave * 64 + 16 * (lane & 3) + (lane >> 2));
 #else
@@ -919,12 +926,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       len = (int64_t)(a.offsets[c + 1] - a.offsets[c]);
     }
   };
-  uint32_t contig[CP];
-  uint64_t key[CP][2];
-  uint32_t bk[CP][2];
+  // Verdicts of every position go through LDS (fid + 1, 0 = no hit), lane t then takes position
+  // t's (back to position order after KMA_LANE_PERM) for the compaction.
+  __shared__ uint32_t xv[CP][2][256];
+#pragma unroll 1
+  for (int sq = 0; sq < kContigSeq; ++sq) {
+  uint32_t contig[CL];
+  uint64_t key[CL][2];
+  uint32_t bk[CL][2];
 #pragma unroll
-  for (int h = 0; h < CP; ++h) {
-    const uint32_t tt = tp + 256u * h;
+  for (int h = 0; h < CL; ++h) {
+    const uint32_t tt = tp + 256u * (sq * CL + h);
     const uint64_t g = base + r0 + tt;
     contig[h] = c_lo;
     int64_t x = 0, len = 0;
@@ -942,9 +954,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     bk[h][0] = pv ? home_bucket(key[h][0], K, M, nb) : kNone;
     bk[h][1] = mv ? home_bucket(key[h][1], K, M, nb) : kNone;
   }
-  uint4 q[CP][2][4][kH];  // every window's quad buckets: all dwordx4 in flight
+  uint4 q[CL][2][4][kH];  // every window's quad buckets: all dwordx4 in flight
 #pragma unroll
-  for (int h = 0; h < CP; ++h)
+  for (int h = 0; h < CL; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const uint32_t b0 = quad_bcast<0>(bk[h][j]), b1 = quad_bcast<1>(bk[h][j]);
@@ -959,10 +971,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
     }
   KMA_CLK(3);  // bucket loads issued
-  bool hit[CP][2];
-  uint32_t fid[CP][2];
 #pragma unroll
-  for (int h = 0; h < CP; ++h)
+  for (int h = 0; h < CL; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const uint32_t klo = (uint32_t)key[h][j];
@@ -982,70 +992,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
       const uint32_t word = quad_reduce_scatter(raw, part);
       const uint32_t w = bk[h][j] != kNone ? word : 0u;
-      hit[h][j] = (w & kWordHit) != 0u;
-      fid[h][j] = w & kFidMask;
+      bool hit = (w & kWordHit) != 0u;
+      uint32_t fid = w & kFidMask;
       uint32_t sid = bk[h][j] * kS + ((w >> kSlotShift) & (kS - 1));
       if (bk[h][j] != kNone && w == 0u) {  // rare: home missed, every filter position set
         if constexpr (kWide)
-          hit[h][j] = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+          hit = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid, sid);
         else
-          hit[h][j] = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid[h][j], sid);
+          hit = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid, sid);
       }
-      if (a.strict_pass && hit[h][j]) {  // KmerFactory.Strict: locations counted by slot id
+      if (a.strict_pass && hit) {  // KmerFactory.Strict: locations counted by slot id
         if (a.strict_pass == 1) atomicAdd(a.slot_count + sid, 1u);
-        else hit[h][j] = a.slot_count[sid] == 1u;
+        else hit = a.slot_count[sid] == 1u;
       }
-      if (a.tally && hit[h][j] && fid[h][j] < a.n_fid)
-        atomicAdd(a.tally + (uint64_t)contig[h] * a.n_fid + fid[h][j], 1u);
+      if (a.tally && hit && fid < a.n_fid)
+        atomicAdd(a.tally + (uint64_t)contig[h] * a.n_fid + fid, 1u);
+      xv[sq * CL + h][j][tp] = hit ? fid + 1u : 0u;
     }
+  }  // sequential slices
   KMA_CLK(4);  // matched (chain walks done)
-#if KMA_LANE_PERM
-  {  // back to position order: lane t takes position t's verdicts
-    __shared__ uint32_t xv[CP][2][256];
-#pragma unroll
-    for (int h = 0; h < CP; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) xv[h][j][tp] = hit[h][j] ? fid[h][j] + 1u : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < CP; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t v = xv[h][j][t];
-        hit[h][j] = v != 0u;
-        fid[h][j] = v - 1u;
-      }
-  }
-#endif
-  // Block-local compaction in canonical order (position, '+' before '-'): positions of the
-  // first 256 before those of the next.
-  uint64_t bp[CP], bm[CP];
-#pragma unroll
+  __syncthreads();
+  // Block-local compaction in canonical order (position, '+' before '-'): slice by slice, each
+  // slice's verdicts read back from LDS twice (counts, then records) rather than kept live.
+#pragma unroll 1
   for (int h = 0; h < CP; ++h) {
-    bp[h] = __ballot(hit[h][0]);
-    bm[h] = __ballot(hit[h][1]);
-    if (lane == 0) wave_tot[h * kWavesPerBlock + wave] = (uint32_t)(__popcll(bp[h]) + __popcll(bm[h]));
+    const uint64_t bp = __ballot(xv[h][0][t] != 0u), bm = __ballot(xv[h][1][t] != 0u);
+    if (lane == 0) wave_tot[h * kWavesPerBlock + wave] = (uint32_t)(__popcll(bp) + __popcll(bm));
   }
   __syncthreads();
   // Staged records are the final kma_hit (the emit pass only copies them): contig, left =
   // KmerPosition.calcLeft, fid, strand and frame (KmerPosition.java:50-93).
   uint32_t total = 0;
   uint4* st = reinterpret_cast<uint4*>(a.staging) + (uint64_t)blockIdx.x * (2 * kContigTile);
-#pragma unroll
+#pragma unroll 1
   for (int h = 0; h < CP; ++h) {
-    uint32_t o = total + popc_below(bp[h]) + popc_below(bm[h]);
+    const uint32_t v0 = xv[h][0][t], v1 = xv[h][1][t];
+    const uint64_t bp = __ballot(v0 != 0u), bm = __ballot(v1 != 0u);
+    uint32_t o = total + popc_below(bp) + popc_below(bm);
     for (int w = 0; w < kWavesPerBlock; ++w) {
       if (w < wave) o += wave_tot[h * kWavesPerBlock + w];
       total += wave_tot[h * kWavesPerBlock + w];
     }
-    if (hit[h][0] || hit[h][1]) {  // hits only at positions inside a contig (g < end)
+    if (v0 | v1) {  // hits only at positions inside a contig (g < end)
       uint32_t c;
       int64_t x, len;
       locate(t + 256u * h, c, x, len);
       const uint32_t left = (uint32_t)(x + 1);
-      if (hit[h][0]) st[o++] = make_uint4(c, left, fid[h][0], '+' | (uint32_t)(x % 3 + 1) << 8);
-      if (hit[h][1])
-        st[o] = make_uint4(c, left, fid[h][1], '-' | (uint32_t)((len - 3 * K - x) % 3 + 1) << 8);
+      if (v0) st[o++] = make_uint4(c, left, v0 - 1u, '+' | (uint32_t)(x % 3 + 1) << 8);
+      if (v1) st[o] = make_uint4(c, left, v1 - 1u, '-' | (uint32_t)((len - 3 * K - x) % 3 + 1) << 8);
     }
   }
   if (t == 0) {

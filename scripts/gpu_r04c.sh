@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: full GPU tests; interleaved A/B of the protein step (packed input on / off) on this
 # build and on the previous commit's library (build/prev: before the vote-record change); the
-# adversarial layout sweep; the genome-directory workload.
+# c5 bench line; the 6-frame probe with two sequential slices per block vs one (build/seq1).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out/r04c; mkdir -p $OUT
@@ -13,12 +13,19 @@ KMERANNO_LIB=kmers.anno_amd/build/prev/libkmeranno.so timeout -k 10 400 python s
 rc=$?; echo "ab prev rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/c5.json 2> $OUT/c5.log
 echo "bench c5 rc=$?" >> $OUT/steps.log
-timeout -k 10 300 python3 scripts/layout_sweep.py --adversarial --lfs 0.5,0.9 > $OUT/adversarial.jsonl 2> $OUT/adversarial.log
-echo "adversarial rc=$?" >> $OUT/steps.log
-timeout -k 10 600 python bench.py --workload genomes > $OUT/genomes.json 2> $OUT/genomes.log
-echo "genomes rc=$?" >> $OUT/steps.log
+for rep in 1 2; do
+  for lib in default seq1; do
+    if [ $lib = default ]; then unset KMERANNO_LIB; else export KMERANNO_LIB=kmers.anno_amd/build/$lib/libkmeranno.so; fi
+    timeout -k 10 300 python bench.py --workload c3 --no-cpu-baseline --no-extras > $OUT/c3_${lib}_r$rep.json 2> $OUT/c3_${lib}_r$rep.log
+    rc=$?; echo "c3 $lib r$rep rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
+  done
+done
+unset KMERANNO_LIB
 python3 - <<'PY'
-import json
+import json, glob
+for f in sorted(glob.glob("gpurun_out/r04c/c3_*.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split("/")[-1], round(d["ms_per_step"], 4), d["phases_ms"])
 for f in ("ab_cur", "ab_prev"):
     for line in open(f"gpurun_out/r04c/{f}.jsonl"):
         d = json.loads(line)

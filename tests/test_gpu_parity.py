@@ -591,20 +591,21 @@ def test_contigs_device_graph_capture_replay(kma, oracle_c):
 
 
 def test_contigs_device_many_groups_scanned(kma):
-    """A device call of more than kDirectGroups x 256 probe blocks (> 67M bases: the emit pass
-    scans the group sums first instead of summing them per block) equals the same genome cut
-    into calls below that size, hit for hit after re-basing, with the same total."""
+    """A device call of more than kDirectGroups x 256 probe blocks (> 134M bases at 512
+    positions per block: the emit pass scans the group sums first instead of summing them per
+    block) equals the same genome cut into calls below that size, hit for hit after re-basing,
+    with the same total."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(2_000_000, 8, 77, table_size=300_000, n_fid=300)
-    # 40 copies of the genome: 80 Mbp in 320 contigs (1,221 emit-offset groups)
-    reps = 40
+    # 70 copies of the genome: 140 Mbp in 560 contigs (1,069 emit-offset groups)
+    reps = 70
     n0 = int(wl.offsets[-1])
     dna = np.concatenate([np.tile(wl.dna[:n0], reps), np.zeros(64, np.uint8)])
     off = np.concatenate([[0]] + [wl.offsets[1:] + np.uint64(i * n0) for i in range(reps)])
     off = off.astype(np.uint64)
     n_contig, n_bases = len(off) - 1, int(off[-1])
-    assert n_bases > 1024 * 256 * 256
+    assert n_bases > 1024 * 256 * 512
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
@@ -616,7 +617,7 @@ def test_contigs_device_many_groups_scanned(kma):
         def call(lo, hi):
             sub = off[lo:hi + 1]
             d_off = torch.from_numpy(sub.view(np.int64)).to(dev)
-            cap = 12_000_000
+            cap = 16_000_000
             d_hits = torch.zeros(cap * kma.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
             kma.annotate_contigs_device(t, ws, d_dna.data_ptr(), d_off.data_ptr(), hi - lo,
                                         int(sub[-1] - sub[0]), 11, d_hits.data_ptr(), cap,
