@@ -48,6 +48,15 @@ def restricted_oracle_table(oracle_c, keys: np.ndarray, fids: np.ndarray, residu
                                       fids[keep].astype(np.int32))
 
 
+def full_oracle_table(oracle_c, keys: np.ndarray, fids: np.ndarray, k: int = K):
+    """The oracle's HashMap of every table row, in file order (10^8 rows load in ~20 s on the
+    GPU box's host: cheaper than restricting them to a whole 1M-protein batch's windows)."""
+    rows = unpack_keys(keys, k)
+    n = len(rows)
+    return oracle_c.Table.from_buffer(rows.tobytes(), np.arange(n + 1, dtype=np.uint64) * k,
+                                      fids.astype(np.int32))
+
+
 def take_proteins(residues: np.ndarray, offsets: np.ndarray, idx: np.ndarray):
     """(residues padded by 32 bytes, offsets) of the proteins idx of a batch, in idx order."""
     idx = np.asarray(idx, np.int64)

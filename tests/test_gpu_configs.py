@@ -7,17 +7,20 @@ Every workload is the bench's own (same generator, same seeds, rank 0):
   c4  ONE 1M-protein batch against the 10^7-row table, cut into 8 residue-balanced shards the
       way the bench's strong-scaling run cuts it (kmeranno.dist.shard): the shards' outputs
       concatenated equal the whole-batch host call on a 4-replica table, the shard tallies sum
-      to the called-fid histogram, and a 20k-protein sample is bit-exact vs the oracle
+      to the called-fid histogram, and the whole batch is bit-exact vs the oracle
       (ApplyKmerProcessor.java:122-148);
-  c5  the 1M-protein batch against the 10^8-row table at load factor 0.5 (the headline) and
-      0.9 (the layout the creator keeps at that load), a 20k sample vs the oracle each, and
-      whole-batch properties.
-The oracle tables are restricted to the rows the batch can look up (tests/helpers.py).
+  c5  the 1M-protein batch against the 10^8-row table at load factor 0.5 (the headline): the
+      whole batch bit-exact vs the oracle, and whole-batch properties; at 0.9 (the layout the
+      creator keeps at that load) equal to the 0.5 answer, plus a 20k sample vs the oracle.
+Whole-batch checks load the full table into the oracle; sample checks use the rows the sample
+can look up (tests/helpers.py).
 """
+import os
+
 import numpy as np
 import pytest
 
-from helpers import restricted_oracle_table, take_proteins, unpack_keys
+from helpers import full_oracle_table, restricted_oracle_table, take_proteins, unpack_keys
 
 pytestmark = pytest.mark.gpu
 K = 8
@@ -38,6 +41,16 @@ def c5data():
     res, off, kinds, true_fid = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
     print(f"c5 workload generated: {len(res)} residues", flush=True)
     return sig, res, off, kinds, true_fid
+
+
+def _whole_batch_vs_oracle(oracle_c, sig, res, off, fid, cnt, st):
+    """Every protein of the batch against the oracle (ApplyKmerProcessor.java:122-148 restated:
+    the whole table in its String-keyed chained map), run on 16 host threads."""
+    ot = full_oracle_table(oracle_c, sig.keys, sig.fids)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    efid, ecnt, est = oracle_c.apply_mt(ot, res, off, K, 5, 0, threads)
+    assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    return est
 
 
 def _sample_vs_oracle(oracle_c, sig, res, off, fid, cnt, st, n=20_000, seed=55):
@@ -94,7 +107,8 @@ def test_config5_size_sample_and_properties(kma, oracle_c, c5data, monkeypatch):
     copies = (kinds == 0) & (st == 1)
     assert copies.sum() > 0.2 * n_seq  # decoy hits make many copies AMBIGUOUS at 10^8
     assert (fid[copies] == true_fid[copies]).mean() > 0.999
-    _sample_vs_oracle(oracle_c, sig, res, off, fid, cnt, st)
+    # the whole 1M-protein batch bit-exact against the oracle (round 3: a 20k sample)
+    _whole_batch_vs_oracle(oracle_c, sig, res, off, fid, cnt, st)
 
 
 @pytest.mark.timeout(600)
@@ -174,7 +188,7 @@ def test_config4_shards_vs_whole_batch_and_oracle(kma, oracle_c):
     assert (d_tally.cpu().numpy().astype(np.uint32) == tally).all()
     assert (tally == np.bincount(fid[st == 1], minlength=n_fid)).all()
     assert (st == 1).sum() > 0.4 * n_seq
-    _sample_vs_oracle(oracle_c, sig, res, off, fid, cnt, st, seed=44)
+    _whole_batch_vs_oracle(oracle_c, sig, res, off, fid, cnt, st)
 
 
 @pytest.mark.timeout(600)
