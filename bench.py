@@ -213,6 +213,88 @@ def pmc_traffic(workload: str, kernel: str):
     return rec["traffic_bytes"], rec.get("read_requests"), src, False
 
 
+def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
+    """Signature table built on rank 0's GPU with the library creators' layout rule
+    (kmeranno.choose_layout), replicated over RCCL (xGMI) to the other ranks."""
+    nb = kmeranno.buckets_for(t_size, load_factor)
+    slots = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int64, device=dev)
+    layout = torch.zeros(1, dtype=torch.int32, device=dev)
+    if rank == 0:
+        winner = torch.empty(nb * kmeranno.bucket_slots(), dtype=torch.int32, device=dev)
+        status = torch.zeros(4, dtype=torch.int32, device=dev)
+        keys = torch.from_numpy(keys_np.view(np.int64)).to(dev)
+        fids = torch.from_numpy(fids_np.view(np.int32)).to(dev)
+
+        times = {}
+
+        def build(m):
+            tb, te = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            tb.record()
+            kmeranno.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
+                                  fids.data_ptr(), len(keys_np), status.data_ptr(), sp, k=K,
+                                  layout=m)
+            te.record()
+            torch.cuda.synchronize()
+            st = status.cpu().numpy().astype(np.int64)
+            assert st[0] == 0, "table full"
+            times[m] = tb.elapsed_time(te)
+            return st
+
+        # the library creators' rule (size rule, then m = 7 / flat rebuilds by measurement)
+        m, st = kmeranno.choose_layout(K, nb, build)
+        ms = times[m]
+        layout.fill_(m)
+        log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 8 * kmeranno.bucket_slots() / 2**20:.0f} MiB), "
+            f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
+            f"built in {ms:.1f} ms")
+        del winner, keys, fids
+    if world > 1:
+        kdist.broadcast_table(slots, src=0)  # RCCL over xGMI (host-staged under gloo)
+        kdist.broadcast(layout, src=0)
+        torch.cuda.synchronize()
+    m = int(layout.item())
+    return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m), slots
+
+
+def timed(step, ws, args, world, stream, dev, before=None, after=None):
+    """W warmup steps, then exactly K steps between barrier + synchronize; then the same K steps
+    again with the library's hipEvents around its kernels. Max over ranks of (wall s, GPU ms,
+    main-kernel ms per call, rest ms per call)."""
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if before is not None:
+        before()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    if after is not None:
+        after()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    ws.timing(True)
+    for _ in range(args.steps):
+        step()
+    n_t, phases = ws.phases_read()
+    ws.timing(False)
+    names = list(phases)
+    stats = torch.tensor([elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        kdist.all_reduce_max(stats)
+    v = stats.tolist()
+    return v[0], v[1], dict(zip(names, v[2:]))
+
+
 def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
     """The dominant kernel's line, by the SURVEY §8(d) rule: achieved = its algorithmic bytes
     per launch (one 64-B bucket line per probed window + the input it streams) / its

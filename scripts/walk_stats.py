@@ -2,7 +2,7 @@
 """Chain-walk event counts of one protein launch (tuning only).
 
 Needs a library built with the counters:
-    make -C kmers.anno_amd variant VNAME=count "VFLAGS=-DKMA_TUNE_COUNT -DKMA_COOP_WALK=0"
+    make -C kmers.anno_amd variant VNAME=count VFLAGS=-DKMA_TUNE_COUNT
     KMERANNO_LIB=kmers.anno_amd/build/count/libkmeranno.so python scripts/walk_stats.py c5 [lf]
 
 Prints one JSON line: flushes, queued walks, probed windows, home hits and walk hits of one
