@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out/r04c; mkdir -p $OUT
-bash scripts/gpu_tests.sh r04c || exit $?
+bash scripts/gpu_tests.sh r04c tests/test_gpu_multirank.py || exit $?
 timeout -k 10 400 python scripts/ab_protein.py > $OUT/ab_cur.jsonl 2> $OUT/ab_cur.log
 rc=$?; echo "ab cur rc=$rc" >> $OUT/steps.log; [ $rc = 0 ] || exit $rc
 KMERANNO_LIB=kmers.anno_amd/build/prev/libkmeranno.so timeout -k 10 400 python scripts/ab_protein.py \
