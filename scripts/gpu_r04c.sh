@@ -21,6 +21,13 @@ for rep in 1 2; do
   done
 done
 unset KMERANNO_LIB
+# tuning builds: chain-walk event counts at c5, block timelines at c2 and c3
+KMERANNO_LIB=kmers.anno_amd/build/count/libkmeranno.so timeout -k 10 300 python scripts/walk_stats.py c5 > $OUT/walk_c5.json 2> $OUT/walk_c5.log
+echo "walk c5 rc=$?" >> $OUT/steps.log
+KMERANNO_LIB=kmers.anno_amd/build/clk/libkmeranno.so timeout -k 10 200 python scripts/block_clock.py c2 > $OUT/clock_c2.json 2> $OUT/clock_c2.log
+echo "clock c2 rc=$?" >> $OUT/steps.log
+KMERANNO_LIB=kmers.anno_amd/build/clk/libkmeranno.so timeout -k 10 200 python scripts/block_clock.py c3 > $OUT/clock_c3.json 2> $OUT/clock_c3.log
+echo "clock c3 rc=$?" >> $OUT/steps.log
 python3 - <<'PY'
 import json, glob
 for f in sorted(glob.glob("gpurun_out/r04c/c3_*.json")):
