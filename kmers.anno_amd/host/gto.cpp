@@ -2,6 +2,8 @@
 #include "gto.h"
 
 #include <dirent.h>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -9,6 +11,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <string_view>
 #include <unordered_map>
 
 namespace kma_host {
@@ -82,6 +85,14 @@ struct Parser {
   std::string string() {
     if (*p != '"') error("expected string");
     ++p;
+    {  // the common case, no escape: one memchr to the closing quote, one for a backslash
+      const char* q = static_cast<const char*>(std::memchr(p, '"', end - p));
+      if (q && !std::memchr(p, '\\', q - p)) {
+        std::string s(p, q);
+        p = q + 1;
+        return s;
+      }
+    }
     std::string s;
     for (;;) {
       const char* q = p;
@@ -136,8 +147,13 @@ struct Parser {
     ws();
     if (p >= end) error("unexpected end");
     if (*p == '"') return skip_string();
-    if (*p != '{' && *p != '[') {
-      (void)value();  // scalars are small
+    if (*p != '{' && *p != '[') {  // number / true / false / null: up to the next delimiter
+      const char* q = p;
+      while (q < end && *q != ',' && *q != '}' && *q != ']' && *q != ' ' && *q != '\n' &&
+             *q != '\t' && *q != '\r')
+        ++q;
+      if (q == p) error("bad value");
+      p = q;
       return;
     }
     int depth = 0;
@@ -153,6 +169,19 @@ struct Parser {
     }
     error("unterminated container");
   }
+  // An object key as a view into the text when it holds no escape (GTO keys never do), else
+  // decoded into `buf`.
+  std::string_view key(std::string& buf) {
+    if (p >= end || *p != '"') error("expected string");
+    const char* q = static_cast<const char*>(std::memchr(p + 1, '"', end - p - 1));
+    if (q && !std::memchr(p + 1, '\\', q - p - 1)) {
+      const std::string_view v(p + 1, (size_t)(q - p - 1));
+      p = q + 1;
+      return v;
+    }
+    buf = string();
+    return buf;
+  }
   // Members of an object, calling f(key) with p at the value; f consumes the value.
   template <class F>
   void members(F f) {
@@ -164,9 +193,10 @@ struct Parser {
       ++p;
       return;
     }
+    std::string buf;
     for (;;) {
       ws();
-      const std::string k = string();
+      const std::string_view k = key(buf);
       ws();
       if (p >= end || *p != ':') error("expected ':'");
       ++p;
@@ -320,13 +350,43 @@ std::string scalar_string(Parser& ps) {  // a string or number member as text
   return ps.value().as_string();
 }
 
+// A GTO mapped read-only (the apply loader reads ~6 MB per genome, most of it contig DNA it
+// skips: mapping the page cache saves a zero-filled buffer and a copy). Falls back to a read.
+struct MappedFile {
+  const char* data = nullptr;
+  size_t size = 0;
+  std::string fallback;
+  void* map = MAP_FAILED;
+  explicit MappedFile(const std::string& path) {
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open " + path);
+    struct stat st;
+    if (fstat(fd, &st) == 0 && st.st_size > 0)
+      map = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (map != MAP_FAILED) {
+      data = static_cast<const char*>(map);
+      size = (size_t)st.st_size;
+    } else {
+      fallback = slurp(path);
+      data = fallback.data();
+      size = fallback.size();
+    }
+  }
+  ~MappedFile() {
+    if (map != MAP_FAILED) ::munmap(map, size);
+  }
+  MappedFile(const MappedFile&) = delete;
+  MappedFile& operator=(const MappedFile&) = delete;
+};
+
 }  // namespace
 
 Genome load_genome_pegs(const std::string& path) {
-  const std::string text = slurp(path);
-  Parser ps{text.data(), text.data(), text.data() + text.size()};
+  const MappedFile text(path);
+  Parser ps{text.data, text.data, text.data + text.size};
   Genome g;
-  ps.members([&](const std::string& k) {
+  ps.members([&](std::string_view k) {
     if (k == "id") {
       g.id = scalar_string(ps);
     } else if (k == "scientific_name") {
@@ -336,7 +396,7 @@ Genome load_genome_pegs(const std::string& path) {
     } else if (k == "features") {
       ps.elements([&]() {
         Feature ft;
-        ps.members([&](const std::string& fk) {
+        ps.members([&](std::string_view fk) {
           if (fk == "id") ft.id = scalar_string(ps);
           else if (fk == "type") ft.type = scalar_string(ps);
           else if (fk == "function") ft.function = scalar_string(ps);

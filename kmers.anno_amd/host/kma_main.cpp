@@ -511,6 +511,19 @@ int run_contigs(const std::vector<std::string>& args) {
   return 0;
 }
 
+// `kma gto-dump file.gto`: what apply's loader reads from a GTO, one feature per line (id, type,
+// function, protein), after the genome's id, name and genetic code; no device needed (tests
+// compare it with a JSON library's reading).
+int run_gto_dump(const std::vector<std::string>& args) {
+  if (args.size() != 1) throw UsageError("usage: kma gto-dump file.gto");
+  const Genome g = load_genome_pegs(args[0]);
+  std::printf("%s\t%s\t%d\n", g.id.c_str(), g.name.c_str(), g.genetic_code);
+  for (const Feature& f : g.features)
+    std::printf("%s\t%s\t%s\t%s\n", f.id.c_str(), f.type.c_str(), f.function.c_str(),
+                f.protein.c_str());
+  return 0;
+}
+
 const char* kCommands =
     "Valid commands are\n"
     "  apply     apply a discriminating-kmer database to genomes to create a role-count file\n"
@@ -528,6 +541,7 @@ int main(int argc, char** argv) {
   try {
     if (command == "apply") return run_apply(rest);
     if (command == "contigs") return run_contigs(rest);
+    if (command == "gto-dump") return run_gto_dump(rest);
     if (command == "-h" || command == "--help") {
       std::fputs(kCommands, stdout);
       return 0;

@@ -187,3 +187,46 @@ def test_kma_contigs_report(kma_bin, oracle_c, small_gto, apply_inputs, tmp_path
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.splitlines() == exp and len(exp) > 5000
+
+
+def _dump_expected(gto):
+    lines = [f"{gto.get('id', '')}\t{gto.get('scientific_name', '')}\t"
+             f"{int(gto.get('genetic_code', 11))}"]
+    for f in gto.get("features", []):
+        lines.append("\t".join(str(f.get(k, "")) for k in
+                               ("id", "type", "function", "protein_translation")))
+    return lines
+
+
+def test_gto_apply_loader_matches_json(kma_bin, small_gto, tmp_path):
+    """apply's GTO loader (host/gto.cpp load_genome_pegs: mapped file, keys as views, skipped
+    members never built) reads what a JSON library reads: the reference's small.gto, and a
+    GTO holding escapes (quotes, backslashes, \\u, surrogate pairs) in the kept strings,
+    brackets and quotes inside skipped strings, nested skipped containers, numbers, booleans
+    and null, and a numeric genetic code given as a string."""
+    path = tmp_path / "small.gto"
+    with gzip.open(os.path.join(GOLDEN, "small.gto.gz"), "rb") as f:
+        path.write_bytes(f.read())
+    out = subprocess.run([kma_bin, "gto-dump", str(path)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == _dump_expected(small_gto)
+    tricky = {
+        "id": "123.4", "scientific_name": "Tricky \"quoted\" \\ name é \U0001F600",
+        "genetic_code": "4", "domain": "Bacteria", "flag": True, "nothing": None,
+        "contigs": [{"id": "c\"1]", "dna": "ac]}gt\\\"" * 50}],
+        "subsystems": [{"a": [1, 2.5e3, -7, {"b": "}{][\",\\"}], "c": False}],
+        "features": [
+            {"id": "fig|123.4.peg.1", "type": "CDS", "location": [["c1", 1, "+", 30]],
+             "function": "role \"A\" / \\B\\ ü", "protein_translation": "MKV*LL",
+             "annotations": [["x", "y\"}]", 0.5]], "aliases": []},
+            {"id": "fig|123.4.rna.1", "type": "rna", "function": "tRNA", "quality": {}},
+            {"type": "peg", "id": "fig|123.4.peg.2", "protein_translation": "",
+             "family_assignments": [["PGF", "x", "y", "z"]], "function": ""},
+        ],
+    }
+    path = tmp_path / "tricky.gto"
+    path.write_text(json.dumps(tricky, indent=1))
+    out = subprocess.run([kma_bin, "gto-dump", str(path)], capture_output=True,
+                         encoding="utf-8")
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == _dump_expected(tricky)
