@@ -204,6 +204,7 @@ __device__ __forceinline__ uint32_t match_part_raw(const uint4 (&v)[kBucketHalve
     const uint32_t want = (need >> (2u * FB * (4u * h + part))) & PM;
     missing |= want & ~held;
   }
+  if constexpr (2 * FB > 4) missing = (missing | missing >> FB) & ((1u << FB) - 1u);  // <= 4 bits
   return w | missing << kAbsentShift;  // nonzero: a filter position of the key is clear
 }
 __device__ __forceinline__ uint32_t match_part(const uint4 (&v)[kBucketHalves], uint32_t kl,

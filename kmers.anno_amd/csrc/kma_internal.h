@@ -42,7 +42,7 @@ constexpr int kSlotBits = kSlotsPerBucket == 16 ? 4 : 3;
 #define KMA_FILTER_BITS 2
 #endif
 constexpr int kFilterBits = KMA_FILTER_BITS;
-static_assert(kFilterBits == 1 || kFilterBits == 2, "one or two filter bits per slot");
+static_assert(kFilterBits >= 1 && kFilterBits <= 3, "one to three filter bits per slot");
 constexpr uint32_t kFidBits = 24 - kFilterBits;  // fid width (KMA_MAX_FID: 22 bits)
 constexpr uint32_t kFidMask = (1u << kFidBits) - 1;
 constexpr uint32_t kKeyHiMask = 0xFF000000u;   // key bits 32..39 in the high dword
@@ -77,10 +77,14 @@ __host__ __device__ inline uint64_t slot_make(uint64_t key, uint32_t fid) {
 #endif
 template <int S>
 __host__ __device__ inline uint32_t filter_pos(uint32_t klo, int h) {
-  constexpr int bits = (S * kFilterBits == 32) ? 5 : (S * kFilterBits == 16) ? 4
-                     : (S * kFilterBits == 8) ? 3 : 2;
+  constexpr int n = S * kFilterBits;  // positions per bucket
+  constexpr int bits = (n == 32) ? 5 : (n == 16) ? 4 : (n == 8) ? 3 : 2;
 #if KMA_HASH_LITE
   const uint32_t x = klo * 0x9E3779B1u;
+  if constexpr ((n & (n - 1)) != 0) {  // 3 bits per slot: 24 (12 wide) positions, fast range
+    const uint32_t r = h == 0 ? x : h == 1 ? (x << 11 | x >> 21) : (x << 22 | x >> 10);
+    return (uint32_t)(((uint64_t)r * n) >> 32);
+  }
   return h ? (x >> (32 - 2 * bits)) & ((1u << bits) - 1u) : x >> (32 - bits);
 #else
   return ((klo * (h ? 0x85EBCA77u : 0x9E3779B1u)) + (h ? 0x165667B1u : 0u)) >> (32 - bits);
