@@ -338,7 +338,7 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
 
 def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
     """Roofline of the protein path's probe kernel (rank 0's shard, times max over ranks)."""
-    packed = kmeranno.get_option(kmeranno.OPT_PACKED_INPUT) == 1
+    packed = "pack_kernel" in ph
     return roofline("windows x 64 B + residues (" + ("packed: 0.625 B" if packed else "1 B") +
                     " each)", workload,
                     f"annotate_kernel<{K}, {m}, 8, {'true' if packed else 'false'}> "
@@ -600,10 +600,10 @@ def main():
                          "staged, to rehearse several ranks on one GPU (with --same-device)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses device 0 (multi-rank rehearsal on a 1-GPU box)")
-    ap.add_argument("--packed-input", type=int, default=1, choices=(0, 1),
-                    help="KMA_OPT_PACKED_INPUT: 1 = residues packed to 5 bits by a pack kernel "
-                         "inside the step, then the packed probe (default); 0 = the probe packs "
-                         "ASCII itself")
+    ap.add_argument("--packed-input", type=int, default=1, choices=(0, 1, 2),
+                    help="KMA_OPT_PACKED_INPUT: 1 (default) = batches of >= 2^25 residues are "
+                         "packed to 5 bits by a pack kernel inside the step, then the packed "
+                         "probe; 2 = every batch; 0 = the probe packs ASCII itself")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, check the multi-rank outputs, tally and table against "
                          "single-rank calls on rank 0 (exit 1 on a mismatch)")

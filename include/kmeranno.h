@@ -153,9 +153,10 @@ int kma_device_count(int* out_n);
  *                           1..16
  *   KMA_OPT_HASH_SLICE      kma_hash_annotate: candidates per prototype slice [0: 2^31 - 1]
  *   KMA_OPT_PACKED_INPUT    protein calls [1]: residues are packed to 5 bits before the probe
- *                           (host calls while staging: the H2D moves 0.625 B per residue;
- *                           device calls with a pack kernel into the workspace) and the probe
- *                           reads the packed stream; 0 = the probe packs ASCII itself
+ *                           and the probe reads the packed stream: host calls while staging
+ *                           (the H2D moves 0.625 B per residue) under 1 and 2; device calls
+ *                           with a pack kernel into the workspace under 2, and under 1 for
+ *                           batches of >= 2^25 residues; 0 = the probe packs ASCII itself
  *   KMA_OPT_HOST_THREADS    host calls: threads staging (copying / packing) the input
  *                           [0: min(16, cores)]; 1..64
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
@@ -282,7 +283,8 @@ int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
  * offsets[n_seq]; n_residues = offsets[n_seq] - offsets[0] (<= the workspace reservation);
  * d_tally (n_fid u32) is accumulated into, not cleared. Asynchronous on `stream`: one kernel
  * launch (annotate_kernel: each window probes the table where it stands, per-protein sets and
- * the vote in LDS), preceded by a pack kernel into the workspace under KMA_OPT_PACKED_INPUT.  */
+ * the vote in LDS), preceded by a pack kernel into the workspace under KMA_OPT_PACKED_INPUT
+ * (default: batches of >= 2^25 residues).                                                      */
 int kma_annotate_proteins_device(const kma_table* table, kma_workspace* ws,
                                  const uint8_t* d_residues, const uint64_t* d_offsets,
                                  uint32_t n_seq, uint64_t n_residues, int min_hits,

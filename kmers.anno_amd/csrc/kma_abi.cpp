@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -46,7 +47,7 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_DEFER: return v >= -1 && v <= 64;
     case KMA_OPT_HOST_PIECES: return v >= 0 && v <= 16;
     case KMA_OPT_HASH_SLICE: return v >= 0;
-    case KMA_OPT_PACKED_INPUT: return v == 0 || v == 1;
+    case KMA_OPT_PACKED_INPUT: return v >= 0 && v <= 2;
     case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
     default: return false;
   }
@@ -79,6 +80,89 @@ int forced_layout() { return (int)opt(KMA_OPT_LAYOUT); }
 size_t staging_threads() {
   const int64_t o = opt(KMA_OPT_HOST_THREADS);
   return o > 0 ? (size_t)o : std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// Library-wide pool of staging threads (grown on demand, never shrunk; threads sleep when idle).
+// run(n, width, fn) calls fn(0..n-1) on the calling thread plus up to width - 1 pool threads and
+// returns when every call has returned. Several host calls may run jobs at once (kma apply's
+// workers each stage their own batch): pool threads take the oldest job with free width, and a
+// caller always works on its own job, so every job finishes even when the pool is busy. Round 3
+// and early round 4 spawned threads per staging piece: a c5 host call spent milliseconds
+// creating ~120 threads, and pieces of 5 chunks kept 5 of 16 threads busy.
+class StagingPool {
+ public:
+  template <class F>
+  void run(uint64_t n, size_t width, F&& fn) {
+    width = std::max<size_t>(1, std::min<size_t>(width, n));
+    Job j;
+    j.n = n;
+    j.width = width;
+    j.call = [](void* f, uint64_t i) { (*static_cast<std::remove_reference_t<F>*>(f))(i); };
+    j.fn = (void*)&fn;
+    if (width > 1) {
+      std::lock_guard<std::mutex> g(mu_);
+      while (threads_.size() < width - 1 && threads_.size() < kMaxThreads)
+        threads_.emplace_back([this] { worker(); });
+      jobs_.push_back(&j);
+      cv_.notify_all();
+    }
+    drain(j);
+    if (width > 1) {
+      std::unique_lock<std::mutex> lk(mu_);
+      jobs_.erase(std::remove(jobs_.begin(), jobs_.end(), &j), jobs_.end());
+      done_cv_.wait(lk, [&] { return j.active == 0; });
+    }
+  }
+  ~StagingPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      cv_.notify_all();
+    }
+    for (auto& t : threads_) t.join();
+  }
+
+ private:
+  static constexpr size_t kMaxThreads = 63;
+  struct Job {
+    uint64_t n = 0;
+    size_t width = 1;
+    size_t active = 0;  // pool threads inside drain() (guarded by mu_)
+    std::atomic<uint64_t> next{0};
+    void (*call)(void*, uint64_t) = nullptr;
+    void* fn = nullptr;
+  };
+  static void drain(Job& j) {
+    for (uint64_t i; (i = j.next.fetch_add(1)) < j.n;) j.call(j.fn, i);
+  }
+  void worker() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      Job* j = nullptr;
+      cv_.wait(lk, [&] {
+        if (stop_) return true;
+        for (Job* c : jobs_)
+          if (c->active + 1 < c->width && c->next.load() < c->n) return (j = c) != nullptr;
+        return false;
+      });
+      if (stop_) return;
+      ++j->active;
+      lk.unlock();
+      drain(*j);
+      lk.lock();
+      if (--j->active == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<Job*> jobs_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
+StagingPool& staging_pool() {
+  static StagingPool* pool = new StagingPool();  // never destroyed: no join at process exit
+  return *pool;
 }
 }  // namespace
 
@@ -965,6 +1049,16 @@ uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
 // entry; stream residue `stream_first` = residue offsets[0]).
 enum class Input { kAscii, kPackOnDevice, kStream };
 
+// Device calls pack first under KMA_OPT_PACKED_INPUT = 2, or = 1 (the default) for batches of
+// at least 2^25 residues: the pack kernel costs a launch (~8 us at c2's 3M residues, where the
+// ASCII probe is 3 us faster in total) and pays off only at scale (c4 2.80 vs 2.83 ms, c5 even:
+// profiles/r04/ab_r04c.jsonl). Host calls pack under 1 and 2 (the H2D is the bound there).
+constexpr uint64_t kPackMinResidues = 1ull << 25;
+bool pack_on_device(uint64_t n_residues) {
+  const int64_t v = opt(KMA_OPT_PACKED_INPUT);
+  return v == 2 || (v == 1 && n_residues >= kPackMinResidues);
+}
+
 // The protein path on one replica (device buffers, asynchronous on s).
 int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws,
                          const uint8_t* d_residues, const uint64_t* d_offsets, uint32_t n_seq,
@@ -1024,75 +1118,51 @@ int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
 // Small inputs take one plain copy.
 hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size_t len,
                      int device, hipStream_t s) {
-  constexpr size_t kChunk = 8u << 20;
+  constexpr size_t kChunk = 2u << 20;
   const size_t n_chunks = (len + kChunk - 1) / kChunk;
   if (n_chunks <= 2) {
     std::memcpy(h_pinned, src, len);
     return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
   }
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t n_threads = std::min<size_t>({staging_threads(), hw, n_chunks});
-  std::atomic<size_t> next{0};
   std::atomic<int> err{(int)hipSuccess};
-  auto work = [&]() {
+  staging_pool().run(n_chunks, staging_threads(), [&](uint64_t i) {
     if (hipSetDevice(device) != hipSuccess) {
       err = (int)hipErrorInvalidDevice;
       return;
     }
-    for (size_t i; (i = next++) < n_chunks;) {
-      const size_t off = i * kChunk, n = std::min(kChunk, len - off);
-      std::memcpy(h_pinned + off, src + off, n);
-      const hipError_t e = hipMemcpyAsync(d_dst + off, h_pinned + off, n,
-                                          hipMemcpyHostToDevice, s);
-      if (e != hipSuccess) err = (int)e;
-    }
-  };
-  std::vector<std::thread> pool;
-  for (size_t i = 1; i < n_threads; ++i) pool.emplace_back(work);
-  work();
-  for (auto& th : pool) th.join();
+    const size_t off = i * kChunk, n = std::min(kChunk, len - off);
+    std::memcpy(h_pinned + off, src + off, n);
+    const hipError_t e = hipMemcpyAsync(d_dst + off, h_pinned + off, n, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) err = (int)e;
+  });
   return (hipError_t)err.load();
 }
 
 // The packed form of stage_h2d: stream groups [ga, gb) (64 residues, 40 bytes each) packed from
 // src (residue 64 ga onwards; residues past n_res read as no code) into the pinned buffer and
-// copied to d_stream, in chunks of 2^17 groups on up to 8 threads; `tail` extra zero bytes
-// (the kernel's read padding) follow the last group.
+// copied to d_stream, in chunks of 2^15 groups (2M residues) on the staging pool; `tail` extra
+// zero bytes (the kernel's read padding) follow the last group.
 hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* lut,
                           const uint8_t* residues, uint64_t n_res, uint64_t ga, uint64_t gb,
                           uint64_t tail, int device, hipStream_t s) {
-  constexpr uint64_t kChunkGroups = 1u << 17;
+  constexpr uint64_t kChunkGroups = 1u << 15;
   const uint64_t n_chunks = std::max<uint64_t>(1, (gb - ga + kChunkGroups - 1) / kChunkGroups);
-  auto chunk = [&](uint64_t i) -> hipError_t {
+  std::atomic<int> err{(int)hipSuccess};
+  auto chunk = [&](uint64_t i) {
+    if (n_chunks > 2 && hipSetDevice(device) != hipSuccess) {
+      err = (int)hipErrorInvalidDevice;
+      return;
+    }
     const uint64_t g0 = ga + i * kChunkGroups, g1 = std::min(gb, g0 + kChunkGroups);
     const uint64_t r0 = 64 * g0, r1 = std::min(64 * g1, n_res);
     const uint64_t bytes = 40 * (g1 - g0) + (g1 == gb ? tail : 0);
     kma::pack_residues_host(lut, residues + r0, r1 > r0 ? r1 - r0 : 0, h_stream + 40 * g0, bytes);
-    return bytes ? hipMemcpyAsync(d_stream + 40 * g0, h_stream + 40 * g0, bytes,
-                                  hipMemcpyHostToDevice, s)
-                 : hipSuccess;
+    if (!bytes) return;
+    const hipError_t e = hipMemcpyAsync(d_stream + 40 * g0, h_stream + 40 * g0, bytes,
+                                        hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) err = (int)e;
   };
-  if (n_chunks <= 2) {
-    for (uint64_t i = 0; i < n_chunks; ++i)
-      if (hipError_t e = chunk(i)) return e;
-    return hipSuccess;
-  }
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t n_threads = std::min<size_t>({staging_threads(), hw, n_chunks});
-  std::atomic<uint64_t> next{0};
-  std::atomic<int> err{(int)hipSuccess};
-  auto work = [&]() {
-    if (hipSetDevice(device) != hipSuccess) {
-      err = (int)hipErrorInvalidDevice;
-      return;
-    }
-    for (uint64_t i; (i = next++) < n_chunks;)
-      if (hipError_t e = chunk(i)) err = (int)e;
-  };
-  std::vector<std::thread> pool;
-  for (size_t i = 1; i < n_threads; ++i) pool.emplace_back(work);
-  work();
-  for (auto& th : pool) th.join();
+  staging_pool().run(n_chunks, n_chunks <= 2 ? 1 : staging_threads(), chunk);
   return (hipError_t)err.load();
 }
 
@@ -1355,7 +1425,7 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   return annotate_proteins_on(t, *r, ws, d_residues, d_offsets, n_seq, n_residues, min_hits,
                               flags, d_fid, d_count, d_status, d_tally, n_fid,
                               static_cast<hipStream_t>(stream),
-                              opt(KMA_OPT_PACKED_INPUT) ? Input::kPackOnDevice : Input::kAscii);
+                              pack_on_device(n_residues) ? Input::kPackOnDevice : Input::kAscii);
 }
 
 uint64_t kma_packed_bytes(uint64_t n_residues) { return kma::packed_bytes(n_residues); }

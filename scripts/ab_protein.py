@@ -5,7 +5,7 @@ around `steps` calls), so that the arms share the box, the table and the batch. 
 (workload, config, rep) on stdout. The library is whatever KMERANNO_LIB names (an older build's
 library compares kernels across commits: run the script once per library).
 
-  python scripts/ab_protein.py [--workloads c5,c4,c2] [--configs packed=1;packed=0] [--reps 2]
+  python scripts/ab_protein.py [--workloads c5,c4,c2] [--configs packed=2;packed=0] [--reps 2]
 """
 import argparse
 import json
@@ -39,7 +39,7 @@ def parse_config(text):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="c5,c4,c2")
-    ap.add_argument("--configs", default="packed=1;packed=0")
+    ap.add_argument("--configs", default="packed=2;packed=0")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--steps", type=int, default=20)
     args = ap.parse_args()

@@ -38,7 +38,7 @@ def test_options_set_get_validate_restore(native_lib):
     for o, v in k.OPT_DEFAULTS.items():
         assert k.get_option(o) == v
     for o, bad in ((k.OPT_LAYOUT, 5), (k.OPT_BLOCK_PROTEINS, 9), (k.OPT_DEFER, 65),
-                   (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 2),
+                   (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 3),
                    (k.OPT_HOST_THREADS, 65), (99, 0)):
         with pytest.raises(k.KmerAnnoError) as e:
             k.set_option(o, bad)

@@ -45,12 +45,13 @@ def path(request, monkeypatch):
 
 @pytest.fixture(params=["packed", "ascii"])
 def input_mode(request):
-    """The protein kernel's input: residues packed to 5 bits first (KMA_OPT_PACKED_INPUT = 1,
-    the default: on the host while staging, or by the pack kernel for device calls), or ASCII
-    packed by the probe itself through the LDS LUT (0)."""
+    """The protein kernel's input: residues packed to 5 bits first (KMA_OPT_PACKED_INPUT = 2:
+    on the host while staging, or by the pack kernel for device calls of any size; the default 1
+    packs device batches of >= 2^25 residues only), or ASCII packed by the probe itself through
+    the LDS LUT (0)."""
     import kmeranno
     kmeranno.load()
-    kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, 1 if request.param == "packed" else 0)
+    kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, 2 if request.param == "packed" else 0)
     return request.param
 
 
@@ -479,7 +480,13 @@ def test_workspace_timing(kma):
         for _ in range(2):
             kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
                                          *[o.data_ptr() for o in outs], 0, 0, stream)
-        calls, ph = ws.phases_read()  # the pack kernel, then the probe (KMA_OPT_PACKED_INPUT)
+        calls, ph = ws.phases_read()  # small batch, default option: the ASCII probe only
+        assert calls == 2 and list(ph) == ["annotate_kernel"]
+        kma.set_option(kma.OPT_PACKED_INPUT, 2)
+        for _ in range(2):
+            kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), n, n_res, 5, 0,
+                                         *[o.data_ptr() for o in outs], 0, 0, stream)
+        calls, ph = ws.phases_read()  # the pack kernel, then the probe (KMA_OPT_PACKED_INPUT 2)
         assert calls == 2 and list(ph) == ["pack_kernel", "annotate_kernel"]
         assert ph["annotate_kernel"] > 0 and ph["pack_kernel"] > 0
         kma.set_option(kma.OPT_PACKED_INPUT, 0)
