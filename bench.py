@@ -336,6 +336,37 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
     return out
 
 
+def link_rates(residues, n_res, dev):
+    """What bounds the host call: the pinned host -> device rate for the packed stream's bytes
+    (one copy, and 2 MiB copies as the staging pool issues them) and the host packer's rate on
+    one thread (kma_pack_residues)."""
+    n_bytes = kmeranno.packed_bytes(n_res)
+    src = torch.empty(n_bytes, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(n_bytes, dtype=torch.uint8, device=dev)
+    src.fill_(1)
+    out = {"packed_bytes": n_bytes}
+    for name, chunk in (("h2d_one_copy_GBps", n_bytes), ("h2d_2MiB_copies_GBps", 2 << 20)):
+        best = None
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for o in range(0, n_bytes, chunk):
+                dst[o:o + chunk].copy_(src[o:o + chunk], non_blocking=True)
+            b.record()
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b)
+            best = ms if best is None else min(best, ms)
+        out[name] = n_bytes / (best * 1e-3) / 1e9
+    n = min(n_res, 64 << 20)
+    buf = np.empty(kmeranno.packed_bytes(n), np.uint8)
+    lib = kmeranno.load()
+    t0 = time.perf_counter()
+    lib.kma_pack_residues(None, residues, n, buf, len(buf))
+    out["pack_1thread_GBps"] = n / (time.perf_counter() - t0) / 1e9
+    out["h2d_bound_ms"] = n_bytes / (out["h2d_one_copy_GBps"] * 1e9) * 1e3
+    return out
+
+
 def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
     """Roofline of the protein path's probe kernel (rank 0's shard, times max over ranks)."""
     packed = "pack_kernel" in ph
@@ -373,7 +404,8 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                          0, 0, sp)
 
     elapsed, gpu_ms, ph = timed(step, ws, args, world, stream, dev)
-    k_ms, rest_ms = ph["contigs_probe_kernel"], ph["scan_emit"]
+    # one kernel since round 4 (hits emitted by the probe); older libraries: + the emit pass
+    k_ms, rest_ms = ph["contigs_probe_kernel"], ph.get("scan_emit", 0.0)
     n_hits = int(d_nh.item())
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
@@ -392,8 +424,8 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                        "parallelism": f"genome-shard x{world}" + collective_note(args, world)},
             "seqs_per_s": n_contig * args.steps * world / elapsed,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "phases_ms": {"probe": k_ms, "scan_emit": rest_ms},
-            # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 8 B per staged hit
+            "phases_ms": {"probe": k_ms, **({"scan_emit": rest_ms} if "scan_emit" in ph else {})},
+            # 6-frame probe: one 64-B bucket per probed window, 1 B per base, 16 B per hit
             "roofline": roofline("probed windows x 64 B + bases + hits x 16 B", "c3",
                                  f"{kname} (6-frame translate + 2 probes per base)", k_ms,
                                  n_probe * BYTES_PER_LOOKUP + n_bases + 16 * n_hits,
@@ -726,7 +758,8 @@ def main():
                     "min(16, cores)",
                     "ms": ms, "lookups_per_s": n_win / (ms * 1e-3),
                     "seqs_per_s": n_seq / (ms * 1e-3), "kernel_ratio": ms / ph["annotate_kernel"],
-                    "ascii_staging_ms": ms_ascii}
+                    "ascii_staging_ms": ms_ascii,
+                    "link": link_rates(residues, n_res, dev)}
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(sig.keys, sig.fids, residues, offsets)
         if verify is not None:

@@ -21,8 +21,9 @@ from bench import K, MIN_HITS, kmeranno, synth  # noqa: E402
 
 
 def contigs_timeline():
-    """c3: contigs_probe_quad_kernel's blocks (256 positions each): clock 0 start, 1 tile
-    loaded + contigs found, 2 translated, 3 bucket loads issued, 4 matched, 5 end."""
+    """c3: contigs_probe_quad_kernel's blocks (512 positions each since round 4): clock 0 start,
+    1 tile loaded + contigs found, 2 translated, 3 bucket loads issued (last slice), 4 matched
+    (last slice), 5 look-back done, 7 records written (end)."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     sp = torch.cuda.current_stream().cuda_stream
@@ -42,14 +43,15 @@ def contigs_timeline():
                                          d_nh.data_ptr(), 0, 0, sp)
     torch.cuda.synchronize()
     lib = C.CDLL(os.environ["KMERANNO_LIB"])
-    nb = min((n_bases + 255) // 256, 65535)
     full = np.zeros(8 * 65536, np.uint64)
     assert lib.kma_debug_block_clock(full.ctypes.data_as(C.c_void_p), C.c_uint64(8 * 65536)) == 0
-    clk = full[:8 * nb].reshape(nb, 8)[:, :6].astype(np.int64)
+    rows = full.reshape(65536, 8)
+    nb = int((rows[:, 0] != 0).sum())  # blocks of the last launch (tile size from the build)
+    clk = rows[:nb][:, [0, 1, 2, 3, 4, 5, 7]].astype(np.int64)
     us = (clk - clk[:, 0].min()) * 10.0 / 1e3
     ph = np.diff(us, axis=1)
-    names = ["tile_and_contigs", "translate", "issue", "match", "compact_store"]
-    s, e = us[:, 0], us[:, 5]
+    names = ["tile_and_contigs", "translate", "slices_issue", "match", "lookback", "write"]
+    s, e = us[:, 0], us[:, 6]
     grid = np.linspace(0, e.max(), 41)
     return {"workload": "c3", "blocks": int(nb), "kernel_span_us": float(e.max()),
             "last_start_us": float(s.max()),
