@@ -363,7 +363,21 @@ def link_rates(residues, n_res, dev):
     t0 = time.perf_counter()
     lib.kma_pack_residues(None, residues, n, buf, len(buf))
     out["pack_1thread_GBps"] = n / (time.perf_counter() - t0) / 1e9
-    out["h2d_bound_ms"] = n_bytes / (out["h2d_one_copy_GBps"] * 1e9) * 1e3
+    # 8 MiB copies alternating over two / four streams (several DMA engines at once?)
+    for n_streams in (2, 4):
+        streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
+        best = None
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i, o in enumerate(range(0, n_bytes, 8 << 20)):
+                with torch.cuda.stream(streams[i % n_streams]):
+                    dst[o:o + (8 << 20)].copy_(src[o:o + (8 << 20)], non_blocking=True)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            best = ms if best is None else min(best, ms)
+        out[f"h2d_{n_streams}_streams_GBps"] = n_bytes / (best * 1e-3) / 1e9
+    out["h2d_bound_ms"] = n_bytes / (max(v for k, v in out.items() if k.startswith("h2d_")) * 1e9) * 1e3
     return out
 
 

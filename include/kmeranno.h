@@ -254,10 +254,11 @@ int kma_workspace_option_set(kma_workspace* ws, int option, int64_t value); /* s
  * synchronise on the recorded events (the last 256 calls) and clear the accumulators.
  *   _phases_read : the calls laid out like the last one (same entry point): their count, the
  *                  number of phases and each phase's summed milliseconds and name (static
- *                  strings): proteins {[pack_kernel,] annotate_kernel}; contigs
- *                  {contigs_probe_kernel} (one kernel since ABI 5: hits are emitted by the
- *                  probe).
- *   _timing_read : kernel_ms = every phase; rest_ms = 0 (ABI 4: the contigs' emit pass).     */
+ *                  strings): proteins {annotate_kernel}; contigs {contigs_probe_kernel,
+ *                  scan_emit}.
+ *   _timing_read : kernel_ms = proteins: every phase / contigs: the probe; rest_ms = contigs:
+ *                  the emit pass (offsets from the group sums the probe adds; the phase keeps
+ *                  its ABI-3 name scan_emit).                                                */
 #define KMA_MAX_PHASES 8
 int kma_workspace_timing(kma_workspace* ws, int enable);
 int kma_workspace_timing_read(kma_workspace* ws, uint32_t* n_calls, double* kernel_ms,
@@ -327,11 +328,9 @@ int kma_annotate_contigs(const kma_table* table, const uint8_t* dna, const uint6
  * d_dna readable for 64 bytes past the last base. Hits [0, cap) go to d_hits in canonical
  * order and *d_n_hits (device u64) receives the total, which may exceed cap (then the hits
  * past cap are dropped: compare and call again with a larger buffer). d_tally (n_contig x
- * n_fid u32, optional) is accumulated into. One kernel; never allocates or synchronises;
- * keeps no host state between calls (the workspace's device words carry a call counter), so a
- * call may be captured in a hipGraph and replayed. Calls on one workspace are ordered on one
- * stream. *d_n_hits = ~0 reports an internal stall (a probe block that waited ~seconds for its
- * predecessors' counts; hits not written).                                                   */
+ * n_fid u32, optional) is accumulated into. Never allocates or synchronises; keeps no host
+ * state between calls (the emit pass leaves the workspace's group sums zero), so a call may be
+ * captured in a hipGraph and replayed. Calls on one workspace are ordered on one stream.     */
 int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases);
 int kma_annotate_contigs_device(const kma_table* table, kma_workspace* ws, const uint8_t* d_dna,
                                 const uint64_t* d_offsets, uint32_t n_contig, uint64_t n_bases,

@@ -377,12 +377,15 @@ struct kma_workspace {
   uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
   uint8_t* d_packed = nullptr; // the call's residues packed (kma_internal.h packed_bytes)
   uint64_t res_cap = 0;        // residues per call
-  // 6-frame path (kma_workspace_reserve_contigs): the probe blocks' look-back status words
-  // (cblocks u64) followed by its control words (ContigArgs::ctl, 16 bytes). Calls keep their
-  // state on the device (a call counter the last block advances), none on the host, so calls
-  // may be graph-captured and replayed.
-  uint64_t* d_cstatus = nullptr;
-  uint64_t cblocks = 0;
+  // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
+  kma_hit* d_cstage = nullptr;
+  uint32_t* d_ccounts = nullptr;
+  // Emit-offset group sums (cgroups u64) and the emit pass's done counter (one u64 after
+  // them): zero between calls — the probe adds into the sums, the emit pass's last block
+  // zeroes both — so a call keeps no host state and may be graph-captured.
+  uint64_t* d_cprefix = nullptr;
+  uint64_t cgroups = 0;
+  bool cpending = false;  // a probe was set up whose emit pass has not been enqueued
   uint64_t contig_cap = 0;  // bases
   // Per-workspace overrides of KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER (kOptUnset: the default).
   int64_t opt_block_proteins = kOptUnset;
@@ -925,9 +928,11 @@ void free_protein_scratch(kma_workspace* ws) {
 }
 
 void free_contig_scratch(kma_workspace* ws) {
-  if (ws->d_cstatus) (void)hipFree(ws->d_cstatus);
-  ws->d_cstatus = nullptr;
-  ws->cblocks = 0;
+  for (void* p : {(void*)ws->d_cstage, (void*)ws->d_ccounts, (void*)ws->d_cprefix})
+    if (p) (void)hipFree(p);
+  ws->d_cstage = nullptr;
+  ws->d_ccounts = nullptr;
+  ws->d_cprefix = nullptr;
   ws->contig_cap = 0;
 }
 
@@ -953,9 +958,14 @@ int contig_args(const kma_table* t, const Replica& r, kma_workspace* ws, const u
   a.total_bases = n_bases;
   a.k = t->k;
   a.mlen = t->mlen;
-  a.status = ws->d_cstatus;
-  a.ctl = reinterpret_cast<uint32_t*>(ws->d_cstatus + ws->cblocks);
-  a.status_cap = ws->cblocks;
+  a.staging = ws->d_cstage;
+  a.block_counts = ws->d_ccounts;
+  // An earlier call failed between its probe and its emit: start clean, ordered on this
+  // call's stream (calls on one workspace are ordered on one stream, kmeranno.h).
+  if (ws->cpending) KMA_HIP(hipMemsetAsync(ws->d_cprefix, 0, (ws->cgroups + 1) * 8, s));
+  ws->cpending = true;
+  a.group_sum = ws->d_cprefix;
+  a.emit_done = reinterpret_cast<uint32_t*>(ws->d_cprefix + ws->cgroups);
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   codon_codes(code, a.codon_codes);
@@ -963,13 +973,16 @@ int contig_args(const kma_table* t, const Replica& r, kma_workspace* ws, const u
   return KMA_OK;
 }
 
-// The probe with its hit emission on s (count only when d_hits is null).
-int enqueue_contig_probe(kma::ContigArgs a, kma_hit* d_hits, uint64_t cap, uint64_t* d_n_hits,
-                         hipStream_t s) {
+// Canonical-order emission after the probe on s (whose atomics summed the block counts into
+// ws's group sums); the emit pass leaves the sums zero for the next call.
+int enqueue_contig_emit(kma_workspace* ws, kma::ContigArgs a, kma_hit* d_hits, uint64_t cap,
+                        uint64_t* d_n_hits, hipStream_t s) {
+  const uint64_t nb = contig_blocks(a.total_bases);
   a.out = d_hits;
   a.cap = d_hits ? cap : 0;
   a.n_hits = d_n_hits;
-  KMA_HIP(kma::launch_contigs_probe(a, contig_blocks(a.total_bases), s));
+  KMA_HIP(kma::launch_contigs_emit(a, nb, s));
+  ws->cpending = false;
   return KMA_OK;
 }
 
@@ -991,7 +1004,7 @@ struct PhaseClock {
 
 const char* const kDirectPhases[] = {"annotate_kernel"};
 const char* const kPackedPhases[] = {"pack_kernel", "annotate_kernel"};
-const char* const kContigPhases[] = {"contigs_probe_kernel"};
+const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 
 // Proteins per annotate_kernel block (KMA_BLOCK_PROTEINS=1..8 overrides, read per call): 6 for
 // batches of more than 4 resident waves of such blocks against a table larger than the Infinity
@@ -1251,14 +1264,18 @@ extern "C" {
 int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
   if (n_bases >= (1ull << 39)) return fail(KMA_E_INVALID, "more than 2^39 bases in one call");
-  if (ws->d_cstatus && n_bases <= ws->contig_cap) return KMA_OK;
+  if (ws->d_cstage && n_bases <= ws->contig_cap) return KMA_OK;
   DeviceScope ds(ws->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   free_contig_scratch(ws);
   const uint64_t nb = contig_blocks(n_bases);
-  KMA_HIP(hipMalloc(&ws->d_cstatus, (nb + 2) * 8));
-  KMA_HIP(hipMemset(ws->d_cstatus, 0, (nb + 2) * 8));
-  ws->cblocks = nb;
+  const uint64_t ng = (nb + kma::kScanGroup - 1) / kma::kScanGroup;
+  KMA_HIP(hipMalloc(&ws->d_cstage, nb * 2 * kma::kContigTile * sizeof(kma_hit)));
+  KMA_HIP(hipMalloc(&ws->d_ccounts, ng * kma::kScanGroup * 4));
+  KMA_HIP(hipMalloc(&ws->d_cprefix, (ng + 1) * 8));
+  KMA_HIP(hipMemset(ws->d_cprefix, 0, (ng + 1) * 8));
+  ws->cgroups = ng;
+  ws->cpending = false;
   ws->contig_cap = nb * kma::kContigTile;
   return KMA_OK;
 }
@@ -1514,11 +1531,14 @@ int kma_annotate_contigs_device(const kma_table* t, kma_workspace* ws, const uin
   if (int rc = contig_args(t, *r, ws, d_dna, d_offsets, n_contig, n_bases, code, d_tally, n_fid,
                            s, &a))
     return rc;
-  PhaseClock clk(ws, s, kContigPhases, 1);
+  PhaseClock clk(ws, s, kContigPhases, 2);
   KMA_HIP(clk.mark());
-  if (int rc = enqueue_contig_probe(a, d_hits, cap, d_n_hits, s)) return rc;
+  const uint64_t nb = contig_blocks(n_bases);
+  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
   KMA_HIP(clk.mark());
-  return KMA_OK;
+  const int rc = enqueue_contig_emit(ws, a, d_hits, cap, d_n_hits, s);
+  if (rc == KMA_OK) KMA_HIP(clk.mark());
+  return rc;
 }
 
 }  // extern "C"
@@ -1577,27 +1597,27 @@ int contig_shard(kma_table* t, const Replica& r, const uint8_t* dna, const uint6
     KMA_HIP(hipMemsetAsync(c->d_aux.p, 0, n_slots * 4, s));
     a.slot_count = c->d_aux.p;
     a.strict_pass = 1;  // count every table key's locations
-    uint64_t* const st = a.status;
-    a.status = nullptr;  // nothing is emitted in this pass
+    uint64_t* const gs = a.group_sum;
+    a.group_sum = nullptr;  // no emit follows this pass
     KMA_HIP(kma::launch_contigs_probe(a, nb, s));
-    a.status = st;
+    a.group_sum = gs;
     a.strict_pass = 2;  // keep keys with exactly one location
   }
+  KMA_HIP(kma::launch_contigs_probe(a, nb, s));
   if (!out_hits) {  // pass 1: count (and tally)
-    if (int rc = enqueue_contig_probe(a, nullptr, 0, d_n, s)) return rc;
+    if (int rc = enqueue_contig_emit(c->ws, a, nullptr, 0, d_n, s)) return rc;
     KMA_HIP(c->h_out.reserve(16 + tb));
     KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
     if (tb) KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, d_tally, tb, hipMemcpyDeviceToHost, s));
     KMA_HIP(hipStreamSynchronize(s));
     std::memcpy(n_hits, c->h_out.p, 8);
-    if (*n_hits == ~0ull) return fail(KMA_E_DEVICE, "6-frame probe: look-back timeout");
     if (tb) std::memcpy(tally, c->h_out.p + 16, tb);
     return KMA_OK;
   }
   // pass 2: emit into d_hits (sized by pass 1's count, passed in *n_hits)
   const uint64_t cap = *n_hits;
   KMA_HIP(c->d_hits.reserve(std::max<uint64_t>(cap, 1)));
-  if (int rc = enqueue_contig_probe(a, c->d_hits.p, cap, d_n, s)) return rc;
+  if (int rc = enqueue_contig_emit(c->ws, a, c->d_hits.p, cap, d_n, s)) return rc;
   KMA_HIP(c->h_out.reserve(16 + cap * sizeof(kma_hit)));
   KMA_HIP(hipMemcpyAsync(c->h_out.p, d_n, 8, hipMemcpyDeviceToHost, s));
   KMA_HIP(hipMemcpyAsync(c->h_out.p + 16, c->d_hits.p, cap * sizeof(kma_hit),

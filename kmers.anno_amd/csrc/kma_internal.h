@@ -351,20 +351,19 @@ struct ContigArgs {
   uint64_t total_bases;        // offsets[n_contig] - offsets[0] (< 2^39)
   int32_t k;
   int32_t mlen;
-  // Hit emission in one pass (decoupled look-back over the probe blocks): block b publishes
-  // its hit count in status[b], then its inclusive prefix once it has summed its predecessors'
-  // counts back to the nearest published prefix, and writes its records at their final
-  // positions. A status word is tag (22 bits) | flag (2 bits) | value (40 bits); the tag is
-  // derived from ctl[0], a call counter on the device that the call's last block advances
-  // (ctl[1] counts finished blocks), so a call leaves no state to reset and graph replays work.
-  uint64_t* status;            // >= n_blocks words (null: no emission, e.g. strict pass 1)
-  uint32_t* ctl;               // [call counter, blocks done, look-back timeouts, 0]
-  uint64_t status_cap;         // words in status (zeroed when the tag wraps)
+  kma_hit* staging;            // n_blocks x kContigTile*2 final hit records (block order)
+  uint32_t* block_counts;      // n_blocks (allocated in whole groups of kScanGroup)
+  uint64_t* group_sum;         // ceil(n_blocks / kScanGroup) group sums, zero before the probe
+                               // (which adds its block counts; null: no emit follows); the
+                               // emit pass leaves them zero again
+  uint32_t* emit_done;         // emit blocks done (zero before the emit; left zero)
+  uint32_t n_groups;           // emit pass (set by launch_contigs_emit)
+  uint32_t groups_scanned;     // emit pass: group_sum holds exclusive prefixes
   uint32_t* tally;             // may be null: n_contig x n_fid
   uint32_t n_fid;
-  kma_hit* out;                // hits [0, cap) in canonical order (null: count only)
+  kma_hit* out;                // emit pass: hits [0, cap) in canonical order
   uint64_t cap;
-  uint64_t* n_hits;            // total hits (also when > cap; ~0 on a look-back timeout)
+  uint64_t* n_hits;            // emit pass: total hits (also when > cap)
   // KmerFactory.Strict (peg join): pass 1 counts the locations of every table key
   // (strict_pass = 1: atomicAdd per hit into slot_count[slot id], nothing else is meaningful),
   // pass 2 keeps only hits whose key has exactly one location (strict_pass = 2).
@@ -390,6 +389,10 @@ constexpr int kContigPos = KMA_CONTIG_POS;
 constexpr int kContigSeq = KMA_CONTIG_SEQ;
 static_assert(kContigSeq == 1 || kContigPos == 1, "sequential slices take one position per lane");
 constexpr int kContigTile = 256 * kContigPos * kContigSeq;  // forward positions per block
+constexpr uint32_t kScanGroup = 256;  // probe blocks per emit-offset group sum
+// Up to this many groups (16 loads per lane, one round trip) an emit block sums the group sums
+// before its own; beyond, a one-block scan turns them into prefixes first.
+constexpr uint32_t kDirectGroups = 1024;
 
 // ---- the projector's proposal sweep (kma_proposals.hip) ----------------------------------------
 struct PropArgs {

@@ -5,9 +5,9 @@
 //                      probed in the table (the HashMap.get of ApplyKmerProcessor.java:130 for
 //                      every kmer of ProteinKmers at :123), per-protein distinct-key sets and
 //                      fid range in LDS, then the vote and min-hits threshold (:129-147).
-//   contigs_probe_quad_kernel  6-frame translation + window + probe + block compaction, hits
-//                      written in canonical order after a look-back over the blocks' counts
+//   contigs_probe_quad_kernel  6-frame translation + window + probe + block compaction
 //                      (KmerReference.java:157-203, KmerPosition.java:50-93)
+//   contigs_emit_kernel   canonical-order hit emission after a block-count scan
 //   peg_windows / singleton_flags / build_windows / signature_flags  table builders (A9, (f)1)
 //
 // Integer / byte work only: the bound is HBM (or Infinity-Cache) random access to 64-byte
@@ -157,9 +157,7 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 #ifdef KMA_BLOCK_CLOCK
 // Tuning builds only (make variant VNAME=clk VFLAGS=-DKMA_BLOCK_CLOCK, scripts/block_clock.py):
 // per block of the last protein launch, wall clock at 0 start, 1 records ready, 2 first step
-// matched, 3 steps done, 4 chain walks done, 5 end; 6 hardware ids; 7 steps. 6-frame probe:
-// 0 start, 1 tile loaded, 2 translated, 3 loads issued, 4 matched (last slice), 5 look-back
-// done, 7 end; 6 hardware ids.
+// matched, 3 steps done, 4 chain walks done, 5 end; 6 hardware ids; 7 steps.
 __device__ uint64_t g_block_clk[8 * 65536];
 #define KMA_CLK_SET(i, v)                                          \
   do {                                                             \
@@ -778,87 +776,6 @@ __device__ __forceinline__ uint32_t contig_of_wave(const uint64_t* __restrict__ 
   return lo;
 }
 
-// ---- one-pass hit emission of the 6-frame probe (decoupled look-back) ----------------------------
-// A block publishes its hit count (flag AGG) as soon as it has it, then sums its predecessors'
-// words back to the nearest inclusive prefix (flag INC), 64 blocks per poll (lane i reads block
-// p - i), and publishes its own inclusive prefix. Progress: a block waits only for lower blocks,
-// and the lowest unfinished block is resident (blocks reach the CUs of their XCD in index
-// order), so it never waits. A poll count bound turns a stall into an error instead of a hang:
-// the block counts a timeout, publishes a prefix so that its successors proceed, writes no
-// records, and the call's n_hits becomes ~0. Round 3 and early round 4 staged records per block
-// and copied them in a second kernel after a group-sum scan (c3: 20 us of 99).
-constexpr uint64_t kLbAgg = 1ull << 40, kLbInc = 2ull << 40, kLbValue = (1ull << 40) - 1;
-constexpr uint32_t kLbTags = (1u << 22) - 1;  // tags 1 .. 2^22 - 1 (0 = never written)
-constexpr uint32_t kLbMaxPolls = 1u << 22;
-
-__device__ __forceinline__ uint64_t lookback_tag(const ContigArgs& a) {
-  const uint32_t calls = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (uint64_t)(calls % kLbTags + 1u) << 42;
-}
-
-// Wave 0 of probe block b, `total` its hit count: the exclusive prefix (wave-uniform), or ~0 on
-// a timeout.
-__device__ uint64_t lookback_prefix(const ContigArgs& a, uint32_t b, uint64_t total) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t tag = lookback_tag(a);
-  if (lane == 0)
-    __hip_atomic_store(a.status + b, tag | (b == 0 ? kLbInc : kLbAgg) | total, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (b == 0) return 0;
-  uint64_t excl = 0;
-  int64_t p = (int64_t)b - 1;
-  for (uint32_t polls = 0;;) {
-    const int64_t idx = p - (int64_t)lane;
-    const uint64_t v = idx >= 0 ? __hip_atomic_load(a.status + idx, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                : tag | kLbInc;  // before block 0: prefix 0
-    const bool ready = (v & ~((1ull << 42) - 1)) == tag && (v & (kLbAgg | kLbInc)) != 0;
-    const uint64_t inc = __ballot(ready && (v & kLbInc));
-    const uint64_t wait = __ballot(!ready);
-    const uint64_t upto = inc ? ((inc & (0 - inc)) << 1) - 1 : ~0ull;  // lanes 0 .. first INC
-    if ((wait & upto) == 0) {
-      uint64_t x = (upto >> lane) & 1u ? (v & kLbValue) : 0u;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-      excl += x;
-      if (inc) break;
-      p -= 64;
-      continue;
-    }
-    if (++polls == kLbMaxPolls) {
-      if (lane == 0) {
-        __hip_atomic_fetch_add(a.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.status + b, tag | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return ~0ull;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (lane == 0)
-    __hip_atomic_store(a.status + b, tag | kLbInc | ((excl + total) & kLbValue), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  return excl;
-}
-
-// The call's last block (every other block has read the tag and published): a timeout turns
-// n_hits into ~0, the counters are reset and the call counter advances; when the tag wraps, every
-// status word is zeroed (words of calls 2^22 - 1 ago would otherwise carry the new tag).
-__device__ void lookback_finish(const ContigArgs& a) {
-  __shared__ uint32_t next;
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_load(a.ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      if (a.n_hits) *a.n_hits = ~0ull;
-      a.ctl[2] = 0;
-    }
-    a.ctl[1] = 0;
-    next = a.ctl[0] + 1u;
-    a.ctl[0] = next;
-  }
-  __syncthreads();
-  if (next % kLbTags == 0)
-    for (uint64_t i = threadIdx.x; i < a.status_cap; i += blockDim.x) a.status[i] = 0;
-}
-
 // Waves per SIMD of the 6-frame probe: 8 with one slice per block (64 VGPRs); the sequential
 // slices' loop carries a few more scalar and vector values (SGPR spills land in VGPR lanes) and
 // takes 7 to stay clear of scratch.
@@ -1060,55 +977,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
     if (lane == 0) wave_tot[h * kWavesPerBlock + wave] = (uint32_t)(__popcll(bp) + __popcll(bm));
   }
   __syncthreads();
-  // The block's place in the call's hits: its count published, its predecessors' summed by
-  // look-back (wave 0), then the records written at their final positions.
-  __shared__ uint64_t lb_excl;
-  __shared__ uint32_t lb_last;
+  // Staged records are the final kma_hit (the emit pass only copies them): contig, left =
+  // KmerPosition.calcLeft, fid, strand and frame (KmerPosition.java:50-93).
   uint32_t total = 0;
-  for (int i = 0; i < CP * kWavesPerBlock; ++i) total += wave_tot[i];
-  if (a.status && wave == 0) {
-    const uint64_t e = lookback_prefix(a, blockIdx.x, total);
-    if (lane == 0) {
-      lb_excl = e;
-      if (a.n_hits && blockIdx.x == gridDim.x - 1) *a.n_hits = e == ~0ull ? e : e + total;
-    }
-  }
-  __syncthreads();
-  KMA_CLK(5);  // look-back done
-  // Records are the final kma_hit: contig, left = KmerPosition.calcLeft, fid, strand and frame
-  // (KmerPosition.java:50-93); those past cap are dropped (the caller compares n_hits with cap).
-  const uint64_t first = a.status ? lb_excl : ~0ull;
-  uint4* out = reinterpret_cast<uint4*>(a.out);
-  const uint64_t cap = out && first != ~0ull ? a.cap : 0;
-  uint32_t run = 0;
+  uint4* st = reinterpret_cast<uint4*>(a.staging) + (uint64_t)blockIdx.x * (2 * kContigTile);
 #pragma unroll 1
   for (int h = 0; h < CP; ++h) {
     const uint32_t v0 = xv[h][0][t], v1 = xv[h][1][t];
     const uint64_t bp = __ballot(v0 != 0u), bm = __ballot(v1 != 0u);
-    uint64_t o = first + run + popc_below(bp) + popc_below(bm);
+    uint32_t o = total + popc_below(bp) + popc_below(bm);
     for (int w = 0; w < kWavesPerBlock; ++w) {
       if (w < wave) o += wave_tot[h * kWavesPerBlock + w];
-      run += wave_tot[h * kWavesPerBlock + w];
+      total += wave_tot[h * kWavesPerBlock + w];
     }
-    if ((v0 | v1) && first < cap) {  // (hits only at positions inside a contig)
+    if (v0 | v1) {  // hits only at positions inside a contig (g < end)
       uint32_t c;
       int64_t x, len;
       locate(t + 256u * h, c, x, len);
       const uint32_t left = (uint32_t)(x + 1);
-      if (v0 && o < cap) out[o] = make_uint4(c, left, v0 - 1u, '+' | (uint32_t)(x % 3 + 1) << 8);
-      o += v0 != 0u;
-      if (v1 && o < cap)
-        out[o] = make_uint4(c, left, v1 - 1u, '-' | (uint32_t)((len - 3 * K - x) % 3 + 1) << 8);
+      if (v0) st[o++] = make_uint4(c, left, v0 - 1u, '+' | (uint32_t)(x % 3 + 1) << 8);
+      if (v1) st[o] = make_uint4(c, left, v1 - 1u, '-' | (uint32_t)((len - 3 * K - x) % 3 + 1) << 8);
     }
   }
-  if (a.status) {  // the call's last block to finish advances the call counter
-    if (t == 0)
-      lb_last = __hip_atomic_fetch_add(a.ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                gridDim.x - 1;
-    __syncthreads();
-    if (lb_last) lookback_finish(a);
+  if (t == 0) {
+    a.block_counts[blockIdx.x] = total;
+    // the emit pass's group sums (zeroed by the previous emit pass on this workspace)
+    if (a.group_sum && total)
+      __hip_atomic_fetch_add(a.group_sum + blockIdx.x / kScanGroup, (uint64_t)total,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  KMA_CLK(7);  // records written
+  KMA_CLK(5);
   KMA_CLK_HW();
 }
 
@@ -1233,6 +1131,103 @@ __global__ __launch_bounds__(256) void sig_clear_kernel(const uint64_t* __restri
     if (k[i] == 0) continue;
     const uint32_t h = run[i], t = tags[i];
     if (t == kBuildNeg || t != tags[h]) flags[h] = 0;  // every writer stores 0
+  }
+}
+
+// Exclusive prefix of block b's hit count (wave 0 of the emit block; wave-uniform result): the
+// group sums of the groups before b's (kScanGroup probe blocks each, summed by the probe's
+// atomics; every load issued at once: one round trip for up to 64 groups) — or, for calls of
+// more than kDirectGroups groups, the exclusive group prefix contigs_group_scan_kernel left in
+// place of the sums (one load) — plus the counts before b in its group.
+__device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b) {
+  const uint32_t lane = threadIdx.x & 63, g = b / kScanGroup;
+  uint64_t s = 0;
+  if (a.groups_scanned) {
+    if (lane == 0) s = a.group_sum[g];
+  } else {
+    for (uint32_t i = lane; i < g; i += 64) s += a.group_sum[i];
+  }
+  const uint32_t c0 = g * kScanGroup + 4u * lane;  // counts are allocated in whole groups
+  if (c0 < b) {
+    const uint4 v = *reinterpret_cast<const uint4*>(a.block_counts + c0);
+    s += (uint64_t)v.x + (c0 + 1 < b ? v.y : 0u) + (c0 + 2 < b ? v.z : 0u) +
+         (c0 + 3 < b ? v.w : 0u);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  return s;
+}
+
+// Calls of more than kDirectGroups groups (> 67M bases): one block turns the group sums into
+// exclusive prefixes in place, so an emit block reads one value instead of summing every group
+// before its own (which grows as blocks x groups: ~2e9 loads at 1 Gbp).
+__global__ __launch_bounds__(1024) void contigs_group_scan_kernel(uint64_t* sums, uint32_t n) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x, per = (n + 1023) / 1024;
+  const uint64_t lo = (uint64_t)t * per, hi = lo + per < n ? lo + per : n;
+  uint64_t s = 0;
+  for (uint64_t i = lo; i < hi; ++i) s += sums[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the parts
+    const uint64_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = t ? part[t - 1] : 0u;
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t x = sums[i];
+    sums[i] = run;
+    run += x;
+  }
+}
+
+// Emit pass: an emit block takes kEmitSpan consecutive probe blocks; probe block b's staged
+// records go to out[prefix[b] ..], those past `cap` are dropped; the last emit block publishes
+// the total (the caller compares it with cap). The call leaves no state behind: every emit
+// block counts itself done (one agent-scope atomic, issued once its offsets are read) and the
+// block that finishes last zeroes the group sums and the counter for the next call (so calls
+// on one workspace may be graph-captured and replayed). Measured alternatives for the offsets
+// (c3, profiles/r03_ab/): a library two-kernel scan ~10 us; a ticket letting the probe's last
+// block scan, 0.6 ms (20k atomics on one address serialize); a one-block scan kernel, ~18 us (a
+// single CU's dependent round trips); a group-sum kernel between probe and emit, and one emit
+// block per probe block (12.5 us for c3's 19.5k blocks of ~9 hits).
+constexpr uint32_t kEmitSpan = 16;
+__global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_t n_blocks) {
+  __shared__ uint64_t pre[kEmitSpan];
+  __shared__ uint32_t cnt[kEmitSpan];
+  __shared__ uint32_t last;
+  const uint32_t b0 = blockIdx.x * kEmitSpan, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (wave == 0) {
+    const uint32_t c = lane < kEmitSpan && b0 + lane < n_blocks ? a.block_counts[b0 + lane] : 0u;
+    const uint64_t base = emit_offset(a, b0);
+    uint64_t inc = c;  // inclusive scan over the span's counts (lanes < kEmitSpan)
+#pragma unroll
+    for (int d = 1; d < (int)kEmitSpan; d <<= 1) {
+      const uint64_t v = __shfl_up(inc, d, 64);
+      inc += lane >= (uint32_t)d ? v : 0u;
+    }
+    if (lane < kEmitSpan) {
+      pre[lane] = base + inc - c;
+      cnt[lane] = c;
+    }
+    if (blockIdx.x == gridDim.x - 1 && lane == kEmitSpan - 1) *a.n_hits = base + inc;
+  }
+  __syncthreads();
+  if (t == 0)  // this block's reads of the group sums are done (their values are in pre[])
+    last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_ACQ_REL,
+                                  __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  uint4* out = reinterpret_cast<uint4*>(a.out);
+  for (uint32_t i = wave; i < kEmitSpan && b0 + i < n_blocks; i += kWavesPerBlock) {
+    const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)(b0 + i) * (2 * kContigTile);
+    const uint64_t o = pre[i];
+    for (uint32_t r = lane; r < cnt[i] && o + r < a.cap; r += 64) out[o + r] = st[r];
+  }
+  __syncthreads();
+  if (last) {  // every other emit block has read its offsets: clean up for the next call
+    for (uint32_t i = t; i < a.n_groups; i += 256) a.group_sum[i] = 0;
+    if (t == 0) *a.emit_done = 0;
   }
 }
 
@@ -1444,6 +1439,20 @@ hipError_t launch_signature_flags(const uint64_t* keys, const uint32_t* tags, ui
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(sig_clear_kernel, dim3(grid_for(n)), dim3(256), 0, stream, keys, tags, run,
                      n, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_contigs_emit(const ContigArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  ContigArgs e = a;
+  e.n_groups = (uint32_t)((n_blocks + kScanGroup - 1) / kScanGroup);
+  e.groups_scanned = e.n_groups > kDirectGroups;
+  if (e.groups_scanned) {
+    hipLaunchKernelGGL(contigs_group_scan_kernel, dim3(1), dim3(1024), 0, stream, e.group_sum,
+                       e.n_groups);
+    if (hipError_t err = hipGetLastError()) return err;
+  }
+  const unsigned g = (unsigned)((n_blocks + kEmitSpan - 1) / kEmitSpan);
+  hipLaunchKernelGGL(contigs_emit_kernel, dim3(g), dim3(256), 0, stream, e, (uint32_t)n_blocks);
   return hipGetLastError();
 }
 

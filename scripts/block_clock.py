@@ -23,7 +23,7 @@ from bench import K, MIN_HITS, kmeranno, synth  # noqa: E402
 def contigs_timeline():
     """c3: contigs_probe_quad_kernel's blocks (512 positions each since round 4): clock 0 start,
     1 tile loaded + contigs found, 2 translated, 3 bucket loads issued (last slice), 4 matched
-    (last slice), 5 look-back done, 7 records written (end)."""
+    (last slice), 5 end (records staged, block count added)."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     sp = torch.cuda.current_stream().cuda_stream
@@ -47,11 +47,11 @@ def contigs_timeline():
     assert lib.kma_debug_block_clock(full.ctypes.data_as(C.c_void_p), C.c_uint64(8 * 65536)) == 0
     rows = full.reshape(65536, 8)
     nb = int((rows[:, 0] != 0).sum())  # blocks of the last launch (tile size from the build)
-    clk = rows[:nb][:, [0, 1, 2, 3, 4, 5, 7]].astype(np.int64)
+    clk = rows[:nb][:, :6].astype(np.int64)
     us = (clk - clk[:, 0].min()) * 10.0 / 1e3
     ph = np.diff(us, axis=1)
-    names = ["tile_and_contigs", "translate", "slices_issue", "match", "lookback", "write"]
-    s, e = us[:, 0], us[:, 6]
+    names = ["tile_and_contigs", "translate", "slices_issue", "match", "compact_store"]
+    s, e = us[:, 0], us[:, 5]
     grid = np.linspace(0, e.max(), 41)
     return {"workload": "c3", "blocks": int(nb), "kernel_span_us": float(e.max()),
             "last_start_us": float(s.max()),

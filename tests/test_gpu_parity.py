@@ -552,10 +552,10 @@ def test_contigs_device_api_planted_genome(kma, oracle_c):
 
 
 def test_contigs_device_graph_capture_replay(kma, oracle_c):
-    """kma_annotate_contigs_device keeps no host state between calls (the look-back's call
-    counter lives on the device and the call's last block advances it), so one call captured in
-    a hipGraph and replayed several times gives the oracle's hits and total every time, and the
-    tally grows by one call's worth per replay."""
+    """kma_annotate_contigs_device keeps no host state between calls (the emit pass's last
+    block zeroes the group sums the probe added into), so one call captured in a hipGraph and
+    replayed several times gives the oracle's hits and total every time, and the tally grows by
+    one call's worth per replay."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(300_000, 5, 57, table_size=200_000, n_fid=400)
@@ -600,9 +600,10 @@ def test_contigs_device_graph_capture_replay(kma, oracle_c):
 
 
 def test_contigs_device_many_groups_scanned(kma):
-    """A 140 Mbp device call (273k probe blocks: look-backs across many blocks; round 3's emit
-    pass scanned its group sums above 134 Mbp) equals the same genome cut into 70 calls, hit for
-    hit after re-basing, with the same total; then the whole call again on the same workspace."""
+    """A device call of more than kDirectGroups x 256 probe blocks (> 134M bases at 512
+    positions per block: the emit pass scans the group sums first instead of summing them per
+    block) equals the same genome cut into calls below that size, hit for hit after re-basing,
+    with the same total; then the whole call again on the same workspace."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(2_000_000, 8, 77, table_size=300_000, n_fid=300)
@@ -652,8 +653,8 @@ def test_contigs_device_many_groups_scanned(kma):
 
 def test_contigs_device_repeated_calls_of_different_sizes(kma, oracle_c):
     """One workspace, calls alternating between a whole genome and a prefix of its contigs (a
-    different number of probe blocks): a call must not take a status word of an earlier,
-    larger call as its predecessor's (status words are tagged with the call counter)."""
+    different number of emit-offset groups): every call must start from clean group sums
+    whatever the size of the call before it (the emit pass of each call zeroes them)."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(400_000, 8, 41, table_size=200_000, n_fid=500)
