@@ -413,7 +413,9 @@ constexpr int kMaxPieces = 16;  // host protein calls: H2D / kernel pipeline dep
 struct HostCtx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t copy = nullptr;            // H2D of piece i + 1 under the kernel of piece i
+  // H2D of piece i + 1 under the kernel of piece i, pieces alternating over two copy streams
+  // (two DMA engines: 57 vs 50 GB/s for c5's packed stream, profiles/r04/link_r04g.json)
+  hipStream_t copy[2] = {};
   hipEvent_t piece_ready[kMaxPieces] = {};
   kma_workspace* ws = nullptr;
   Grow<uint8_t> d_in;     // residues / DNA (+ padding)
@@ -448,7 +450,8 @@ void destroy_ctx(HostCtx* c) {
   DeviceScope ds(c->device);
   if (c->ws) kma_workspace_destroy(c->ws);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->copy) (void)hipStreamDestroy(c->copy);
+  for (hipStream_t cs : c->copy)
+    if (cs) (void)hipStreamDestroy(cs);
   for (hipEvent_t e : c->piece_ready)
     if (e) (void)hipEventDestroy(e);
   c->d_in.release();
@@ -477,7 +480,8 @@ int acquire_ctx(kma_table* t, int device, HostCtx** out) {
   HostCtx* c = new HostCtx();
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  for (hipStream_t& cs : c->copy)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
   for (int i = 0; i < kMaxPieces && e == hipSuccess; ++i)
     e = hipEventCreateWithFlags(&c->piece_ready[i], hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -502,7 +506,7 @@ struct CtxGuard {
     if (!c) return;
     // A call that failed after queueing work returns early: let the context's copies and
     // kernels drain before the next call reuses its pinned and device buffers.
-    (void)hipStreamSynchronize(c->copy);
+    for (hipStream_t cs : c->copy) (void)hipStreamSynchronize(cs);
     (void)hipStreamSynchronize(c->stream);
     release_ctx(t, c);
   }
@@ -1112,58 +1116,43 @@ int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
 }
 
 // One shard [lo, hi) of a host protein call on replica r (host buffers, synchronous).
-// Host bytes -> pinned staging -> device, pipelined: `len` bytes are cut into 8 MiB chunks;
-// up to 8 threads copy chunks into the pinned buffer and queue each chunk's DMA on `s` as soon
-// as it is staged, so the copies into pinned memory overlap each other and the transfers.
-// Small inputs take one plain copy.
+// Host bytes -> pinned staging -> device, pipelined: the input is cut into pieces of whole
+// proteins; the staging pool fills piece i's part of the pinned buffer (copying or packing in
+// 2 MiB chunks) and ONE copy per piece goes on the copy stream, so piece i + 1 is staged while
+// piece i's copy and kernel run. One large copy per piece: r04g's trace of 153 chunk-sized
+// copies (c5) kept the DMA engine idle a quarter of the time (profiles/r04/e2e_trace_r04g.json).
 hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size_t len,
                      int device, hipStream_t s) {
   constexpr size_t kChunk = 2u << 20;
   const size_t n_chunks = (len + kChunk - 1) / kChunk;
-  if (n_chunks <= 2) {
-    std::memcpy(h_pinned, src, len);
-    return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
-  }
-  std::atomic<int> err{(int)hipSuccess};
   staging_pool().run(n_chunks, staging_threads(), [&](uint64_t i) {
-    if (hipSetDevice(device) != hipSuccess) {
-      err = (int)hipErrorInvalidDevice;
-      return;
-    }
-    const size_t off = i * kChunk, n = std::min(kChunk, len - off);
-    std::memcpy(h_pinned + off, src + off, n);
-    const hipError_t e = hipMemcpyAsync(d_dst + off, h_pinned + off, n, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) err = (int)e;
+    const size_t off = i * kChunk;
+    std::memcpy(h_pinned + off, src + off, std::min(kChunk, len - off));
   });
-  return (hipError_t)err.load();
+  (void)device;
+  return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
 }
 
 // The packed form of stage_h2d: stream groups [ga, gb) (64 residues, 40 bytes each) packed from
-// src (residue 64 ga onwards; residues past n_res read as no code) into the pinned buffer and
-// copied to d_stream, in chunks of 2^15 groups (2M residues) on the staging pool; `tail` extra
-// zero bytes (the kernel's read padding) follow the last group.
+// src (residue 64 ga onwards; residues past n_res read as no code) into the pinned buffer in
+// chunks of 2^15 groups (2M residues) on the staging pool, then copied to d_stream in one
+// copy; `tail` extra zero bytes (the kernel's read padding) follow the last group.
 hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* lut,
                           const uint8_t* residues, uint64_t n_res, uint64_t ga, uint64_t gb,
                           uint64_t tail, int device, hipStream_t s) {
   constexpr uint64_t kChunkGroups = 1u << 15;
   const uint64_t n_chunks = std::max<uint64_t>(1, (gb - ga + kChunkGroups - 1) / kChunkGroups);
-  std::atomic<int> err{(int)hipSuccess};
-  auto chunk = [&](uint64_t i) {
-    if (n_chunks > 2 && hipSetDevice(device) != hipSuccess) {
-      err = (int)hipErrorInvalidDevice;
-      return;
-    }
+  staging_pool().run(n_chunks, staging_threads(), [&](uint64_t i) {
     const uint64_t g0 = ga + i * kChunkGroups, g1 = std::min(gb, g0 + kChunkGroups);
     const uint64_t r0 = 64 * g0, r1 = std::min(64 * g1, n_res);
     const uint64_t bytes = 40 * (g1 - g0) + (g1 == gb ? tail : 0);
     kma::pack_residues_host(lut, residues + r0, r1 > r0 ? r1 - r0 : 0, h_stream + 40 * g0, bytes);
-    if (!bytes) return;
-    const hipError_t e = hipMemcpyAsync(d_stream + 40 * g0, h_stream + 40 * g0, bytes,
-                                        hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) err = (int)e;
-  };
-  staging_pool().run(n_chunks, n_chunks <= 2 ? 1 : staging_threads(), chunk);
-  return (hipError_t)err.load();
+  });
+  (void)device;
+  const uint64_t bytes = 40 * (gb - ga) + tail;
+  return bytes ? hipMemcpyAsync(d_stream + 40 * ga, h_stream + 40 * ga, bytes,
+                                hipMemcpyHostToDevice, s)
+               : hipSuccess;
 }
 
 int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
@@ -1195,19 +1184,20 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   KMA_HIP(c->h_out.reserve(out_bytes));
   if (int rc = kma_workspace_reserve_batch(c->ws, nres, n)) return rc;
   // Stage: rebased offsets, then the residues (and, with the last piece, their zero padding)
-  // in pieces of whole proteins, in one pinned buffer. Copies go on the copy stream; the
-  // kernel of piece i waits for piece i's event on the compute stream, so the staging and
-  // transfer of piece i + 1 run under the kernel of piece i (pieces of >= kPieceBytes residues,
+  // in pieces of whole proteins, in one pinned buffer. Piece i's copy goes on copy stream
+  // i % 2 (the offsets with piece 0); the kernel of piece i waits for piece i's event on the
+  // compute stream, so the staging and transfer of piece i + 1 run under the kernel of piece i,
+  // and two pieces' copies may run at once on two DMA engines (pieces of >= kPieceBytes residues,
   // at most KMA_HOST_PIECES (default 8, <= kMaxPieces; read per call); a small call is one
   // piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (profiles/r02r_host_pipeline/).
   constexpr uint64_t kPieceBytes = 16ull << 20;
   const int64_t po = opt(KMA_OPT_HOST_PIECES);
   const uint64_t max_pieces = po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : 8;
   uint8_t* hin = c->h_in.p;
-  hipStream_t s = c->stream, cs = c->copy;
+  hipStream_t s = c->stream;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
   for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
-  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, cs));
+  KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, c->copy[0]));
   uint8_t* dout = c->d_out.p;
   int32_t* d_fid = reinterpret_cast<int32_t*>(dout);
   int32_t* d_cnt = d_fid + n;
@@ -1218,6 +1208,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   uint32_t pa = 0;  // first protein of the piece (relative to lo)
   uint64_t ga = 0;  // packed: first stream group the piece stages
   for (int i = 0; i < n_pieces; ++i) {
+    hipStream_t cs = c->copy[i & 1];
     uint32_t pb = n;
     if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
       const uint64_t target = nres * (uint64_t)(i + 1) / n_pieces;

@@ -45,7 +45,7 @@ def main():
         ev.append(("d2h" if "DEVICE_TO_HOST" in d.upper() or "D2H" in d.upper() else
                    "h2d" if "HOST_TO_DEVICE" in d.upper() or "H2D" in d.upper() else d,
                    int(col(r, "Start_Timestamp")), int(col(r, "End_Timestamp")),
-                   int(col(r, "Bytes", "Size", "Copy_Bytes") or 0)))
+                   int(r.get("Bytes") or r.get("Size") or 0)))
     for r in rows(root + "/**/*kernel_trace.csv"):
         ev.append(("kernel:" + col(r, "Kernel_Name")[:40], int(col(r, "Start_Timestamp")),
                    int(col(r, "End_Timestamp")), 0))
@@ -81,6 +81,10 @@ def main():
                         "last_end_ms": (max(b for _, b in kall) - t0) / 1e6},
             "overlap_ms": both / 1e6,
             "d2h": [((a - t0) / 1e6, (b - a) / 1e6, n) for k, a, b, n in c if k == "d2h"][:4],
+            "h2d_ms_each": sorted(round((b - a) / 1e6, 4) for a, b in h2d)[::max(1, len(h2d) // 8)],
+            "kernel_ms_each": [round((b - a) / 1e6, 4) for a, b in sorted(ker)],
+            "timeline": [(k[:22], round((a - t0) / 1e6, 3), round((b - t0) / 1e6, 3))
+                         for k, a, b, _ in c if k != "h2d"][:40],
         }))
 
 
