@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -1155,12 +1156,25 @@ hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* l
                : hipSuccess;
 }
 
+// Host-side phase times of the last host protein shard call (kma_debug_host_profile, for the
+// host-call measurements in scripts/e2e_host.py): ms in setup (context, reservations, offsets),
+// staging (packing / copying into pinned memory and queueing the copies), launches, the final
+// wait for the stream, the output copies, and the whole call.
+std::mutex g_prof_mu;
+double g_prof[6] = {};
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point a) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - a).count();
+}
+
 int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                   const uint64_t* offsets, uint32_t lo, uint32_t hi, int min_hits,
                   uint32_t flags, int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                   uint32_t* tally, uint32_t n_fid) {
   const uint32_t n = hi - lo;
   if (n == 0) return KMA_OK;
+  const Clock::time_point t_call = Clock::now();
+  double t_stage = 0, t_launch = 0;
   const uint64_t base = offsets[lo], nres = offsets[hi] - base;
   if (nres > kMaxResidues)
     return fail(KMA_E_INVALID, "%llu residues in one device call (limit 2^32 - 128)",
@@ -1207,8 +1221,10 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   const int n_pieces = (int)std::max<uint64_t>(1, std::min<uint64_t>(max_pieces, nres / kPieceBytes));
   uint32_t pa = 0;  // first protein of the piece (relative to lo)
   uint64_t ga = 0;  // packed: first stream group the piece stages
+  const double t_setup = ms_since(t_call);
   for (int i = 0; i < n_pieces; ++i) {
     hipStream_t cs = c->copy[i & 1];
+    const Clock::time_point t_piece = Clock::now();
     uint32_t pb = n;
     if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
       const uint64_t target = nres * (uint64_t)(i + 1) / n_pieces;
@@ -1229,6 +1245,8 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
       }
     }
     KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
+    const Clock::time_point t_staged = Clock::now();
+    t_stage += std::chrono::duration<double, std::milli>(t_staged - t_piece).count();
     KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
     if (pb > pa)
       if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + pa, pb - pa,
@@ -1236,21 +1254,38 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                                         d_cnt + pa, d_st + pa, d_tally, n_fid, s,
                                         packed ? Input::kStream : Input::kAscii, hoff[pa]))
         return rc;
+    t_launch += ms_since(t_staged);
     pa = pb;
   }
   KMA_HIP(hipMemcpyAsync(c->h_out.p, dout, out_bytes - 16, hipMemcpyDeviceToHost, s));
+  const Clock::time_point t_w = Clock::now();
   KMA_HIP(hipStreamSynchronize(s));
+  const double t_wait = ms_since(t_w);
+  const Clock::time_point t_o = Clock::now();
   const uint8_t* hout = c->h_out.p;
   std::memcpy(out_fid + lo, hout, n * 4ull);
   std::memcpy(out_count + lo, hout + n * 4ull, n * 4ull);
   const uint8_t* ht = hout + n * 8ull;
   std::memcpy(out_status + lo, ht + (tally ? n_fid * 4ull : 0), n);
   if (tally) std::memcpy(tally, ht, n_fid * 4ull);
+  {
+    const double p[6] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o), ms_since(t_call)};
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    std::copy(p, p + 6, g_prof);
+  }
   return KMA_OK;
 }
 }  // namespace
 
 extern "C" {
+
+// Not in kmeranno.h: measurement hook (see g_prof).
+int kma_debug_host_profile(double* out, int n) {
+  if (!out || n < 0) return KMA_E_INVALID;
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  std::copy(g_prof, g_prof + std::min(n, 6), out);
+  return KMA_OK;
+}
 
 int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");

@@ -675,7 +675,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(protein_occ
   __shared__ ProteinSmem<P> sm;
   KMA_CLK(0);
   const int t = threadIdx.x;
-  if (!Packed) sm.lut[t] = a.lut[t];  // read after annotate_block's first barrier
+  // The ASCII kernel's LUT: loaded now, stored to LDS once the first residue loads are issued
+  // (its store right here made the block wait for it before loading the offsets: one more
+  // dependent round trip per block). Read after annotate_block's first barrier.
+  const uint8_t lut_b = Packed ? 0 : a.lut[t];
   // Two-pass grid (defer_below > 0): blocks [0, n_groups) annotate the long groups, blocks
   // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
   // one (blocks are dispatched in index order); a block whose group is the other pass's exits
@@ -687,6 +690,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(protein_occ
   const uint32_t b = blockIdx.x - (second ? a.n_groups : 0u);
   head_offsets(a, a.defer_below ? b : xcd_group(b, a.n_groups), h);
   head_residues<kProbeWin, Packed>(a, h, lane_window(t), ww);
+  if (!Packed) sm.lut[t] = lut_b;
   annotate_block<K, M, P, Packed>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
   KMA_CLK(5);
   KMA_CLK_HW();
@@ -807,6 +811,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
   const uint64_t r0 = (uint64_t)blockIdx.x * kContigTile;
   const uint32_t nb = a.n_buckets;
   KMA_CLK(0);
+  // The tile's DNA bytes: every load issued before the contig search below, so that their
+  // round trip overlaps the offsets' (as a strided loop of load, wait, store they took three
+  // dependent trips: ~3.8 us of a ~12 us block, profiles/r04/clock_c3_r04g.json).
+  constexpr int kTileIters = (kSpan + 255) / 256;
+  uint8_t tb[kTileIters];
+#pragma unroll
+  for (int j = 0; j < kTileIters; ++j) {
+    const int i = t + 256 * j;
+    const uint64_t g = base + r0 + i;
+    tb[j] = i < kSpan && g < end ? a.dna[g] : (uint8_t)'N';
+  }
   if (wave == 3) codon[lane] = a.codon_codes[lane];  // LDS copy of the kernel-argument table
   if (a.n_contig < (uint32_t)kOffCache) {
     // Every offset fits the cache: wave 0 loads them once and finds the tile's first / last
@@ -835,9 +850,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
       if (lane == 0) offc[kOffCache] = a.offsets[min(c + kOffCache, a.n_contig)];
     }
   }
-  for (int i = t; i < kSpan; i += blockDim.x) {
-    const uint64_t g = base + r0 + i;
-    bases[i] = (uint8_t)(g < end ? base2(a.dna[g]) : 4u);
+#pragma unroll
+  for (int j = 0; j < kTileIters; ++j) {
+    const int i = t + 256 * j;
+    if (i < kSpan) bases[i] = (uint8_t)(base + r0 + i < end ? base2(tb[j]) : 4u);
   }
   __syncthreads();
   KMA_CLK(1);  // tile loaded, contigs found

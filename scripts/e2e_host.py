@@ -8,6 +8,7 @@ copies and the piece kernels overlap.
   python scripts/e2e_host.py [--configs "pieces=8,threads=16;pieces=16,threads=16"] [--reps 2]
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -39,22 +40,30 @@ def main():
     print(f"generated in {time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
     table = kmeranno.SignatureTable.from_packed(sig.keys, sig.fids, K)
     names = {"pieces": "host_pieces", "threads": "host_threads", "packed": "packed_input"}
+    lib = kmeranno.load()
+    prof = (C.c_double * 6)()
+    lib.kma_debug_host_profile.argtypes = [C.c_void_p, C.c_int]
+    keys = ("setup", "stage", "launch", "wait", "outputs", "total")
     ref = None
     for rep in range(args.reps):
         for text in args.configs.split(";"):
             cfg = {names[k]: int(v) for k, v in (p.split("=") for p in text.split(",") if p)}
             with kmeranno.options(**cfg):
                 kmeranno.annotate_proteins(table, res, off, MIN_HITS, 0, n_fid=n_fid)
-                best = 1e30
+                best, best_prof = 1e30, None
                 for _ in range(args.calls):
                     t1 = time.perf_counter()
                     got = kmeranno.annotate_proteins(table, res, off, MIN_HITS, 0, n_fid=n_fid)
-                    best = min(best, time.perf_counter() - t1)
+                    dt = time.perf_counter() - t1
+                    if dt < best:
+                        lib.kma_debug_host_profile(C.addressof(prof), 6)
+                        best, best_prof = dt, dict(zip(keys, (round(x, 4) for x in prof)))
             if ref is None:
                 ref = got
             same = all(np.array_equal(a, b) for a, b in zip(got, ref))
             print(json.dumps({"workload": args.workload, "config": text, "rep": rep,
                               "ms": best * 1e3, "residues": int(off[-1]),
+                              "host_profile_ms": best_prof,
                               "outputs_equal_first": bool(same)}), flush=True)
     table.close()
 
