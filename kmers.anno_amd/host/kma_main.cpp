@@ -346,9 +346,11 @@ class ApplyKmerProcessor {
     std::vector<ParsedGenome> pending;  // batched mode: genomes of the current batch
     ProteinBatch b;
     uint64_t n_prot = 0, n_res = 0;
-    double wait_s = 0, report_s = 0;
+    double wait_s = 0, report_s = 0, free_s = 0;
     for (size_t i = 0; i < files.size();) {
-      pending.clear();
+      const auto f0 = Clock::now();
+      pending.clear();  // the previous genomes' parsed GTOs
+      free_s += seconds(f0);
       const auto w0 = Clock::now();
       if (on_workers) {
         pending.push_back(feed.take(i++));
@@ -393,10 +395,12 @@ class ApplyKmerProcessor {
     std::fprintf(stderr,
                  "[kma] apply-stats {\"genomes\": %zu, \"proteins\": %llu, \"residues\": %llu, "
                  "\"calls\": %llu, \"loop_s\": %.6f, \"native_call_s\": %.6f, "
-                 "\"report_wait_s\": %.6f, \"report_s\": %.6f, \"calls_on\": \"%s\", "
+                 "\"report_wait_s\": %.6f, \"report_s\": %.6f, \"free_s\": %.6f, "
+                 "\"calls_on\": \"%s\", "
                  "\"parse_threads\": %d, \"batch_residues\": %llu, \"table_load_s\": %.6f}\n",
                  files.size(), (unsigned long long)n_prot, (unsigned long long)n_res,
                  (unsigned long long)calls.load(), wall, call_us.load() * 1e-6, wait_s, report_s,
+                 free_s,
                  on_workers ? "parse workers" : "report thread", feed.threads(),
                  (unsigned long long)batchResidues_, tableLoadS_);
   }
