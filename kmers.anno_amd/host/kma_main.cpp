@@ -179,17 +179,38 @@ class GenomeFeed {
     return out;
   }
   int threads() const { return (int)pool_.size(); }
+  // Genomes the consumer is done with: freed by the workers (a parsed GTO is ~16k small
+  // allocations; freeing them on the report thread cost ~0.5-0.9 ms per genome).
+  void recycle(std::vector<ParsedGenome>& done) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (ParsedGenome& pg : done) trash_.push_back(std::move(pg));
+    }
+    done.clear();
+    cv_.notify_all();  // (the consumer waits on the same condition)
+  }
 
  private:
   void work() {
     for (;;) {
-      size_t i;
+      std::vector<ParsedGenome> trash;
+      size_t i = 0;
+      bool parse = false;
       {
         std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || next_ >= files_.size() || next_ < taken_ + lookahead_; });
-        if (stop_ || next_ >= files_.size()) return;
-        i = next_++;
+        cv_.wait(g, [&] {
+          return stop_ || !trash_.empty() || (next_ < files_.size() && next_ < taken_ + lookahead_);
+        });
+        if (!trash_.empty()) {
+          trash.swap(trash_);
+        } else if (stop_) {
+          return;
+        } else {
+          i = next_++;
+          parse = true;
+        }
       }
+      if (!parse) continue;  // (trash freed here, outside the lock)
       ParsedGenome pg;
       std::string err;
       try {
@@ -213,6 +234,7 @@ class GenomeFeed {
   std::vector<ParsedGenome> slots_;
   std::vector<std::string> errors_;
   std::vector<char> ready_;
+  std::vector<ParsedGenome> trash_;
   size_t lookahead_, next_ = 0, taken_ = 0;
   bool stop_ = false;
   After after_;
@@ -349,7 +371,7 @@ class ApplyKmerProcessor {
     double wait_s = 0, report_s = 0, free_s = 0;
     for (size_t i = 0; i < files.size();) {
       const auto f0 = Clock::now();
-      pending.clear();  // the previous genomes' parsed GTOs
+      feed.recycle(pending);  // the previous genomes' parsed GTOs: freed by the parse workers
       free_s += seconds(f0);
       const auto w0 = Clock::now();
       if (on_workers) {
