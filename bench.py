@@ -457,10 +457,10 @@ def bench_genomes(args):
     """The drop-in's own regime: `kma apply` (the C++ mirror of ApplyKmerProcessor over the C
     ABI) on a directory of synthetic GTOs, as a SEEDtk pipeline runs it (ApplyKmerProcessor.
     java:116-151: genome by genome, every peg's protein). Timed: the command's genome loop
-    (parse + native calls + reports; its apply-stats line), pipelined (GTO parse-ahead pool,
-    the native call of each genome made by its parse worker: the default), with consecutive
-    genomes batched into 16M-residue calls on the report thread, and as round 3 ran it (one
-    thread, one call per genome).
+    (parse + native calls + reports; its apply-stats line) in the command's default mode (GTO
+    parse-ahead pool, consecutive genomes batched into 16M-residue calls), with each parse
+    worker making its own genome's call (--batch 0), and as round 3 ran it (one thread, one
+    call per genome).
     The APPLY report is checked line for line against the oracle's calls."""
     import shutil
     import tempfile
@@ -500,11 +500,11 @@ def bench_genomes(args):
             log(f"kma apply {tag}: {stats}")
             return stats, open(out_path).read().splitlines()
 
-        piped, report = run([], "pipelined")
-        piped2, report2 = run([], "pipelined2")  # the GTOs are in the page cache for both
-        batched, report_b = run(["--batch", str(16 << 20)], "batched")
+        dflt, report = run([], "default")
+        dflt2, report2 = run([], "default2")  # the GTOs are in the page cache for both
+        workers, report_w = run(["--batch", "0"], "worker_calls")
         seq, report_seq = run(["--threads", "1", "--batch", "1"], "per_genome")
-        best = min((piped, piped2), key=lambda s: s["loop_s"])
+        best = min((dflt, dflt2), key=lambda s: s["loop_s"])
         # parity: the oracle's calls (restatement of the same loop) -> the APPLY report
         table, load_s = oracle_table(sig.keys, sig.fids)
         col = {synth.role_name(i): j for j, i in enumerate(range(0, n_fid, 10))}
@@ -516,7 +516,7 @@ def bench_genomes(args):
             keep = called[called % 10 == 0] // 10
             np.add.at(counts, keep, 1)
             expect.append(gid + "\t" + "\t".join(map(str, counts.tolist())))
-        parity = all(r == expect for r in (report, report2, report_b, report_seq))
+        parity = all(r == expect for r in (report, report2, report_w, report_seq))
         loop = best["loop_s"]
         out = {
             "metric": "genomes annotated/s through `kma apply` (ApplyKmerProcessor mirror over "
@@ -529,8 +529,8 @@ def bench_genomes(args):
                        "gto_bytes": gbytes, "proteins": n_prot, "windows": n_win,
                        "table_entries": t_size, "k": K, "min_hits": MIN_HITS},
             "seqs_per_s": n_prot / loop, "lookups_per_s": n_win / loop,
-            "pipelined": best, "pipelined_runs_loop_s": [piped["loop_s"], piped2["loop_s"]],
-            "batched_on_report_thread": dict(batched, genomes_per_s=n_gen / batched["loop_s"]),
+            "default_batched": best, "default_runs_loop_s": [dflt["loop_s"], dflt2["loop_s"]],
+            "calls_on_parse_workers": dict(workers, genomes_per_s=n_gen / workers["loop_s"]),
             "per_genome_sequential": dict(seq, genomes_per_s=n_gen / seq["loop_s"]),
             "speedup_vs_per_genome": seq["loop_s"] / loop,
             "native_call_share": best["native_call_s"] / loop,

@@ -345,11 +345,12 @@ class ApplyKmerProcessor {
   // :114-155. The reference loops genome by genome: parse a GTO, run every peg's ProteinKmers
   // through the map, report. Here the same reports come out in the same order, while
   //   - GTOs are parsed ahead by a pool of threads (GenomeFeed: the loader skips contig DNA),
-  //   - the native calls run off the report thread: by default each parse worker makes its
-  //     genome's call (concurrent host calls on one table: a pooled context and stream each,
-  //     include/kmeranno.h), so parsing, staging and the GPU overlap across genomes;
-  //     --batch R > 0 instead concatenates consecutive genomes into one call of >= R residues
-  //     on the report thread (fewer, larger launches),
+  //   - consecutive genomes are concatenated into one native call of >= R residues
+  //     (--batch R, default 16M: c4-sized launches instead of ~4k-protein ones; 1,498 vs 1,244
+  //     genomes/s over 500 GTOs, profiles/r04_end/bench_genomes.json), made on the report
+  //     thread while the pool parses ahead; --batch 0 instead has each parse worker make its
+  //     own genome's call (concurrent host calls on one table: a pooled context and stream
+  //     each, include/kmeranno.h),
   //   - the report thread only waits for genome i, then writes its report.
   void runCommand() {
     const std::vector<std::string> files = genome_files(inDir_);
@@ -462,7 +463,7 @@ class ApplyKmerProcessor {
   int device_ = 0;
   bool help_ = false;
   int parseThreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  uint64_t batchResidues_ = 0;  // 0: a native call per genome on its parse worker
+  uint64_t batchResidues_ = 16u << 20;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
   std::unique_ptr<ApplyKmerReporter> reporter_;
@@ -479,8 +480,8 @@ const char* kApplyUsage =
     " --format FMT      reporting format: APPLY (default) or VERIFY\n"
     " --device D        HIP device ordinal (default 0)\n"
     " --threads N       GTO parser threads (default min(16, cores))\n"
-    " --batch R         0 (default): each parser thread makes its genome's native call;\n"
-    "                   R > 0: consecutive genomes batched into calls of >= R residues\n";
+    " --batch R         consecutive genomes batched into native calls of >= R residues\n"
+    "                   (default 16777216); 0: each parser thread makes its genome's call\n";
 
 int run_apply(const std::vector<std::string>& args) {
   ApplyKmerProcessor p;

@@ -91,7 +91,7 @@ def test_kma_apply_reports(kma_bin, oracle_c, small_gto, apply_inputs, min_hits)
 @pytest.mark.parametrize("threads,batch", [(6, 0), (1, 1), (4, 500_000), (8, 1 << 40)])
 def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads, batch):
     """`kma apply` over a directory of 14 synthetic GTOs (600 pegs each, a contig of DNA the
-    loader skips): GTOs parsed ahead by a thread pool; batch 0 (the default): every parse
+    loader skips): GTOs parsed ahead by a thread pool; batch 0: every parse
     worker makes its own genome's native call (concurrent host calls on one table); batch > 0:
     consecutive genomes batched on the report thread into one native call of >= `batch`
     residues (1: a call per genome, as round 3; 500k: several genomes per call; 2^40: one
