@@ -287,7 +287,7 @@ __device__ __forceinline__ void dedupe_lists(ProteinSmem<P>& sm, const ProteinAr
       uint32_t* set = a.gset + 2 * (span_lo + b0) + L;
       for (uint32_t i = t; i < L; i += 256)
         __hip_atomic_store(set + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
+      __threadfence();  // (giant proteins only: an L2 writeback per such protein)
       __syncthreads();
       for (uint32_t i = t; i < h; i += 256) fresh += global_set_insert(set, L, list[i]);
     }
@@ -1231,8 +1231,13 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
     if (blockIdx.x == gridDim.x - 1 && lane == kEmitSpan - 1) *a.n_hits = base + inc;
   }
   __syncthreads();
-  if (t == 0)  // this block's reads of the group sums are done (their values are in pre[])
-    last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_ACQ_REL,
+  // This block's reads of the group sums have returned (their values are in pre[], behind the
+  // barrier), so a relaxed count suffices: the last block's zeroing cannot reach a read that
+  // has already completed. (An acq_rel atomic here compiles to a whole-L2 writeback and
+  // invalidate around it, buffer_wbl2 / buffer_inv, in every emit block: 18 vs ~5 us per c3
+  // emit pass, profiles/r04_end/stats_c3_kernel_stats.csv.)
+  if (t == 0)
+    last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   uint4* out = reinterpret_cast<uint4*>(a.out);
   for (uint32_t i = wave; i < kEmitSpan && b0 + i < n_blocks; i += kWavesPerBlock) {
