@@ -383,8 +383,10 @@ constexpr int kContigPos = KMA_CONTIG_POS;
 // other blocks of the CU overlap them; a lane keeps one slice's loads in flight, so VGPRs stay
 // those of one slice (kContigPos = 2 holds two slices' loads at once: 97 VGPRs, 4 waves/SIMD,
 // measured slower).
+// Round 4: 2 slices (c3 0.124 -> 0.099 ms, profiles/r04/c3_seq_r04c.log), then 4 (0.0916 ->
+// 0.087 ms against 3 slices' 0.088, ABAB, profiles/r04/c3_seq_ab_r04final.log).
 #ifndef KMA_CONTIG_SEQ
-#define KMA_CONTIG_SEQ 2
+#define KMA_CONTIG_SEQ 4
 #endif
 constexpr int kContigSeq = KMA_CONTIG_SEQ;
 static_assert(kContigSeq == 1 || kContigPos == 1, "sequential slices take one position per lane");

@@ -21,7 +21,7 @@ from bench import K, MIN_HITS, kmeranno, synth  # noqa: E402
 
 
 def contigs_timeline():
-    """c3: contigs_probe_quad_kernel's blocks (512 positions each since round 4): clock 0 start,
+    """c3: contigs_probe_quad_kernel's blocks (256 x KMA_CONTIG_SEQ positions each): clock 0 start,
     1 tile loaded + contigs found, 2 translated, 3 bucket loads issued (last slice), 4 matched
     (last slice), 5 end (records staged, block count added)."""
     dev = torch.device("cuda", 0)

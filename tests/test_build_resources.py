@@ -49,7 +49,7 @@ def test_no_scratch_in_our_kernels(usage):
 
 def test_hot_kernels_occupancy(usage):
     # the protein probe keeps 7 waves per SIMD (amdgpu_waves_per_eu(7, 8)); the 6-frame probe 7
-    # (its two sequential 256-position slices per block, KMA_CONTIG_SEQ; 8 with one)
+    # (its four sequential 256-position slices per block, KMA_CONTIG_SEQ; 8 with one)
     hot = {"annotate_kernelILi8ELi6ELi8E": 7, "contigs_probe_quad_kernelILi8ELi6E": 7}
     for frag, occ in hot.items():
         names = [k for k in usage if frag in k]

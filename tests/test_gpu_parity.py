@@ -600,21 +600,22 @@ def test_contigs_device_graph_capture_replay(kma, oracle_c):
 
 
 def test_contigs_device_many_groups_scanned(kma):
-    """A device call of more than kDirectGroups x 256 probe blocks (> 134M bases at 512
+    """A device call of more than kDirectGroups x 256 probe blocks (> 268M bases at 1,024
     positions per block: the emit pass scans the group sums first instead of summing them per
     block) equals the same genome cut into calls below that size, hit for hit after re-basing,
     with the same total; then the whole call again on the same workspace."""
     torch = pytest.importorskip("torch")
     from kmeranno import synth
     wl = synth.make_contig_workload(2_000_000, 8, 77, table_size=300_000, n_fid=300)
-    # 70 copies of the genome: 140 Mbp in 560 contigs (1,069 emit-offset groups)
-    reps = 70
+    # 140 copies of the genome: 280 Mbp in 1,120 contigs (1,069 emit-offset groups of 256
+    # probe blocks of 1,024 positions)
+    reps = 140
     n0 = int(wl.offsets[-1])
     dna = np.concatenate([np.tile(wl.dna[:n0], reps), np.zeros(64, np.uint8)])
     off = np.concatenate([[0]] + [wl.offsets[1:] + np.uint64(i * n0) for i in range(reps)])
     off = off.astype(np.uint64)
     n_contig, n_bases = len(off) - 1, int(off[-1])
-    assert n_bases > 1024 * 256 * 512
+    assert n_bases > 1024 * 256 * 1024
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
