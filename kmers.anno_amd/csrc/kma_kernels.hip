@@ -1239,11 +1239,37 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
   if (t == 0)
     last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  // The span's records, flattened: thread t copies records t, t + 256, ... (kEmitU loads in
+  // flight before their stores). Record r belongs to the last span block whose first record is
+  // <= r. (A wave per probe block, a load-then-store loop per 64 records, took a dependent
+  // round trip per iteration: 11.6 us per c3 emit pass, profiles/r04_final.)
+  constexpr int kEmitU = 4;
+  uint32_t first[kEmitSpan];  // span-local first record of each probe block
+  const uint64_t p0 = pre[0];
+#pragma unroll
+  for (uint32_t k = 0; k < kEmitSpan; ++k) first[k] = (uint32_t)(pre[k] - p0);
+  const uint32_t total = first[kEmitSpan - 1] + cnt[kEmitSpan - 1];
+  const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)b0 * (2 * kContigTile);
   uint4* out = reinterpret_cast<uint4*>(a.out);
-  for (uint32_t i = wave; i < kEmitSpan && b0 + i < n_blocks; i += kWavesPerBlock) {
-    const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)(b0 + i) * (2 * kContigTile);
-    const uint64_t o = pre[i];
-    for (uint32_t r = lane; r < cnt[i] && o + r < a.cap; r += 64) out[o + r] = st[r];
+  for (uint32_t r0 = 0; r0 < total; r0 += 256u * kEmitU) {
+    uint4 v[kEmitU];
+    uint64_t d[kEmitU];
+#pragma unroll
+    for (int u = 0; u < kEmitU; ++u) {
+      const uint32_t r = r0 + 256u * u + t;
+      d[u] = ~0ull;
+      if (r < total) {
+        uint32_t i = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < kEmitSpan; ++k) i = first[k] <= r ? k : i;
+        const uint32_t j = r - first[i];
+        v[u] = st[(uint64_t)i * (2 * kContigTile) + j];
+        d[u] = p0 + r;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kEmitU; ++u)
+      if (d[u] < a.cap) out[d[u]] = v[u];
   }
   __syncthreads();
   if (last) {  // every other emit block has read its offsets: clean up for the next call
