@@ -165,6 +165,28 @@ StagingPool& staging_pool() {
   static StagingPool* pool = new StagingPool();  // never destroyed: no join at process exit
   return *pool;
 }
+
+// dst[i] = src[i] - base for i < n, on the staging pool for large n (a host call's rebased
+// offsets: 8 MB for c5's 1M proteins).
+void rebase_offsets(uint64_t* dst, const uint64_t* src, uint64_t n, uint64_t base) {
+  constexpr uint64_t kChunk = 1u << 17;
+  staging_pool().run((n + kChunk - 1) / kChunk, n >= 4 * kChunk ? staging_threads() : 1,
+                     [&](uint64_t c) {
+                       const uint64_t e = std::min(n, (c + 1) * kChunk);
+                       for (uint64_t i = c * kChunk; i < e; ++i) dst[i] = src[i] - base;
+                     });
+}
+
+// memcpy on the staging pool in 1 MiB chunks (the outputs of a large host call).
+void pool_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kChunk = 1u << 20;
+  staging_pool().run((n + kChunk - 1) / kChunk, n >= 4 * kChunk ? staging_threads() : 1,
+                     [&](uint64_t c) {
+                       const size_t o = c * kChunk;
+                       std::memcpy(static_cast<uint8_t*>(dst) + o,
+                                   static_cast<const uint8_t*>(src) + o, std::min(kChunk, n - o));
+                     });
+}
 }  // namespace
 
 int kma::minimizer_len(int k, uint64_t n_buckets) {
@@ -1210,7 +1232,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   uint8_t* hin = c->h_in.p;
   hipStream_t s = c->stream;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
-  for (uint32_t i = 0; i <= n; ++i) hoff[i] = offsets[lo + i] - base;
+  rebase_offsets(hoff, offsets + lo, (uint64_t)n + 1, base);
   KMA_HIP(hipMemcpyAsync(c->d_off.p, hoff, off_bytes, hipMemcpyHostToDevice, c->copy[0]));
   uint8_t* dout = c->d_out.p;
   int32_t* d_fid = reinterpret_cast<int32_t*>(dout);
@@ -1263,10 +1285,10 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   const double t_wait = ms_since(t_w);
   const Clock::time_point t_o = Clock::now();
   const uint8_t* hout = c->h_out.p;
-  std::memcpy(out_fid + lo, hout, n * 4ull);
-  std::memcpy(out_count + lo, hout + n * 4ull, n * 4ull);
+  pool_memcpy(out_fid + lo, hout, n * 4ull);
+  pool_memcpy(out_count + lo, hout + n * 4ull, n * 4ull);
   const uint8_t* ht = hout + n * 8ull;
-  std::memcpy(out_status + lo, ht + (tally ? n_fid * 4ull : 0), n);
+  pool_memcpy(out_status + lo, ht + (tally ? n_fid * 4ull : 0), n);
   if (tally) std::memcpy(tally, ht, n_fid * 4ull);
   {
     const double p[6] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o), ms_since(t_call)};
