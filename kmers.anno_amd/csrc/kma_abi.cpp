@@ -1486,7 +1486,20 @@ int kma_pack_residues(const kma_table* t, const uint8_t* residues, uint64_t n, u
                 (unsigned long long)n, (unsigned long long)kma::packed_bytes(n));
   uint8_t std_lut[256];
   if (!t) standard_lut(std_lut);
-  kma::pack_residues_host(t ? t->lut : std_lut, residues, n, out, out_bytes);
+  const uint8_t* lut = t ? t->lut : std_lut;
+  // large streams on the staging pool, in chunks of 2^15 groups (64 residues = 40 bytes each)
+  constexpr uint64_t kChunkGroups = 1u << 15;
+  const uint64_t n_groups = (n + 63) / 64, n_chunks = (n_groups + kChunkGroups - 1) / kChunkGroups;
+  if (n_chunks < 4) {
+    kma::pack_residues_host(lut, residues, n, out, out_bytes);
+    return KMA_OK;
+  }
+  staging_pool().run(n_chunks, staging_threads(), [&](uint64_t c) {
+    const uint64_t g0 = c * kChunkGroups, g1 = std::min(n_groups, g0 + kChunkGroups);
+    const uint64_t r0 = 64 * g0, r1 = std::min(64 * g1, n);
+    const uint64_t bytes = g1 == n_groups ? out_bytes - 40 * g0 : 40 * (g1 - g0);
+    kma::pack_residues_host(lut, residues + r0, r1 - r0, out + 40 * g0, bytes);
+  });
   return KMA_OK;
 }
 

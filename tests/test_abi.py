@@ -126,6 +126,39 @@ def _pack_reference(res: np.ndarray) -> np.ndarray:
     return np.packbits(bits)  # MSB first, zero-padded to a byte
 
 
+
+def test_pack_residues_staging_pool_concurrent(native_lib):
+    """Large streams are packed on the library's staging pool (chunks of 2^15 groups): four
+    Python threads packing at once (ctypes releases the GIL, so their jobs share the pool) get
+    the same streams as one-thread packing (KMA_OPT_HOST_THREADS = 1: the caller alone)."""
+    import threading
+    import kmeranno
+    rng = np.random.default_rng(7)
+    alphabet = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY*x", np.uint8)
+    arrays = [alphabet[rng.integers(0, len(alphabet), (1 << 23) + 777 * i)] for i in range(4)]
+    with kmeranno.options(host_threads=1):
+        want = [kmeranno.pack_residues(None, a) for a in arrays]
+    got = [None] * 4
+    errors = []
+
+    def run(i):
+        try:
+            for _ in range(3):
+                got[i] = kmeranno.pack_residues(None, arrays[i])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors and not any(t.is_alive() for t in threads)
+    assert all(np.array_equal(g, w) for g, w in zip(got, want))
+    head = _pack_reference(arrays[0][:1 << 16])  # the pool's first chunk against the format
+    assert np.array_equal(want[0][:len(head)], head)
+
+
 @pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 63, 64, 65, 200, 4096 + 37, 100_003])
 def test_pack_residues_host_matches_bitwise_reference(native_lib, n):
     """kma_pack_residues (AVX2 body + scalar tail, chosen by the CPU) against a bitwise numpy
