@@ -19,6 +19,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -72,6 +74,11 @@ class ApplyKmerReporter {
   virtual void openReport() = 0;
   virtual void openGenome(const Genome& g) = 0;
   virtual void recordFeature(const Feature& f, const std::string& role, int count) = 0;
+  // The same call with the role's dense id in the kmer database (the caller's map key): lets
+  // a reporter cache per-role work (the default reporter's role -> column lookup).
+  virtual void recordFeature(const Feature& f, uint32_t fid, const std::string& role, int count) {
+    recordFeature(f, role, count);
+  }
   virtual void closeGenome() = 0;
   virtual void closeReport() {}
   int getRoleIdx(const std::string& role) const {  // :92-95, 0 when not interesting
@@ -91,8 +98,13 @@ class DefaultApplyKmerReporter : public ApplyKmerReporter {  // DefaultApplyKmer
     genomeId_ = g.id;
     std::fill(roleCounts_.begin(), roleCounts_.end(), 0);
   }
-  void recordFeature(const Feature&, const std::string& role, int) override {
-    const int idx = getRoleIdx(role);
+  void recordFeature(const Feature&, const std::string& role, int) override { count(getRoleIdx(role)); }
+  void recordFeature(const Feature&, uint32_t fid, const std::string& role, int) override {
+    if (fid >= colOfFid_.size()) colOfFid_.resize(fid + 1, -1);
+    if (colOfFid_[fid] < 0) colOfFid_[fid] = getRoleIdx(role);
+    count(colOfFid_[fid]);
+  }
+  void count(int idx) {
     if (idx > 0) {
       if (idx - 1 >= (int)roleCounts_.size())  // Java: ArrayIndexOutOfBoundsException
         throw std::runtime_error("role column " + std::to_string(idx) + " out of range");
@@ -101,15 +113,18 @@ class DefaultApplyKmerReporter : public ApplyKmerReporter {  // DefaultApplyKmer
   }
   void closeGenome() override {
     std::string line = genomeId_ + "\t";
+    char num[16];
     for (size_t i = 0; i < roleCounts_.size(); ++i) {
       if (i) line += '\t';
-      line += std::to_string(roleCounts_[i]);
+      line.append(num, (size_t)std::snprintf(num, sizeof num, "%d", roleCounts_[i]));
     }
-    std::printf("%s\n", line.c_str());
+    line += '\n';
+    std::fwrite(line.data(), 1, line.size(), stdout);
   }
 
  private:
   std::vector<int> roleCounts_;
+  std::vector<int> colOfFid_;  // role column of a kmer-database role id (-1: not looked up)
   std::string genomeId_;
 };
 
@@ -347,11 +362,12 @@ class ApplyKmerProcessor {
   //   - GTOs are parsed ahead by a pool of threads (GenomeFeed: the loader skips contig DNA),
   //   - consecutive genomes are concatenated into one native call of >= R residues
   //     (--batch R, default 16M: c4-sized launches instead of ~4k-protein ones; 1,498 vs 1,244
-  //     genomes/s over 500 GTOs, profiles/r04_end/bench_genomes.json), made on the report
-  //     thread while the pool parses ahead; --batch 0 instead has each parse worker make its
+  //     genomes/s over 500 GTOs, profiles/r04_end/bench_genomes.json), made on a caller thread
+  //     while the pool parses ahead; --batch 0 instead has each parse worker make its
   //     own genome's call (concurrent host calls on one table: a pooled context and stream
   //     each, include/kmeranno.h),
-  //   - the report thread only waits for genome i, then writes its report.
+  //   - the report thread only waits for genome i, then writes its report; batches are called
+  //     on a caller thread, so a batch's call overlaps the previous batch's reports.
   void runCommand() {
     const std::vector<std::string> files = genome_files(inDir_);
     log_info("%zu genomes found in input directory.", files.size());
@@ -366,51 +382,110 @@ class ApplyKmerProcessor {
     };
     GenomeFeed feed(files, parseThreads_, on_workers ? 4 * (size_t)parseThreads_ : 4 * batchGenomesHint(),
                     on_workers ? annotate : nullptr);
-    std::vector<ParsedGenome> pending;  // batched mode: genomes of the current batch
-    ProteinBatch b;
+    // Batched mode: a caller thread takes the parsed genomes in order, makes one native call per
+    // batch and queues the annotated genomes for the report thread, so batch i + 1's call runs
+    // while batch i is reported.
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::deque<ParsedGenome> ready;
+    bool caller_done = false, reports_failed = false;
+    std::exception_ptr caller_error;
+    double caller_wait_s = 0;
+    std::thread caller;
+    if (!on_workers) {
+      caller = std::thread([&] {
+        try {
+          const size_t max_ready = 2 * batchGenomesHint();
+          ProteinBatch b;
+          std::vector<ParsedGenome> batch;
+          for (size_t i = 0; i < files.size();) {
+            batch.clear();
+            b.clear();
+            const auto w0 = Clock::now();
+            while (i < files.size() && (batch.empty() || b.residues.size() < batchResidues_)) {
+              batch.push_back(feed.take(i++));
+              b.add(batch.back().pegs);
+            }
+            caller_wait_s += seconds(w0);
+            ParsedGenome all;  // the batch's outputs, split back per genome below
+            call(b, all, calls, call_us);
+            size_t at = 0;
+            for (ParsedGenome& pg : batch) {
+              const size_t n = pg.pegs.size();
+              pg.fid.assign(all.fid.begin() + at, all.fid.begin() + at + n);
+              pg.count.assign(all.count.begin() + at, all.count.begin() + at + n);
+              pg.status.assign(all.status.begin() + at, all.status.begin() + at + n);
+              at += n;
+            }
+            std::unique_lock<std::mutex> g(qmu);
+            qcv.wait(g, [&] { return ready.size() < max_ready || reports_failed; });
+            if (reports_failed) break;
+            for (ParsedGenome& pg : batch) ready.push_back(std::move(pg));
+            g.unlock();
+            qcv.notify_all();
+          }
+        } catch (...) {
+          caller_error = std::current_exception();
+        }
+        {
+          std::lock_guard<std::mutex> g(qmu);
+          caller_done = true;
+        }
+        qcv.notify_all();
+      });
+    }
+    std::vector<ParsedGenome> done;  // reported genomes: freed by the parse workers
     uint64_t n_prot = 0, n_res = 0;
     double wait_s = 0, report_s = 0, free_s = 0;
-    for (size_t i = 0; i < files.size();) {
+    struct JoinCaller {  // a failing report stops and joins the caller before unwinding
+      std::thread& t;
+      std::mutex& mu;
+      std::condition_variable& cv;
+      bool& failed;
+      ~JoinCaller() {
+        if (!t.joinable()) return;
+        {
+          std::lock_guard<std::mutex> g(mu);
+          failed = true;
+        }
+        cv.notify_all();
+        t.join();
+      }
+    } join_caller{caller, qmu, qcv, reports_failed};
+    for (size_t i = 0; i < files.size(); ++i) {
       const auto f0 = Clock::now();
-      feed.recycle(pending);  // the previous genomes' parsed GTOs: freed by the parse workers
+      if (done.size() >= 8) feed.recycle(done);
       free_s += seconds(f0);
       const auto w0 = Clock::now();
       if (on_workers) {
-        pending.push_back(feed.take(i++));
+        done.push_back(feed.take(i));
       } else {
-        b.clear();
-        while (i < files.size() && (pending.empty() || b.residues.size() < batchResidues_)) {
-          pending.push_back(feed.take(i++));
-          b.add(pending.back().pegs);
-        }
+        std::unique_lock<std::mutex> g(qmu);
+        qcv.wait(g, [&] { return !ready.empty() || caller_done; });
+        if (ready.empty()) break;  // the caller failed (rethrown below)
+        done.push_back(std::move(ready.front()));
+        ready.pop_front();
+        g.unlock();
+        qcv.notify_all();
       }
       wait_s += seconds(w0);
-      if (!on_workers) {
-        ParsedGenome all;  // the batch's outputs, split back per genome below
-        call(b, all, calls, call_us);
-        size_t at = 0;
-        for (ParsedGenome& pg : pending) {
-          const size_t n = pg.pegs.size();
-          pg.fid.assign(all.fid.begin() + at, all.fid.begin() + at + n);
-          pg.count.assign(all.count.begin() + at, all.count.begin() + at + n);
-          pg.status.assign(all.status.begin() + at, all.status.begin() + at + n);
-          at += n;
-        }
-      }
       const auto r0 = Clock::now();
-      for (const ParsedGenome& pg : pending) {
-        const Genome& genome = *pg.genome;
-        log_info("Processing genome %s (%s).", genome.id.c_str(), genome.name.c_str());
-        reporter_->openGenome(genome);
-        for (size_t j = 0; j < pg.pegs.size(); ++j)
-          if (pg.status[j] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
-            reporter_->recordFeature(*pg.pegs[j], db_.roles[pg.fid[j]], pg.count[j]);
-        reporter_->closeGenome();
-        n_prot += pg.pegs.size();
-        for (const Feature* f : pg.pegs) n_res += f->protein.size();
-      }
+      const ParsedGenome& pg = done.back();
+      const Genome& genome = *pg.genome;
+      log_info("Processing genome %s (%s).", genome.id.c_str(), genome.name.c_str());
+      reporter_->openGenome(genome);
+      for (size_t j = 0; j < pg.pegs.size(); ++j)
+        if (pg.status[j] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
+          reporter_->recordFeature(*pg.pegs[j], (uint32_t)pg.fid[j], db_.roles[pg.fid[j]],
+                                   pg.count[j]);
+      reporter_->closeGenome();
+      n_prot += pg.pegs.size();
+      for (const Feature* f : pg.pegs) n_res += f->protein.size();
       report_s += seconds(r0);
     }
+    if (caller.joinable()) caller.join();  // (it has queued every genome, or failed)
+    if (caller_error) std::rethrow_exception(caller_error);
+    feed.recycle(done);
     reporter_->closeReport();
     std::fflush(stdout);
     const double wall = seconds(t0);
@@ -419,13 +494,12 @@ class ApplyKmerProcessor {
                  "[kma] apply-stats {\"genomes\": %zu, \"proteins\": %llu, \"residues\": %llu, "
                  "\"calls\": %llu, \"loop_s\": %.6f, \"native_call_s\": %.6f, "
                  "\"report_wait_s\": %.6f, \"report_s\": %.6f, \"free_s\": %.6f, "
-                 "\"calls_on\": \"%s\", "
+                 "\"caller_wait_s\": %.6f, \"calls_on\": \"%s\", "
                  "\"parse_threads\": %d, \"batch_residues\": %llu, \"table_load_s\": %.6f}\n",
                  files.size(), (unsigned long long)n_prot, (unsigned long long)n_res,
                  (unsigned long long)calls.load(), wall, call_us.load() * 1e-6, wait_s, report_s,
-                 free_s,
-                 on_workers ? "parse workers" : "report thread", feed.threads(),
-                 (unsigned long long)batchResidues_, tableLoadS_);
+                 free_s, caller_wait_s, on_workers ? "parse workers" : "caller thread",
+                 feed.threads(), (unsigned long long)batchResidues_, tableLoadS_);
   }
 
   // One native call on the proteins of `b`; outputs into pg (fid, count, status).

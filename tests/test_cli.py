@@ -132,7 +132,7 @@ def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads
     assert st["genomes"] == 14 and st["proteins"] == 14 * 600
     if batch in (0, 1):
         assert st["calls"] == 14
-        assert st["calls_on"] == ("parse workers" if batch == 0 else "report thread")
+        assert st["calls_on"] == ("parse workers" if batch == 0 else "caller thread")
     elif batch == 1 << 40:
         assert st["calls"] == 1
     else:
