@@ -1240,9 +1240,10 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
     last = __hip_atomic_fetch_add(a.emit_done, 1u, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   // The span's records, flattened: thread t copies records t, t + 256, ... (kEmitU loads in
-  // flight before their stores). Record r belongs to the last span block whose first record is
-  // <= r. (A wave per probe block, a load-then-store loop per 64 records, took a dependent
-  // round trip per iteration: 11.6 us per c3 emit pass, profiles/r04_final.)
+  // flight before their stores: no branch around a load, so the compiler keeps them in
+  // registers and issues them back to back). Record r belongs to the last span block whose
+  // first record is <= r. (A wave per probe block, a load-then-store loop per 64 records, took
+  // a dependent round trip per iteration: 11.6 us per c3 emit pass, profiles/r04_final.)
   constexpr int kEmitU = 4;
   uint32_t first[kEmitSpan];  // span-local first record of each probe block
   const uint64_t p0 = pre[0];
@@ -1252,24 +1253,31 @@ __global__ __launch_bounds__(256) void contigs_emit_kernel(ContigArgs a, uint32_
   const uint4* st = reinterpret_cast<const uint4*>(a.staging) + (uint64_t)b0 * (2 * kContigTile);
   uint4* out = reinterpret_cast<uint4*>(a.out);
   for (uint32_t r0 = 0; r0 < total; r0 += 256u * kEmitU) {
-    uint4 v[kEmitU];
-    uint64_t d[kEmitU];
+    uint4 v0, v1, v2, v3;
+    uint32_t rr[kEmitU];
+    uint64_t src[kEmitU];
 #pragma unroll
     for (int u = 0; u < kEmitU; ++u) {
       const uint32_t r = r0 + 256u * u + t;
-      d[u] = ~0ull;
-      if (r < total) {
-        uint32_t i = 0;
+      rr[u] = r < total ? r : 0u;  // out of range: record 0 of the span (read, not stored)
+      uint32_t i = 0, fi = 0;
 #pragma unroll
-        for (uint32_t k = 1; k < kEmitSpan; ++k) i = first[k] <= r ? k : i;
-        const uint32_t j = r - first[i];
-        v[u] = st[(uint64_t)i * (2 * kContigTile) + j];
-        d[u] = p0 + r;
-      }
+      for (uint32_t k = 1; k < kEmitSpan; ++k)
+        if (first[k] <= rr[u]) {
+          i = k;
+          fi = first[k];
+        }
+      src[u] = (uint64_t)i * (2 * kContigTile) + (rr[u] - fi);
     }
-#pragma unroll
-    for (int u = 0; u < kEmitU; ++u)
-      if (d[u] < a.cap) out[d[u]] = v[u];
+    v0 = st[src[0]];
+    v1 = st[src[1]];
+    v2 = st[src[2]];
+    v3 = st[src[3]];
+    const uint32_t r = r0 + t;
+    if (r < total && p0 + r < a.cap) out[p0 + r] = v0;
+    if (r + 256u < total && p0 + r + 256u < a.cap) out[p0 + r + 256u] = v1;
+    if (r + 512u < total && p0 + r + 512u < a.cap) out[p0 + r + 512u] = v2;
+    if (r + 768u < total && p0 + r + 768u < a.cap) out[p0 + r + 768u] = v3;
   }
   __syncthreads();
   if (last) {  // every other emit block has read its offsets: clean up for the next call
