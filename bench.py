@@ -338,8 +338,8 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
 
 def link_rates(residues, n_res, dev):
     """What bounds the host call: the pinned host -> device rate for the packed stream's bytes
-    (one copy, and 2 MiB copies as the staging pool issues them) and the host packer's rate on
-    one thread (kma_pack_residues)."""
+    (one copy, 2 MiB copies, 8 MiB copies over two / four streams) and the host packer's rate
+    (kma_pack_residues on one thread and on the staging pool), in GB of residues per second."""
     n_bytes = kmeranno.packed_bytes(n_res)
     src = torch.empty(n_bytes, dtype=torch.uint8).pin_memory()
     dst = torch.empty(n_bytes, dtype=torch.uint8, device=dev)
@@ -359,10 +359,13 @@ def link_rates(residues, n_res, dev):
         out[name] = n_bytes / (best * 1e-3) / 1e9
     n = min(n_res, 64 << 20)
     buf = np.empty(kmeranno.packed_bytes(n), np.uint8)
+    buf[:] = 0
     lib = kmeranno.load()
-    t0 = time.perf_counter()
-    lib.kma_pack_residues(None, residues, n, buf, len(buf))
-    out["pack_1thread_GBps"] = n / (time.perf_counter() - t0) / 1e9
+    for key, threads in (("pack_1thread_GBps", 1), ("pack_pool_GBps", 0)):
+        with kmeranno.options(host_threads=threads):  # 0: the staging pool's default width
+            t0 = time.perf_counter()
+            lib.kma_pack_residues(None, residues, n, buf, len(buf))
+            out[key] = n / (time.perf_counter() - t0) / 1e9
     # 8 MiB copies alternating over two / four streams (several DMA engines at once?)
     for n_streams in (2, 4):
         streams = [torch.cuda.Stream(dev) for _ in range(n_streams)]
