@@ -183,8 +183,23 @@ struct Parser {
     return buf;
   }
   // Members of an object, calling f(key) with p at the value; f consumes the value.
+  // members() that stops after the member for which f returns true (p is then just past that
+  // member's value; the rest of the object is not read). Returns whether it stopped early.
+  template <class F>
+  bool members_until(F f) {
+    bool stopped = false;
+    members_impl([&](std::string_view k) { return stopped = f(k); });
+    return stopped;
+  }
   template <class F>
   void members(F f) {
+    members_impl([&](std::string_view k) {
+      f(k);
+      return false;
+    });
+  }
+  template <class F>
+  void members_impl(F f) {
     ws();
     if (p >= end || *p != '{') error("expected object");
     ++p;
@@ -201,7 +216,7 @@ struct Parser {
       if (p >= end || *p != ':') error("expected ':'");
       ++p;
       ws();
-      f(k);
+      if (f(k)) return;
       ws();
       if (p < end && *p == ',') {
         ++p;
@@ -386,14 +401,22 @@ Genome load_genome_pegs(const std::string& path) {
   const MappedFile text(path);
   Parser ps{text.data, text.data, text.data + text.size};
   Genome g;
-  ps.members([&](std::string_view k) {
+  // Reading stops once id, scientific_name, genetic_code and features have been read: SEEDtk
+  // GTOs put the contigs (the DNA: most of the file) after them (small.gto's member order), so
+  // their pages are never touched. A file is then not checked past that point.
+  unsigned seen = 0;
+  const bool stopped = ps.members_until([&](std::string_view k) {
     if (k == "id") {
       g.id = scalar_string(ps);
+      seen |= 1;
     } else if (k == "scientific_name") {
       g.name = scalar_string(ps);
+      seen |= 2;
     } else if (k == "genetic_code") {
       g.genetic_code = (int)ps.value().as_int(11);
+      seen |= 4;
     } else if (k == "features") {
+      seen |= 8;
       ps.elements([&]() {
         Feature ft;
         ps.members([&](std::string_view fk) {
@@ -408,9 +431,12 @@ Genome load_genome_pegs(const std::string& path) {
     } else {
       ps.skip();  // contigs (their DNA), close genomes, subsystems, ...
     }
+    return seen == 15;
   });
-  ps.ws();
-  if (ps.p != ps.end) ps.error("trailing characters");
+  if (!stopped) {
+    ps.ws();
+    if (ps.p != ps.end) ps.error("trailing characters");
+  }
   return g;
 }
 

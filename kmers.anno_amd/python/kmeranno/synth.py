@@ -179,8 +179,8 @@ def write_roles_in_use(path: str, n_fid: int, every: int = 1):
 
 def write_genome_dir(out_dir: str, sig: SignatureSet, n_genomes: int, pegs_per_genome: int,
                      seed: int, contig_bp: int = 0, first: int = 0) -> list:
-    """Synthetic GTO files for `apply` (small.gto-like: id, scientific_name, genetic_code,
-    contigs, features of type CDS with protein_translation; the function is the peg's true
+    """Synthetic GTO files for `apply` (small.gto-like, in its member order: features of type
+    CDS with protein_translation, genetic_code, id, scientific_name, contigs; the function is the peg's true
     role or "hypothetical protein"). Proteins come from make_queries (the SURVEY §8(d) mix);
     each genome gets one random contig of contig_bp bases (skipped by the apply loader, but
     read). Returns [(genome id, residues, offsets)] per genome, in file-name order."""
@@ -201,10 +201,12 @@ def write_genome_dir(out_dir: str, sig: SignatureSet, n_genomes: int, pegs_per_g
         dna = b"acgt"[0:0]
         if contig_bp:
             dna = np.frombuffer(b"acgt", np.uint8)[rng.integers(0, 4, contig_bp)].tobytes()
-        text = (f'{{"id": "{gid}", "scientific_name": "Synthetica genomica {g}", '
-                f'"genetic_code": 11, "domain": "Bacteria", '
-                f'"contigs": [{{"id": "{gid}.con.0001", "dna": "{dna.decode()}"}}], '
-                f'"features": [' + ", ".join(feats) + ']}')
+        # top-level members in small.gto's order (domain, features, genetic_code, id,
+        # scientific_name, then contigs: the DNA comes last in SEEDtk GTOs)
+        text = (f'{{"domain": "Bacteria", "features": [' + ", ".join(feats) + '], '
+                f'"genetic_code": 11, "id": "{gid}", '
+                f'"scientific_name": "Synthetica genomica {g}", '
+                f'"contigs": [{{"id": "{gid}.con.0001", "dna": "{dna.decode()}"}}]}}')
         with open(os.path.join(out_dir, f"{gid}.gto"), "w") as f:
             f.write(text)
         out.append((gid, res, off))

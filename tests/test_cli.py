@@ -230,3 +230,17 @@ def test_gto_apply_loader_matches_json(kma_bin, small_gto, tmp_path):
                          encoding="utf-8")
     assert out.returncode == 0, out.stderr
     assert out.stdout.splitlines() == _dump_expected(tricky)
+    # members in small.gto's order: reading stops after id / scientific_name / genetic_code /
+    # features, so bytes after them (here: not even JSON) are never read; the same members
+    # with the contigs first are read through
+    early = {k: tricky[k] for k in ("features", "genetic_code", "id", "scientific_name")}
+    path = tmp_path / "early.gto"
+    path.write_text(json.dumps(early)[:-1] + ', "contigs": [{"id": "c1", "dna": "acgt"  <not json')
+    out = subprocess.run([kma_bin, "gto-dump", str(path)], capture_output=True, encoding="utf-8")
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == _dump_expected(tricky)
+    late = dict([("contigs", tricky["contigs"])] + list(early.items()))
+    path.write_text(json.dumps(late))
+    out = subprocess.run([kma_bin, "gto-dump", str(path)], capture_output=True, encoding="utf-8")
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.splitlines() == _dump_expected(tricky)
