@@ -310,6 +310,8 @@ class ApplyKmerProcessor {
         device_ = std::atoi(need("--device").c_str());
       } else if (a == "--threads") {
         parseThreads_ = std::max(1, std::atoi(need("--threads").c_str()));
+      } else if (a == "--staging-threads") {
+        stagingThreads_ = std::max(0, std::atoi(need("--staging-threads").c_str()));
       } else if (a == "--batch") {
         batchResidues_ = std::strtoull(need("--batch").c_str(), nullptr, 10);
       } else if (!a.empty() && a[0] == '-' && a.size() > 1) {
@@ -332,6 +334,7 @@ class ApplyKmerProcessor {
     if (!can_read(kmerDbFile_))
       throw NotFound("Kmer database file " + kmerDbFile_ + " not found or unreadable.");
     if (minHits_ < 1) throw UsageError("Min-hits must be positive.");
+    if (stagingThreads_ >= 0) check(kma_option_set(KMA_OPT_HOST_THREADS, stagingThreads_), "kma_option_set");
     if (outputType_ == "VERIFY") reporter_.reset(new VerifyApplyKmerReporter());
     else reporter_.reset(new DefaultApplyKmerReporter());
     if (!can_read(goodRoleFile_))
@@ -537,6 +540,7 @@ class ApplyKmerProcessor {
   int device_ = 0;
   bool help_ = false;
   int parseThreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  int stagingThreads_ = -1;  // KMA_OPT_HOST_THREADS for this run (-1: the library's default)
   uint64_t batchResidues_ = 16u << 20;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
@@ -554,6 +558,7 @@ const char* kApplyUsage =
     " --format FMT      reporting format: APPLY (default) or VERIFY\n"
     " --device D        HIP device ordinal (default 0)\n"
     " --threads N       GTO parser threads (default min(16, cores))\n"
+    " --staging-threads N  library threads packing a call's residues (default: min(16, cores))\n"
     " --batch R         consecutive genomes batched into native calls of >= R residues\n"
     "                   (default 16777216); 0: each parser thread makes its genome's call\n";
 
