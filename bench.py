@@ -30,6 +30,8 @@ Beside the timed steps, rank 0 of a 1-GPU run also reports
                 same full table.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c4]
+  python bench.py --workload genomes|fasta   (the drop-in's command-level regimes: `kma apply`
+                  over a GTO directory / `kma apply-fasta` over a protein FASTA file)
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0.
@@ -547,6 +549,96 @@ def bench_genomes(args):
         shutil.rmtree(root, ignore_errors=True)
 
 
+def bench_fasta(args):
+    """The FASTA form of the drop-in (north_star: "throughput on synthetic
+    FASTA of a stated length distribution"): `kma apply-fasta` as a child process over one
+    protein FASTA file of c4's 1M proteins (lengths resampled from small.gto's CDS lengths,
+    SURVEY §8(d) query mix, 60-residue lines, ">fig|... function" headers) against c4's
+    10^7-row table. Timed: the command's loop, file open -> last report row written (parse,
+    native calls, VERIFY rows; its apply-fasta-stats line), best of 2 runs with the file in the
+    page cache; the table load is reported beside it. The VERIFY report is checked line for
+    line against the oracle's calls on the same proteins."""
+    import shutil
+    import tempfile
+    from oracle import c_oracle
+    n_seq, t_size, n_fid, seed = synth.CONFIGS["c4"]
+    n_seq = args.n_seq or n_seq
+    root = tempfile.mkdtemp(prefix="kma_fasta_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        t0 = time.perf_counter()
+        sig = synth.make_table(t_size, n_fid, seed, K)
+        res, off, _, true_fid = synth.make_queries(sig, n_seq, seed * 1_000_003 + 17)
+        db, roles, faa = (os.path.join(root, x) for x in ("kmerdb.tbl", "roles.in.use",
+                                                             "83333.1.faa"))
+        synth.write_kmer_db(db, sig.keys, sig.fids)
+        synth.write_roles_in_use(roles, n_fid, every=10)
+        ids = [f"fig|83333.1.peg.{i + 1}" for i in range(n_seq)]
+        com = [synth.role_name(int(t)) if t >= 0 else "hypothetical protein" for t in true_fid]
+        fbytes = synth.write_fasta(faa, res, off, ids, com, width=60)
+        n_win = int(np.maximum(np.diff(off).astype(np.int64) - K + 1, 0).sum())
+        log(f"FASTA: {n_seq} proteins, {int(off[-1])} residues, {fbytes / 1e6:.0f} MB, "
+            f"{n_win} windows; table + file written in {time.perf_counter() - t0:.0f}s")
+        kma = os.path.join(ROOT, "kmers.anno_amd", "build", "kma")
+
+        def run(fmt, tag):
+            out_path = os.path.join(root, f"report_{tag}.txt")
+            w0 = time.perf_counter()
+            with open(out_path, "w") as out:
+                p = subprocess.run([kma, "apply-fasta", "--format", fmt, db, roles, faa],
+                                   stdout=out, stderr=subprocess.PIPE, text=True, timeout=1200)
+            wall = time.perf_counter() - w0
+            if p.returncode != 0:
+                raise RuntimeError(f"kma apply-fasta {tag}: rc {p.returncode}\n{p.stderr[-3000:]}")
+            line = [ln for ln in p.stderr.splitlines() if "apply-fasta-stats" in ln][-1]
+            stats = json.loads(line.split("apply-fasta-stats ", 1)[1])
+            stats["command_wall_s"] = wall
+            log(f"kma apply-fasta {tag}: {stats}")
+            return stats, open(out_path).read().splitlines()
+
+        runs = [run("VERIFY", f"verify{i}") for i in range(2)]
+        apply_stats, apply_report = run("APPLY", "apply")
+        best = min(runs, key=lambda r: r[0]["loop_s"])[0]
+        table, load_s = oracle_table(sig.keys, sig.fids)
+        fid, cnt, st = c_oracle.apply_mt(table, res, off, K, MIN_HITS, 0, host_threads())
+        called = np.flatnonzero(st == kmeranno.STATUS_CALLED)
+        expect = ["genome_id\tpeg_id\trole\thits\tfunction"] + [
+            f"83333.1\t{ids[i]}\t{synth.role_name(int(fid[i]))}\t{int(cnt[i])}\t{com[i]}"
+            for i in called]
+        counts = np.zeros(len(range(0, n_fid, 10)), np.int64)
+        keep = fid[called][fid[called] % 10 == 0] // 10
+        np.add.at(counts, keep, 1)
+        expect_apply = ["83333.1\t" + "\t".join(map(str, counts.tolist()))]
+        parity = all(r[1] == expect for r in runs) and apply_report == expect_apply
+        loop = best["loop_s"]
+        out = {
+            "metric": METRIC, "value": n_win / loop, "unit": "kmer lookups/s", "n_gpus": 1,
+            "steps": 1, "warmup": 1, "ms_per_step": loop * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic protein FASTA (seeded; SURVEY.md §8(d) generator: small.gto CDS "
+                    "length distribution, 50% mutated prototypes / 40% random / 10% chimeras)",
+            "config": {"workload": "fasta: `kma apply-fasta` (file -> VERIFY report) over one "
+                                   "FASTA file of c4's 1M proteins vs the 10^7-row table",
+                       "proteins": n_seq, "residues": int(off[-1]), "fasta_bytes": fbytes,
+                       "windows": n_win, "table_entries": t_size, "k": K, "min_hits": MIN_HITS,
+                       "line_width": 60, "parallelism": "one GPU; segments of 16 MiB parsed and "
+                                                        "called on 16 host threads"},
+            "seqs_per_s": n_seq / loop, "fasta_mb_per_s": fbytes / 1e6 / loop,
+            "loop": best, "runs_loop_s": [r[0]["loop_s"] for r in runs],
+            "apply_format": apply_stats,
+            "table_load_s": best["table_load_s"],
+            "command_wall_s": best["command_wall_s"],
+            "native_call_share": best["native_call_s"] / max(loop, 1e-9),
+            "verify_report_equals_oracle": all(r[1] == expect for r in runs),
+            "apply_report_equals_oracle": apply_report == expect_apply,
+            "called": len(called), "oracle_table_load_s": load_s,
+        }
+        print(json.dumps(out), flush=True)
+        if not parity:
+            sys.exit(1)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
 def e2e_host(table, residues, offsets, n_fid, reps=3):
     """kma_annotate_proteins from host memory (H2D + kernel + D2H through the table's pooled
     pinned staging): best of `reps` calls after one warmup call, in ms."""
@@ -633,7 +725,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS) + ["genomes"])
+    ap.add_argument("--workload", default="c5",
+                    choices=sorted(WORKLOADS) + ["genomes", "fasta"])
     ap.add_argument("--genomes", type=int, default=500,
                     help="genomes workload: GTO files (4,000 pegs each)")
     ap.add_argument("--contig-bp", type=int, default=4_000_000,
@@ -661,6 +754,9 @@ def main():
     kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, args.packed_input)
     if args.workload == "genomes":  # a command-level run: `kma apply` as a child process
         bench_genomes(args)
+        return
+    if args.workload == "fasta":  # a command-level run: `kma apply-fasta` as a child process
+        bench_fasta(args)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

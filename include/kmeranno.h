@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 5
+#define KMA_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -118,6 +118,9 @@ typedef struct kma_table_info {
   uint64_t n_displaced;  /* keys stored past their home bucket (overflow chains)            */
   int32_t n_replicas;    /* devices holding a copy of the slot array                        */
   int32_t slots_per_bucket; /* kma_bucket_slots_for(k): 8 (16) narrow, 4 wide               */
+  double replicate_ms;   /* ABI 6: wall time of the last kma_table_replicate (its copies run
+                            concurrently, one stream per destination); 0 before any         */
+  uint64_t replicate_bytes; /* ABI 6: bytes that call copied (slot array x destinations)    */
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -159,6 +162,9 @@ int kma_device_count(int* out_n);
  *                           batches of >= 2^25 residues; 0 = the probe packs ASCII itself
  *   KMA_OPT_HOST_THREADS    host calls: threads staging (copying / packing) the input
  *                           [0: min(16, cores)]; 1..64
+ *   KMA_OPT_HOST_SLICE      host protein calls: residues per device call [0: 2^31]; a replica's
+ *                           share of a larger batch is annotated as consecutive slices of
+ *                           whole proteins (tallies summed); >= 1 (tests set it low)
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -168,6 +174,7 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_HASH_SLICE 5
 #define KMA_OPT_PACKED_INPUT 6
 #define KMA_OPT_HOST_THREADS 7
+#define KMA_OPT_HOST_SLICE 8
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);
@@ -207,8 +214,11 @@ int kma_table_layout_for(int k, uint64_t n_buckets);
  * kma_table_create_replicated: kma_table_create on device_ids[0], then kma_table_replicate on
  * the others. kma_table_replicate: copy replica 0's slot array to each listed device (a peer
  * copy over xGMI between MI355X GPUs; a device may be listed twice — two replicas on one GPU,
- * each served by its own host thread and stream). kma_table_replicas: the replica count and
- * (up to cap) their devices, in shard order.                                                  */
+ * each served by its own host thread and stream). Every destination is allocated first, then
+ * all copies are issued at once, each on a stream of its destination (each GPU's copy engine
+ * pulls over its own xGMI link), and the call waits for all of them; the time and bytes are in
+ * kma_table_info. kma_table_replicas: the replica count and (up to cap) their devices, in
+ * shard order.                                                                                */
 int kma_table_create_replicated(const char* text, const uint64_t* offsets, const uint32_t* fids,
                                 uint64_t n, int k, int n_devices, const int* device_ids,
                                 double load_factor, kma_table** out);
@@ -273,7 +283,9 @@ int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phase
  * Host form: synchronous, host buffers. A batch of >= 32 MiB of residues is cut into pieces of
  * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16) whose staging (packing, under
  * KMA_OPT_PACKED_INPUT, on KMA_OPT_HOST_THREADS threads) and H2D run on the context's copy
- * stream under the previous piece's kernel.                                                   */
+ * stream under the previous piece's kernel. A replica's share of more than 2^31 residues
+ * (KMA_OPT_HOST_SLICE) is annotated as consecutive slices of whole proteins, one device call
+ * each; only a single protein longer than 2^32 - 128 residues is refused (KMA_E_INVALID).     */
 int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,
                           const uint64_t* offsets, uint32_t n_seq, int min_hits, uint32_t flags,
                           int32_t* out_fid, int32_t* out_count, uint8_t* out_status,

@@ -37,8 +37,8 @@ namespace {
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 8;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}};
+constexpr int kNumOpts = 9;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
@@ -50,6 +50,7 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_HASH_SLICE: return v >= 0;
     case KMA_OPT_PACKED_INPUT: return v >= 0 && v <= 2;
     case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
+    case KMA_OPT_HOST_SLICE: return v >= 0;
     default: return false;
   }
 }
@@ -837,31 +838,72 @@ int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
     return fail(KMA_E_INVALID, "null argument");
   const Replica src = replicas(t)[0];
   const uint64_t bytes = t->n_buckets * bucket_bytes(t->k);
-  for (int i = 0; i < n_devices; ++i) {
-    const int dev = device_ids[i];
-    int n_dev = 0;
-    if (hipGetDeviceCount(&n_dev) != hipSuccess || dev < 0 || dev >= n_dev)
-      return fail(KMA_E_INVALID, "device %d not present", dev);
+  int n_dev = 0;
+  if (hipGetDeviceCount(&n_dev) != hipSuccess) return fail(KMA_E_DEVICE, "hipGetDeviceCount");
+  for (int i = 0; i < n_devices; ++i)
+    if (device_ids[i] < 0 || device_ids[i] >= n_dev)
+      return fail(KMA_E_INVALID, "device %d not present", device_ids[i]);
+  // Every destination's slot array and copy stream first; then all copies at once (each on its
+  // destination's stream, so each GPU's copy engine pulls replica 0 over its own xGMI link
+  // instead of one link at a time); then one wait for all of them.
+  struct Dest {
+    int dev;
     uint64_t* d = nullptr;
-    {
-      DeviceScope ds(dev);
-      if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", dev);
-      KMA_HIP(hipMalloc(&d, bytes));
-      // Device 0's replica to this device: a peer copy (xGMI between MI355X GPUs).
-      hipError_t e = dev == src.device
-                         ? hipMemcpy(d, src.d_slots, bytes, hipMemcpyDeviceToDevice)
-                         : hipMemcpyPeer(d, dev, src.d_slots, src.device, bytes);
-      if (e != hipSuccess) {
-        (void)hipFree(d);
-        return fail(KMA_E_DEVICE, "replica copy to device %d: %s", dev, hipGetErrorString(e));
-      }
+    hipStream_t s = nullptr;
+  };
+  std::vector<Dest> dst(n_devices);
+  auto cleanup = [&](bool free_slots) {
+    for (Dest& x : dst) {
+      DeviceScope ds(x.dev);
+      if (x.s) (void)hipStreamDestroy(x.s);
+      if (free_slots && x.d) (void)hipFree(x.d);
+      x.s = nullptr;
     }
-    if (int rc = add_replica(t, dev, d, true)) {
-      DeviceScope ds(dev);
-      (void)hipFree(d);
-      return rc;
+  };
+  for (int i = 0; i < n_devices; ++i) {
+    Dest& x = dst[i];
+    x.dev = device_ids[i];
+    DeviceScope ds(x.dev);
+    hipError_t e = ds.err;
+    if (e == hipSuccess) e = hipMalloc(&x.d, bytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      cleanup(true);
+      return fail(e == hipErrorOutOfMemory ? KMA_E_NOMEM : KMA_E_DEVICE,
+                  "replica on device %d: %s", x.dev, hipGetErrorString(e));
     }
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e = hipSuccess;
+  for (Dest& x : dst) {
+    DeviceScope ds(x.dev);
+    e = x.dev == src.device
+            ? hipMemcpyAsync(x.d, src.d_slots, bytes, hipMemcpyDeviceToDevice, x.s)
+            : hipMemcpyPeerAsync(x.d, x.dev, src.d_slots, src.device, bytes, x.s);
+    if (e != hipSuccess) break;
+  }
+  for (Dest& x : dst) {
+    DeviceScope ds(x.dev);
+    const hipError_t w = hipStreamSynchronize(x.s);  // every issued copy, even after a failure
+    if (e == hipSuccess) e = w;
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (e != hipSuccess) {
+    cleanup(true);
+    return fail(KMA_E_DEVICE, "replica copies: %s", hipGetErrorString(e));
+  }
+  cleanup(false);
+  for (size_t i = 0; i < dst.size(); ++i)
+    if (int rc = add_replica(t, dst[i].dev, dst[i].d, true)) {
+      for (size_t j = i; j < dst.size(); ++j) {
+        DeviceScope ds(dst[j].dev);
+        (void)hipFree(dst[j].d);
+      }
+      return rc;
+    }
+  std::lock_guard<std::mutex> g(t->reps_mu);
+  t->info.replicate_ms = ms;
+  t->info.replicate_bytes = bytes * (uint64_t)n_devices;
   return KMA_OK;
 }
 
@@ -1199,7 +1241,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   double t_stage = 0, t_launch = 0;
   const uint64_t base = offsets[lo], nres = offsets[hi] - base;
   if (nres > kMaxResidues)
-    return fail(KMA_E_INVALID, "%llu residues in one device call (limit 2^32 - 128)",
+    return fail(KMA_E_INVALID, "a protein of %llu residues (limit 2^32 - 128)",
                 (unsigned long long)nres);
   HostCtx* c = nullptr;
   if (int rc = acquire_ctx(t, r.device, &c)) return rc;
@@ -1543,10 +1585,26 @@ int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const ui
   const int nr = (int)std::min<uint64_t>(reps.size(), n_seq);
   const std::vector<uint32_t> b = shard_bounds(offsets, n_seq, nr);
   std::vector<std::vector<uint32_t>> part(tally ? nr : 0, std::vector<uint32_t>(n_fid));
+  // A replica's share in slices of at most KMA_OPT_HOST_SLICE residues (default 2^31) of whole
+  // proteins, one device call each (the kernels index residues with 32 bits); slice tallies add.
+  const int64_t so = opt(KMA_OPT_HOST_SLICE);
+  const uint64_t slice = so > 0 ? (uint64_t)so : 1ull << 31;
   const int rc = fan_out(nr, [&](int i) {
-    return protein_shard(t, reps[i], residues, offsets, b[i], b[i + 1], min_hits, flags,
-                         out_fid, out_count, out_status, tally ? part[i].data() : nullptr,
-                         n_fid);
+    std::vector<uint32_t> st(tally ? n_fid : 0);
+    for (uint32_t lo = b[i]; lo < b[i + 1];) {
+      uint32_t hi = (uint32_t)(std::upper_bound(offsets + lo + 1, offsets + b[i + 1] + 1,
+                                                offsets[lo] + slice) - offsets) - 1;
+      if (hi <= lo) hi = lo + 1;  // one protein longer than a slice: a call of its own
+      const bool whole = lo == b[i] && hi == b[i + 1];
+      uint32_t* tl = !tally ? nullptr : whole ? part[i].data() : st.data();
+      if (int rc = protein_shard(t, reps[i], residues, offsets, lo, hi, min_hits, flags, out_fid,
+                                 out_count, out_status, tl, n_fid))
+        return rc;
+      if (tally && !whole)
+        for (uint32_t f = 0; f < n_fid; ++f) part[i][f] += st[f];
+      lo = hi;
+    }
+    return (int)KMA_OK;
   });
   if (rc != KMA_OK) return rc;
   for (int i = 0; i < (tally ? nr : 0); ++i)  // the tally reduce of the replicas

@@ -365,37 +365,31 @@ std::string scalar_string(Parser& ps) {  // a string or number member as text
   return ps.value().as_string();
 }
 
-// A GTO mapped read-only (the apply loader reads ~6 MB per genome, most of it contig DNA it
-// skips: mapping the page cache saves a zero-filled buffer and a copy). Falls back to a read.
-struct MappedFile {
-  const char* data = nullptr;
-  size_t size = 0;
-  std::string fallback;
-  void* map = MAP_FAILED;
-  explicit MappedFile(const std::string& path) {
-    const int fd = ::open(path.c_str(), O_RDONLY);
-    if (fd < 0) throw std::runtime_error("cannot open " + path);
-    struct stat st;
-    if (fstat(fd, &st) == 0 && st.st_size > 0)
-      map = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
-    ::close(fd);
-    if (map != MAP_FAILED) {
-      data = static_cast<const char*>(map);
-      size = (size_t)st.st_size;
-    } else {
-      fallback = slurp(path);
-      data = fallback.data();
-      size = fallback.size();
-    }
-  }
-  ~MappedFile() {
-    if (map != MAP_FAILED) ::munmap(map, size);
-  }
-  MappedFile(const MappedFile&) = delete;
-  MappedFile& operator=(const MappedFile&) = delete;
-};
 
 }  // namespace
+
+MappedFile::MappedFile(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + path);
+  struct stat st;
+  void* m = MAP_FAILED;
+  if (fstat(fd, &st) == 0 && st.st_size > 0)
+    m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  ::close(fd);
+  if (m != MAP_FAILED) {
+    map_ = m;
+    data = static_cast<const char*>(m);
+    size = (size_t)st.st_size;
+  } else {
+    fallback_ = slurp(path);
+    data = fallback_.data();
+    size = fallback_.size();
+  }
+}
+
+MappedFile::~MappedFile() {
+  if (map_) ::munmap(map_, size);
+}
 
 Genome load_genome_pegs(const std::string& path) {
   const MappedFile text(path);
@@ -404,32 +398,34 @@ Genome load_genome_pegs(const std::string& path) {
   // Reading stops once id, scientific_name, genetic_code and features have been read: SEEDtk
   // GTOs put the contigs (the DNA: most of the file) after them (small.gto's member order), so
   // their pages are never touched. A file is then not checked past that point.
+  // A member that appears twice keeps its first value, as Json::get (load_genome) does.
   unsigned seen = 0;
   const bool stopped = ps.members_until([&](std::string_view k) {
-    if (k == "id") {
+    if (k == "id" && !(seen & 1)) {
       g.id = scalar_string(ps);
       seen |= 1;
-    } else if (k == "scientific_name") {
+    } else if (k == "scientific_name" && !(seen & 2)) {
       g.name = scalar_string(ps);
       seen |= 2;
-    } else if (k == "genetic_code") {
+    } else if (k == "genetic_code" && !(seen & 4)) {
       g.genetic_code = (int)ps.value().as_int(11);
       seen |= 4;
-    } else if (k == "features") {
+    } else if (k == "features" && !(seen & 8)) {
       seen |= 8;
       ps.elements([&]() {
         Feature ft;
+        unsigned fseen = 0;
         ps.members([&](std::string_view fk) {
-          if (fk == "id") ft.id = scalar_string(ps);
-          else if (fk == "type") ft.type = scalar_string(ps);
-          else if (fk == "function") ft.function = scalar_string(ps);
-          else if (fk == "protein_translation") ft.protein = scalar_string(ps);
+          if (fk == "id" && !(fseen & 1)) ft.id = scalar_string(ps), fseen |= 1;
+          else if (fk == "type" && !(fseen & 2)) ft.type = scalar_string(ps), fseen |= 2;
+          else if (fk == "function" && !(fseen & 4)) ft.function = scalar_string(ps), fseen |= 4;
+          else if (fk == "protein_translation" && !(fseen & 8)) ft.protein = scalar_string(ps), fseen |= 8;
           else ps.skip();
         });
         g.features.push_back(std::move(ft));
       });
     } else {
-      ps.skip();  // contigs (their DNA), close genomes, subsystems, ...
+      ps.skip();  // contigs (their DNA), close genomes, subsystems, repeated members, ...
     }
     return seen == 15;
   });
@@ -480,18 +476,21 @@ Genome load_genome(const std::string& path) {
   return g;
 }
 
-std::vector<std::string> genome_files(const std::string& dir) {
+std::vector<std::string> files_with_suffix(const std::string& dir, const std::string& suffix) {
   std::vector<std::string> out;
   DIR* d = opendir(dir.c_str());
   if (!d) throw std::runtime_error("cannot list " + dir);
   while (dirent* e = readdir(d)) {
-    std::string n = e->d_name;
-    if (n.size() > 4 && n.compare(n.size() - 4, 4, ".gto") == 0) out.push_back(dir + "/" + n);
+    const std::string n = e->d_name;
+    if (n.size() > suffix.size() && n.compare(n.size() - suffix.size(), suffix.size(), suffix) == 0)
+      out.push_back(dir + "/" + n);
   }
   closedir(d);
   std::sort(out.begin(), out.end());
   return out;
 }
+
+std::vector<std::string> genome_files(const std::string& dir) { return files_with_suffix(dir, ".gto"); }
 
 KmerRows read_kmer_db(const std::string& path) {
   std::ifstream f(path, std::ios::binary);

@@ -50,6 +50,8 @@ Genome load_genome_pegs(const std::string& path);
 
 // GenomeDirectory: the *.gto files of a directory, sorted by file name.
 std::vector<std::string> genome_files(const std::string& dir);
+// The files of a directory whose names end in `suffix` (and are longer than it), sorted.
+std::vector<std::string> files_with_suffix(const std::string& dir, const std::string& suffix);
 
 // ---- text inputs of `apply` -------------------------------------------------------------------
 // TabbedLineReader(file, 2) over the headerless kmerdb.tbl: rows (col0, col1) in file order.
@@ -66,5 +68,21 @@ std::map<std::string, int> read_roles(const std::string& path, int* n_lines);
 
 bool is_directory(const std::string& path);
 bool can_read(const std::string& path);
+
+// A file mapped read-only (the apply loader reads ~6 MB per GTO, most of it contig DNA it skips;
+// the FASTA reader cuts a mapped file into segments parsed in parallel): mapping the page cache
+// saves a zero-filled buffer and a copy. Falls back to a read for what cannot be mapped.
+struct MappedFile {
+  const char* data = nullptr;
+  size_t size = 0;
+  explicit MappedFile(const std::string& path);  // throws std::runtime_error
+  ~MappedFile();
+  MappedFile(const MappedFile&) = delete;
+  MappedFile& operator=(const MappedFile&) = delete;
+
+ private:
+  std::string fallback_;
+  void* map_ = nullptr;  // the mapping (nullptr: fallback_ holds the bytes)
+};
 
 }  // namespace kma_host

@@ -29,6 +29,7 @@
 #include <thread>
 #include <vector>
 
+#include "fasta.h"
 #include "gto.h"
 #include "kmeranno.h"
 
@@ -278,8 +279,13 @@ struct ProteinBatch {
 // ---- ApplyKmerProcessor -----------------------------------------------------------------------
 class ApplyKmerProcessor {
  public:
+  // fasta: the FASTA form (`kma apply-fasta`): protein FASTA files in place of the GTO directory.
+  explicit ApplyKmerProcessor(bool fasta = false) : fasta_(fasta) {}
+
   void setDefaults() {  // :77-80
-    outputType_ = "APPLY";
+    // The FASTA form reports per sequence by default (VERIFY rows); APPLY gives a tally row per
+    // file.
+    outputType_ = fasta_ ? "VERIFY" : "APPLY";
     minHits_ = 5;
   }
 
@@ -321,16 +327,34 @@ class ApplyKmerProcessor {
       }
     }
     if (help_) return;
-    if (pos.size() != 3) throw UsageError("Argument \"kmerdb.tbl roles.in.use gtoDir\" is required");
+    if (fasta_) {
+      if (pos.size() < 3)
+        throw UsageError("Argument \"kmerdb.tbl roles.in.use proteins.faa...\" is required");
+      fastaInputs_.assign(pos.begin() + 2, pos.end());
+    } else {
+      if (pos.size() != 3) throw UsageError("Argument \"kmerdb.tbl roles.in.use gtoDir\" is required");
+      inDir_ = pos[2];
+    }
     kmerDbFile_ = pos[0];
     goodRoleFile_ = pos[1];
-    inDir_ = pos[2];
     validateParms();
   }
 
   void validateParms() {  // :83-111
-    if (!is_directory(inDir_))
+    if (fasta_) {
+      fastaFiles_.clear();
+      for (const std::string& in : fastaInputs_) {
+        if (is_directory(in)) {
+          for (const std::string& f : fasta_files(in)) fastaFiles_.push_back(f);
+        } else if (can_read(in)) {
+          fastaFiles_.push_back(in);
+        } else {
+          throw NotFound("Input FASTA file " + in + " not found or unreadable.");
+        }
+      }
+    } else if (!is_directory(inDir_)) {
       throw NotFound("Input directory " + inDir_ + " not found or invalid.");
+    }
     if (!can_read(kmerDbFile_))
       throw NotFound("Kmer database file " + kmerDbFile_ + " not found or unreadable.");
     if (minHits_ < 1) throw UsageError("Min-hits must be positive.");
@@ -372,6 +396,7 @@ class ApplyKmerProcessor {
   //   - the report thread only waits for genome i, then writes its report; batches are called
   //     on a caller thread, so a batch's call overlaps the previous batch's reports.
   void runCommand() {
+    if (fasta_) return runFasta();
     const std::vector<std::string> files = genome_files(inDir_);
     log_info("%zu genomes found in input directory.", files.size());
     const auto t0 = Clock::now();
@@ -401,15 +426,22 @@ class ApplyKmerProcessor {
           const size_t max_ready = 2 * batchGenomesHint();
           ProteinBatch b;
           std::vector<ParsedGenome> batch;
-          for (size_t i = 0; i < files.size();) {
+          std::exception_ptr take_error;  // a GTO that failed to parse ends the loop after
+          for (size_t i = 0; i < files.size() && !take_error;) {  // the genomes before it
             batch.clear();
             b.clear();
             const auto w0 = Clock::now();
             while (i < files.size() && (batch.empty() || b.residues.size() < batchResidues_)) {
-              batch.push_back(feed.take(i++));
+              try {
+                batch.push_back(feed.take(i++));
+              } catch (...) {
+                take_error = std::current_exception();
+                break;
+              }
               b.add(batch.back().pegs);
             }
             caller_wait_s += seconds(w0);
+            if (batch.empty()) break;
             ParsedGenome all;  // the batch's outputs, split back per genome below
             call(b, all, calls, call_us);
             size_t at = 0;
@@ -427,6 +459,7 @@ class ApplyKmerProcessor {
             g.unlock();
             qcv.notify_all();
           }
+          if (take_error) std::rethrow_exception(take_error);
         } catch (...) {
           caller_error = std::current_exception();
         }
@@ -508,20 +541,197 @@ class ApplyKmerProcessor {
   // One native call on the proteins of `b`; outputs into pg (fid, count, status).
   void call(const ProteinBatch& b, ParsedGenome& pg, std::atomic<uint64_t>& calls,
             std::atomic<uint64_t>& call_us) const {
-    const uint32_t n = b.size();
+    call(b.residues, b.offsets, pg, calls, call_us);
+  }
+  void call(const std::string& residues, const std::vector<uint64_t>& offsets, ParsedGenome& pg,
+            std::atomic<uint64_t>& calls, std::atomic<uint64_t>& call_us) const {
+    const uint32_t n = (uint32_t)(offsets.size() - 1);
     pg.fid.resize(n);
     pg.count.resize(n);
     pg.status.resize(n);
     if (n == 0) return;
     const auto c0 = Clock::now();
-    check(kma_annotate_proteins(table_, reinterpret_cast<const uint8_t*>(b.residues.data()),
-                                b.offsets.data(), n, minHits_, 0, pg.fid.data(), pg.count.data(),
+    check(kma_annotate_proteins(table_, reinterpret_cast<const uint8_t*>(residues.data()),
+                                offsets.data(), n, minHits_, 0, pg.fid.data(), pg.count.data(),
                                 pg.status.data(), nullptr, 0),
           "kma_annotate_proteins");
     pg.annotated = true;
     pg.call_s = seconds(c0);
     calls += 1;
     call_us += (uint64_t)(pg.call_s * 1e6);
+  }
+
+  // The FASTA form (protein FASTA as read through FastaInputStream,
+  // anno/BuildKmerProcessor.java:196-198; reader rules in host/fasta.h). Each file is one
+  // "genome" (id: the file name without its last extension): VERIFY writes one row per called
+  // sequence (genome_id, sequence id, role, hits, the header's comment as the function), APPLY
+  // one tally row per file. A file is mapped and cut at record headers into segments of about
+  // --batch bytes; a pool of threads parses segments and makes one native call per segment
+  // (concurrent host calls on one table, each on a pooled context and stream), at most
+  // 2 x threads segments ahead of this thread, which writes the segments' rows in file order.
+  void runFasta() {
+    log_info("%zu FASTA files to process.", fastaFiles_.size());
+    const auto t0 = Clock::now();
+    const bool verify = outputType_ == "VERIFY";
+    const size_t seg_bytes = batchResidues_ ? (size_t)batchResidues_ : (size_t)16 << 20;
+    std::atomic<uint64_t> calls{0}, call_us{0}, parse_us{0}, format_us{0};
+    uint64_t n_seq = 0, n_res = 0, n_called = 0, n_bytes = 0, n_segs_all = 0;
+    double wait_s = 0, write_s = 0;
+    int n_threads = 1;
+    struct Segment {
+      FastaSegment recs;
+      ParsedGenome out;
+      std::string text;  // VERIFY rows
+      std::string err;
+    };
+    for (const std::string& path : fastaFiles_) {
+      const MappedFile file(path);
+      Genome g;
+      g.id = g.name = fasta_genome_id(path);
+      log_info("Processing FASTA file %s (%s).", path.c_str(), g.id.c_str());
+      reporter_->openGenome(g);
+      const std::vector<size_t> bounds = fasta_segment_bounds(file.data, file.size, seg_bytes);
+      const size_t n_segs = bounds.size() - 1;
+      std::vector<Segment> segs(n_segs);
+      std::vector<char> ready(n_segs, 0);
+      std::mutex mu;
+      std::condition_variable cv;
+      size_t next = 0, taken = 0;
+      bool stop = false;
+      const size_t lookahead = 2 * (size_t)parseThreads_;
+      auto work = [&] {
+        for (;;) {
+          size_t i;
+          {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return stop || (next < n_segs && next < taken + lookahead); });
+            if (stop || next >= n_segs) return;
+            i = next++;
+          }
+          Segment& s = segs[i];
+          try {
+            const auto p0 = Clock::now();
+            parse_fasta_segment(file.data + bounds[i], file.data + bounds[i + 1], s.recs);
+            parse_us += (uint64_t)(seconds(p0) * 1e6);
+            call(s.recs.residues, s.recs.offsets, s.out, calls, call_us);
+            if (verify) {
+              const auto f0 = Clock::now();
+              format_verify(g.id, s);
+              format_us += (uint64_t)(seconds(f0) * 1e6);
+            }
+          } catch (const std::exception& e) {
+            s.err = *e.what() ? e.what() : "failure";
+          }
+          {
+            std::lock_guard<std::mutex> g(mu);
+            ready[i] = 1;
+          }
+          cv.notify_all();
+        }
+      };
+      std::vector<std::thread> pool;
+      n_threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)parseThreads_, n_segs));
+      for (int t = 0; t < n_threads; ++t) pool.emplace_back(work);
+      struct Join {  // a failing segment stops the pool before unwinding
+        std::vector<std::thread>& pool;
+        std::mutex& mu;
+        std::condition_variable& cv;
+        bool& stop;
+        ~Join() {
+          {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+          }
+          cv.notify_all();
+          for (auto& t : pool) t.join();
+        }
+      } join{pool, mu, cv, stop};
+      Feature dummy;
+      for (size_t i = 0; i < n_segs; ++i) {
+        const auto w0 = Clock::now();
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [&] { return ready[i] != 0; });
+        }
+        wait_s += seconds(w0);
+        Segment& s = segs[i];
+        if (!s.err.empty()) throw std::runtime_error(path + ": " + s.err);
+        const auto r0 = Clock::now();
+        const uint32_t n = s.recs.size();
+        if (verify) {
+          std::fwrite(s.text.data(), 1, s.text.size(), stdout);
+        } else {
+          for (uint32_t j = 0; j < n; ++j)
+            if (s.out.status[j] == KMA_STATUS_CALLED)
+              reporter_->recordFeature(dummy, (uint32_t)s.out.fid[j], db_.roles[s.out.fid[j]],
+                                       s.out.count[j]);
+        }
+        for (uint32_t j = 0; j < n; ++j) n_called += s.out.status[j] == KMA_STATUS_CALLED;
+        n_seq += n;
+        n_res += s.recs.residues.size();
+        write_s += seconds(r0);
+        {
+          std::lock_guard<std::mutex> g(mu);
+          taken = i + 1;
+        }
+        cv.notify_all();
+        s = Segment();  // free as we go
+      }
+      reporter_->closeGenome();
+      n_bytes += file.size;
+      n_segs_all += n_segs;
+    }
+    reporter_->closeReport();
+    std::fflush(stdout);
+    const double wall = seconds(t0);
+    std::fprintf(stderr,
+                 "[kma] apply-fasta-stats {\"files\": %zu, \"sequences\": %llu, \"residues\": "
+                 "%llu, \"called\": %llu, \"bytes\": %llu, \"segments\": %llu, \"calls\": %llu, "
+                 "\"loop_s\": %.6f, \"native_call_s\": %.6f, \"parse_s\": %.6f, \"format_s\": "
+                 "%.6f, \"report_wait_s\": %.6f, \"write_s\": %.6f, \"threads\": %d, "
+                 "\"segment_bytes\": %zu, \"format\": \"%s\", \"table_load_s\": %.6f}\n",
+                 fastaFiles_.size(), (unsigned long long)n_seq, (unsigned long long)n_res,
+                 (unsigned long long)n_called, (unsigned long long)n_bytes,
+                 (unsigned long long)n_segs_all, (unsigned long long)calls.load(), wall,
+                 call_us.load() * 1e-6, parse_us.load() * 1e-6, format_us.load() * 1e-6, wait_s,
+                 write_s, n_threads, seg_bytes, outputType_.c_str(), tableLoadS_);
+  }
+
+  // VerifyApplyKmerReporter's rows (rep/VerifyApplyKmerReporter.java:42-45) of one segment's
+  // called sequences: genome_id, peg_id (the FASTA label), role, hits, function (the comment).
+  template <class Segment>
+  void format_verify(const std::string& gid, Segment& s) const {
+    std::string& t = s.text;
+    char num[16];
+    for (uint32_t j = 0; j < s.recs.size(); ++j) {
+      if (s.out.status[j] != KMA_STATUS_CALLED) continue;
+      t += gid;
+      t += '\t';
+      t += s.recs.ids[j];
+      t += '\t';
+      t += db_.roles[s.out.fid[j]];
+      t += '\t';
+      t.append(num, (size_t)std::snprintf(num, sizeof num, "%d", s.out.count[j]));
+      t += '\t';
+      t += s.recs.comments[j];
+      t += '\n';
+    }
+  }
+
+  // A FASTA file's "genome id": its name without directories and without its last extension.
+  static std::string fasta_genome_id(const std::string& path) {
+    std::string n = path.substr(path.find_last_of('/') == std::string::npos ? 0 : path.find_last_of('/') + 1);
+    const size_t dot = n.find_last_of('.');
+    return dot == std::string::npos || dot == 0 ? n : n.substr(0, dot);
+  }
+
+  // The FASTA files of a directory (*.faa, *.fa, *.fasta), sorted by name.
+  static std::vector<std::string> fasta_files(const std::string& dir) {
+    std::vector<std::string> out;
+    for (const char* ext : {".faa", ".fa", ".fasta"})
+      for (const std::string& f : files_with_suffix(dir, ext)) out.push_back(f);
+    std::sort(out.begin(), out.end());
+    return out;
   }
 
   bool help() const { return help_; }
@@ -544,6 +754,8 @@ class ApplyKmerProcessor {
   uint64_t batchResidues_ = 16u << 20;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
+  const bool fasta_;
+  std::vector<std::string> fastaInputs_, fastaFiles_;
   std::unique_ptr<ApplyKmerReporter> reporter_;
   KmerRows db_;
   kma_table* table_ = nullptr;
@@ -562,11 +774,23 @@ const char* kApplyUsage =
     " --batch R         consecutive genomes batched into native calls of >= R residues\n"
     "                   (default 16777216); 0: each parser thread makes its genome's call\n";
 
-int run_apply(const std::vector<std::string>& args) {
-  ApplyKmerProcessor p;
+const char* kApplyFastaUsage =
+    "kma apply-fasta [options] kmerdb.tbl roles.in.use proteins.faa|dir ...\n"
+    "  apply a discriminating-kmer database to protein FASTA files (each file: one genome)\n"
+    " -h, --help        display command-line usage\n"
+    " -v, --verbose     display more frequent progress messages on the log\n"
+    " -m, --min N       minimum number of hits required to call a role (default 5)\n"
+    " --format FMT      VERIFY (default): a row per called sequence; APPLY: a row per file\n"
+    " --device D        HIP device ordinal (default 0)\n"
+    " --threads N       parser / caller threads (default min(16, cores))\n"
+    " --staging-threads N  library threads packing a call's residues (default: min(16, cores))\n"
+    " --batch B         bytes of FASTA per segment (one native call each; default 16777216)\n";
+
+int run_apply(const std::vector<std::string>& args, bool fasta = false) {
+  ApplyKmerProcessor p(fasta);
   p.parseCommand(args);
   if (p.help()) {
-    std::fputs(kApplyUsage, stderr);
+    std::fputs(fasta ? kApplyFastaUsage : kApplyUsage, stderr);
     return 0;
   }
   p.runCommand();
@@ -630,9 +854,42 @@ int run_gto_dump(const std::vector<std::string>& args) {
   return 0;
 }
 
+// `kma fasta-dump [--batch B] file.faa`: the records the FASTA form reads (host/fasta.h), one
+// per line (label, comment, sequence), parsed in segments of about B bytes (default 16 MiB) as
+// apply-fasta cuts them; no device needed (tests compare it with a restatement of the reader).
+int run_fasta_dump(const std::vector<std::string>& args) {
+  size_t seg = (size_t)16 << 20;
+  std::vector<std::string> pos;
+  for (size_t i = 0; i < args.size(); ++i) {
+    if (args[i] == "--batch" && i + 1 < args.size()) seg = std::strtoull(args[++i].c_str(), nullptr, 10);
+    else pos.push_back(args[i]);
+  }
+  if (pos.size() != 1) throw UsageError("usage: kma fasta-dump [--batch B] file.faa");
+  if (!can_read(pos[0])) throw NotFound("Input FASTA file " + pos[0] + " not found or unreadable.");
+  const MappedFile file(pos[0]);
+  const std::vector<size_t> b = fasta_segment_bounds(file.data, file.size, seg);
+  std::string out;
+  for (size_t i = 0; i + 1 < b.size(); ++i) {
+    FastaSegment s;
+    parse_fasta_segment(file.data + b[i], file.data + b[i + 1], s);
+    for (uint32_t j = 0; j < s.size(); ++j) {
+      out.append(s.ids[j]);
+      out += '\t';
+      out.append(s.comments[j]);
+      out += '\t';
+      out.append(s.residues, s.offsets[j], s.offsets[j + 1] - s.offsets[j]);
+      out += '\n';
+    }
+  }
+  std::fwrite(out.data(), 1, out.size(), stdout);
+  std::fprintf(stderr, "[kma] fasta-dump segments %zu\n", b.size() - 1);
+  return 0;
+}
+
 const char* kCommands =
     "Valid commands are\n"
     "  apply     apply a discriminating-kmer database to genomes to create a role-count file\n"
+    "  apply-fasta  the same on protein FASTA files (a row per called sequence)\n"
     "  contigs   6-frame contig kmers probed against a discriminating-kmer database\n";
 
 }  // namespace
@@ -646,8 +903,10 @@ int main(int argc, char** argv) {
   std::vector<std::string> rest(argv + 2, argv + argc);
   try {
     if (command == "apply") return run_apply(rest);
+    if (command == "apply-fasta") return run_apply(rest, true);
     if (command == "contigs") return run_contigs(rest);
     if (command == "gto-dump") return run_gto_dump(rest);
+    if (command == "fasta-dump") return run_fasta_dump(rest);
     if (command == "-h" || command == "--help") {
       std::fputs(kCommands, stdout);
       return 0;
@@ -655,7 +914,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "Invalid command %s.\n", command.c_str());  // App.java:301
     return 1;
   } catch (const UsageError& e) {
-    std::fprintf(stderr, "%s\n%s", e.what(), command == "apply" ? kApplyUsage : "");
+    std::fprintf(stderr, "%s\n%s", e.what(),
+                 command == "apply" ? kApplyUsage : command == "apply-fasta" ? kApplyFastaUsage : "");
     return 2;
   } catch (const NotFound& e) {
     std::fprintf(stderr, "java.io.FileNotFoundException: %s\n", e.what());

@@ -43,13 +43,14 @@ EXPORTS = (
 
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
-OPT_PACKED_INPUT, OPT_HOST_THREADS = 6, 7
+OPT_PACKED_INPUT, OPT_HOST_THREADS, OPT_HOST_SLICE = 6, 7, 8
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
-                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0}
+                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0, OPT_HOST_SLICE: 0}
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
 _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
               "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
-              "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS}
+              "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS,
+              "host_slice": OPT_HOST_SLICE}
 
 
 class KmerAnnoError(RuntimeError):
@@ -64,7 +65,8 @@ class TableInfo(C.Structure):
                 ("device", C.c_int32), ("max_probe", C.c_uint32), ("n_extra_syms", C.c_uint32),
                 ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32),
                 ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32),
-                ("slots_per_bucket", C.c_int32)]
+                ("slots_per_bucket", C.c_int32), ("replicate_ms", C.c_double),
+                ("replicate_bytes", C.c_uint64)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),

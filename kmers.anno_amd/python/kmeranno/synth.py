@@ -177,6 +177,39 @@ def write_roles_in_use(path: str, n_fid: int, every: int = 1):
         f.writelines(f"{role_name(i)}\tsynthetic role {i}\n" for i in range(0, n_fid, every))
 
 
+def write_fasta(path: str, residues: np.ndarray, offsets: np.ndarray, ids, comments=None,
+                width: int = 60, chunk: int = 65536) -> int:
+    """Protein FASTA (">id comment" headers, sequence lines of `width` residues) of the
+    proteins [offsets[i], offsets[i+1]) of `residues`; vectorized over chunks of records (c4's
+    1M proteins in a few seconds). Returns the file's size in bytes."""
+    n = len(offsets) - 1
+    total = 0
+    with open(path, "wb") as f:
+        for a in range(0, n, chunk):
+            b = min(n, a + chunk)
+            off = np.asarray(offsets[a:b + 1], np.int64)
+            m = b - a
+            lens = np.diff(off)
+            heads = [f">{ids[i]}" + (f" {comments[i]}" if comments is not None and comments[i]
+                                     else "") + "\n" for i in range(a, b)]
+            hb = np.frombuffer("".join(heads).encode(), np.uint8)
+            hlen = np.fromiter((len(h) for h in heads), np.int64, m)  # ASCII: chars == bytes
+            lines = (lens + width - 1) // width
+            start = np.zeros(m + 1, np.int64)
+            np.cumsum(hlen + lens + lines, out=start[1:])
+            out = np.full(int(start[-1]), ord("\n"), np.uint8)  # unwritten slots: line ends
+            hstart = np.zeros(m + 1, np.int64)
+            np.cumsum(hlen, out=hstart[1:])
+            rec = np.repeat(np.arange(m), hlen)
+            out[start[rec] + (np.arange(len(hb)) - hstart[rec])] = hb
+            rec = np.repeat(np.arange(m), lens)
+            p = np.arange(int(off[-1] - off[0]), dtype=np.int64) - (off[rec] - off[0])
+            out[start[rec] + hlen[rec] + p + p // width] = residues[int(off[0]):int(off[-1])]
+            f.write(out.tobytes())
+            total += len(out)
+    return total
+
+
 def write_genome_dir(out_dir: str, sig: SignatureSet, n_genomes: int, pegs_per_genome: int,
                      seed: int, contig_bp: int = 0, first: int = 0) -> list:
     """Synthetic GTO files for `apply` (small.gto-like, in its member order: features of type

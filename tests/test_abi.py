@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 5
+    assert native_lib.kma_abi_version() == 6
     assert isinstance(native_lib.kma_last_error(), bytes)
 
 
@@ -39,15 +39,15 @@ def test_options_set_get_validate_restore(native_lib):
         assert k.get_option(o) == v
     for o, bad in ((k.OPT_LAYOUT, 5), (k.OPT_BLOCK_PROTEINS, 9), (k.OPT_DEFER, 65),
                    (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 3),
-                   (k.OPT_HOST_THREADS, 65), (99, 0)):
+                   (k.OPT_HOST_THREADS, 65), (k.OPT_HOST_SLICE, -1), (99, 0)):
         with pytest.raises(k.KmerAnnoError) as e:
             k.set_option(o, bad)
         assert e.value.code == k.E_INVALID
     with k.options(layout=7, block_proteins=1, defer=0, host_pieces=3, hash_slice=1000,
-                   packed_input=0, host_threads=4):
-        assert [k.get_option(o) for o in range(1, 8)] == [7, 1, 0, 3, 1000, 0, 4]
+                   packed_input=0, host_threads=4, host_slice=12345):
+        assert [k.get_option(o) for o in range(1, 9)] == [7, 1, 0, 3, 1000, 0, 4, 12345]
         assert k.layout_for(8, 1000) == 7
-    assert [k.get_option(o) for o in range(1, 8)] == [-1, 0, -1, 0, 0, 1, 0]
+    assert [k.get_option(o) for o in range(1, 9)] == [-1, 0, -1, 0, 0, 1, 0, 0]
     assert k.layout_for(8, 1000) == 6
     src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
     assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src

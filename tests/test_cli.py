@@ -143,6 +143,34 @@ def test_kma_apply_genome_directory_batched(kma_bin, oracle_c, tmp_path, threads
     assert out.stdout.splitlines() == exp_verify
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [0, 1, 1 << 24])
+def test_kma_apply_corrupt_gto_mid_directory(kma_bin, oracle_c, tmp_path, batch):
+    """A GTO that fails to parse in the middle of the directory: every genome before it is
+    reported (as the reference's in-order loop does before its exception,
+    ApplyKmerProcessor.java:116-151), then the command fails naming the file; in every call
+    mode (a call per parse worker, a call per genome, one batch holding all of them)."""
+    from kmeranno import synth
+    sig = synth.make_table(100_000, 200, 6, 8)
+    gdir = tmp_path / "gtos"
+    genomes = synth.write_genome_dir(str(gdir), sig, 8, 300, seed=4)
+    synth.write_kmer_db(str(tmp_path / "db.tbl"), sig.keys, sig.fids)
+    synth.write_roles_in_use(str(tmp_path / "roles"), 200, every=1)
+    bad = gdir / f"{genomes[5][0]}.gto"
+    bad.write_text(bad.read_text()[:5000])  # truncated JSON
+    ot = oracle_c.Table([synth.unpack_key(x) for x in sig.keys], sig.fids.astype(np.int32))
+    exp = []
+    for gid, res, off in genomes[:5]:
+        fid, _, st = oracle_c.apply(ot, res, off, 8, 5, 0)
+        counts = np.bincount(fid[st == 1], minlength=200)
+        exp.append(gid + "\t" + "\t".join(map(str, counts.tolist())))
+    out = subprocess.run([kma_bin, "apply", "--batch", str(batch), str(tmp_path / "db.tbl"),
+                          str(tmp_path / "roles"), str(gdir)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 1 and bad.name in out.stderr, out.stderr
+    assert out.stdout.splitlines() == exp
+
+
 def test_kma_apply_errors(kma_bin, apply_inputs, tmp_path):
     d, _, _, _ = apply_inputs
     r = subprocess.run([kma_bin, "apply", str(d / "kmerdb.tbl"), str(d / "roles.in.use"),

@@ -274,6 +274,28 @@ def test_replicated_table_host_fan_out(kma, oracle_c, path):
     assert (ref[2] == est).all() and (ref[0] == efid).all() and (ref[1] == ecnt).all()
 
 
+@pytest.mark.parametrize("slice_res,devs", [(50_000, [0]), (137_777, [0, 0]), (1, [0])])
+def test_host_call_slices_large_shares(kma, oracle_c, slice_res, devs):
+    """A replica's share larger than KMA_OPT_HOST_SLICE residues (2^31 by default: the kernels
+    index residues with 32 bits) is annotated as consecutive slices of whole proteins, one
+    device call each, instead of being refused; outputs and the tally (summed over slices and
+    replicas) equal the oracle's. Slice 1: every protein a call of its own."""
+    from kmeranno import synth
+    n = 300 if slice_res == 1 else 3000
+    wl = synth.make_workload(n, 100_000, 500, seed=37)
+    assert slice_res == 1 or wl.offsets[-1] > 4 * slice_res
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    with kma.SignatureTable.from_rows_replicated(kmers, wl.fids, devs, K) as t:
+        with kma.options(host_slice=slice_res):
+            fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0,
+                                                        n_fid=500)
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
+    assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    assert (tally == np.bincount(efid[est == 1], minlength=500)).all()
+    assert (st == 1).sum() > 0.2 * n
+
+
 def test_concurrent_host_callers(kma):
     """Concurrent host calls on one table (each takes its own pooled context and stream)."""
     import threading
