@@ -250,12 +250,20 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
             f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
             f"built in {ms:.1f} ms")
         del winner, keys, fids
+    bcast_ms = None
     if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
         kdist.broadcast_table(slots, src=0)  # RCCL over xGMI (host-staged under gloo)
         kdist.broadcast(layout, src=0)
         torch.cuda.synchronize()
+        bcast_ms = (time.perf_counter() - t0) * 1e3
     m = int(layout.item())
-    return kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m), slots
+    table = kmeranno.SignatureTable.wrap_device(slots.data_ptr(), nb, K, dev.index, m)
+    # the replica's broadcast (this rank's wall time from a common barrier to its copy landing)
+    table.broadcast_ms = bcast_ms
+    return table, slots
 
 
 def timed(step, ws, args, world, stream, dev, before=None, after=None):
@@ -289,12 +297,33 @@ def timed(step, ws, args, world, stream, dev, before=None, after=None):
     n_t, phases = ws.phases_read()
     ws.timing(False)
     names = list(phases)
-    stats = torch.tensor([elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names],
-                         dtype=torch.float64, device=dev)
+    mine = [elapsed, gpu_ms] + [phases[k] / max(n_t, 1) for k in names]
+    stats = torch.tensor(mine, dtype=torch.float64, device=dev)
     if world > 1:
         kdist.all_reduce_max(stats)
     v = stats.tolist()
+    timed.ranks = rank_report(mine, args, world, dev)
     return v[0], v[1], dict(zip(names, v[2:]))
+
+
+def rank_report(mine, args, world, dev):
+    """The ranks that joined the timed region (rank, local rank, host, device and its PCI bus),
+    each with its own ms per step and main-kernel ms, gathered on rank 0 (None elsewhere and on
+    one rank): a scaling record explains itself — which GPUs ran and which one was slowest."""
+    if world == 1:
+        return None
+    import socket
+    try:
+        props = torch.cuda.get_device_properties(dev)
+        name, bus = props.name, getattr(props, "pci_bus_id", None)
+    except Exception:  # noqa: BLE001 - identity is best effort
+        name, bus = None, None
+    me = {"rank": int(os.environ.get("RANK", "0")),
+          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "host": socket.gethostname(),
+          "device_index": dev.index, "device": name, "pci_bus_id": bus,
+          "ms_per_step": mine[0] * 1e3 / args.steps,
+          "kernel_ms": mine[2] if len(mine) > 2 else None}
+    return kdist.gather_objects(me)
 
 
 def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows, live=True):
@@ -450,6 +479,8 @@ def bench_contigs(args, rank, world, dev, stream, sp):
                                  n_probe * BYTES_PER_LOOKUP + n_bases + 16 * n_hits,
                                  table.info.bytes, n_probe),
         }
+        if world > 1:
+            add_rank_fields(out, table, args)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_contigs(wl)
         print(json.dumps(out), flush=True)
@@ -734,6 +765,8 @@ def main():
     ap.add_argument("--load-factor", type=float, default=0.5)
     ap.add_argument("--n-seq", type=int, default=0,
                     help="override the workload's proteins per rank (tuning runs only)")
+    ap.add_argument("--table-rows", type=int, default=0,
+                    help="override the workload's table rows (tests and tuning runs only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the gather ceiling and the host-path (e2e) measurement")
@@ -783,6 +816,7 @@ def main():
 
     n_seq, t_size, n_fid, seed = synth.CONFIGS[args.workload]
     n_seq = args.n_seq or n_seq
+    t_size = args.table_rows or t_size
     strong = args.workload == "c4"
     t0 = time.perf_counter()
     sig = synth.make_table(t_size, n_fid, seed, K, protos_only=rank != 0)
@@ -858,6 +892,8 @@ def main():
         }
         out["roofline"] = protein_roofline(ph, args.workload, m, n_win, n_res, table.info.bytes,
                                            live=not args.no_extras)
+        if world > 1:
+            add_rank_fields(out, table, args)
         if world == 1:
             if not args.no_extras:
                 ms = e2e_host(table, residues, offsets, n_fid)
@@ -884,6 +920,24 @@ def main():
         dist.destroy_process_group()
     if verify is not None and not verify["ok"]:
         sys.exit(1)
+
+
+def add_rank_fields(out, table, args):
+    """Multi-rank lines: the joined ranks (timed.ranks), the spread of their step times and the
+    table broadcast's time (rank 0's wall time from a barrier until its copy completed; the
+    broadcast sends table.info.bytes to every other rank)."""
+    ranks = getattr(timed, "ranks", None) or []
+    out["ranks"] = ranks
+    steps = [r["ms_per_step"] for r in ranks]
+    if steps:
+        out["rank_ms_per_step_min"] = min(steps)
+        out["rank_ms_per_step_max"] = max(steps)
+        out["devices_distinct"] = len({(r["host"], r["pci_bus_id"], r["device_index"])
+                                        for r in ranks})
+    ms = getattr(table, "broadcast_ms", None)
+    out["table_broadcast"] = {"ms": ms, "bytes": table.info.bytes, "backend": args.dist_backend,
+                              "GBps_per_receiver": table.info.bytes / (ms * 1e-3) / 1e9
+                              if ms else None}
 
 
 def collective_note(args, world: int) -> str:

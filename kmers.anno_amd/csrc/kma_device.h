@@ -133,7 +133,7 @@ __device__ __forceinline__ void scan_half(const uint4 (&q)[4], int half, uint64_
 constexpr int kWalkGroup = KMA_WALK_GROUP;
 __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, uint32_t n_buckets,
                                            uint32_t b, uint64_t key, uint32_t& fid,
-                                           uint32_t& sid) {
+                                           uint32_t& sid, uint32_t* walked = nullptr) {
   bool hit = false, empty = false;
   const uint32_t home = b;
   uint32_t slot = 0, steps = 1;
@@ -165,6 +165,7 @@ __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, u
       ++steps;
     }
   }
+  if (walked) *walked = steps - 1;  // chain buckets scanned (tuning counters)
   return hit;
 }
 

@@ -178,7 +178,8 @@ __device__ uint64_t g_block_clk[8 * 65536];
 // Tuning builds only (make variant VNAME=count VFLAGS=-DKMA_TUNE_COUNT): wave-level event
 // counts of the protein launches since the last reset (kma_debug_walk_stats): 0 chain flushes,
 // 1 queued walks, 2 probed windows, 3 home-bucket hits, 4 walk hits, 5 walk hits in the
-// chain's first bucket.
+// chain's first bucket, 6 chain buckets loaded by walks, 7 the sum over flush passes of the
+// longest walk (buckets) in the pass.
 __device__ unsigned long long g_walk_stats[8];
 #define KMA_COUNT(i, v)                                                                    \
   do {                                                                                     \
@@ -501,12 +502,20 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     __builtin_amdgcn_wave_barrier();  // queue writes of other lanes are visible (LDS in order)
     KMA_COUNT(0, 1);
     KMA_COUNT(1, cn);
+#ifdef KMA_TUNE_COUNT
+    uint32_t wsum = 0, wmax = 0;
+#endif
     for (uint32_t e = lane; e < cn; e += 64) {
       const uint32_t w2 = cq[2 * e + 1];
       const uint64_t key = (uint64_t)(w2 & 0xFFu) << 32 | cq[2 * e];
       const uint32_t p = w2 >> 8;
       uint32_t fid = 0, sid = 0;
+#ifdef KMA_TUNE_COUNT
+      uint32_t walked = 0;
+      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid, &walked);
+#else
       const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid);
+#endif
       if (hit) record_hit<P>(sm, a, span_lo, multiset, p, fid, sid);
 #ifdef KMA_TUNE_COUNT
       {
@@ -514,9 +523,15 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
         const bool first = hit && sid / kSlotsPerBucket == s1;  // resolved in chain step 1
         KMA_COUNT(4, __popcll(__ballot(hit)));
         KMA_COUNT(5, __popcll(__ballot(first)));
+        wsum += walked;
+        wmax = walked > wmax ? walked : wmax;
       }
 #endif
     }
+#ifdef KMA_TUNE_COUNT
+    KMA_COUNT(6, wave_sum(wsum));  // chain buckets loaded by walks (converged here)
+    KMA_COUNT(7, wave_max(wmax));  // the flush waits for its longest walk
+#endif
     __builtin_amdgcn_wave_barrier();
     cn = 0;
   };

@@ -276,6 +276,34 @@ struct ProteinBatch {
   uint32_t size() const { return (uint32_t)(offsets.size() - 1); }
 };
 
+// A counting semaphore (C++17) and its scoped slot.
+class Semaphore {
+ public:
+  explicit Semaphore(int n) : n_(std::max(1, n)) {}
+  void acquire() {
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] { return n_ > 0; });
+    --n_;
+  }
+  void release() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++n_;
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  int n_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+struct CallSlot {
+  Semaphore& s;
+  explicit CallSlot(Semaphore& sem) : s(sem) { s.acquire(); }
+  ~CallSlot() { s.release(); }
+};
+
 // ---- ApplyKmerProcessor -----------------------------------------------------------------------
 class ApplyKmerProcessor {
  public:
@@ -320,6 +348,8 @@ class ApplyKmerProcessor {
         stagingThreads_ = std::max(0, std::atoi(need("--staging-threads").c_str()));
       } else if (a == "--batch") {
         batchResidues_ = std::strtoull(need("--batch").c_str(), nullptr, 10);
+      } else if (a == "--callers" && fasta_) {
+        callers_ = std::max(1, std::atoi(need("--callers").c_str()));
       } else if (!a.empty() && a[0] == '-' && a.size() > 1) {
         throw UsageError("\"" + a + "\" is not a valid option");
       } else {
@@ -594,6 +624,7 @@ class ApplyKmerProcessor {
       const size_t n_segs = bounds.size() - 1;
       std::vector<Segment> segs(n_segs);
       std::vector<char> ready(n_segs, 0);
+      Semaphore callers(callers_);
       std::mutex mu;
       std::condition_variable cv;
       size_t next = 0, taken = 0;
@@ -613,7 +644,10 @@ class ApplyKmerProcessor {
             const auto p0 = Clock::now();
             parse_fasta_segment(file.data + bounds[i], file.data + bounds[i + 1], s.recs);
             parse_us += (uint64_t)(seconds(p0) * 1e6);
-            call(s.recs.residues, s.recs.offsets, s.out, calls, call_us);
+            {
+              CallSlot slot(callers);  // at most --callers native calls at once
+              call(s.recs.residues, s.recs.offsets, s.out, calls, call_us);
+            }
             if (verify) {
               const auto f0 = Clock::now();
               format_verify(g.id, s);
@@ -689,12 +723,13 @@ class ApplyKmerProcessor {
                  "%llu, \"called\": %llu, \"bytes\": %llu, \"segments\": %llu, \"calls\": %llu, "
                  "\"loop_s\": %.6f, \"native_call_s\": %.6f, \"parse_s\": %.6f, \"format_s\": "
                  "%.6f, \"report_wait_s\": %.6f, \"write_s\": %.6f, \"threads\": %d, "
-                 "\"segment_bytes\": %zu, \"format\": \"%s\", \"table_load_s\": %.6f}\n",
+                 "\"segment_bytes\": %zu, \"callers\": %d, \"format\": \"%s\", "
+                 "\"table_load_s\": %.6f}\n",
                  fastaFiles_.size(), (unsigned long long)n_seq, (unsigned long long)n_res,
                  (unsigned long long)n_called, (unsigned long long)n_bytes,
                  (unsigned long long)n_segs_all, (unsigned long long)calls.load(), wall,
                  call_us.load() * 1e-6, parse_us.load() * 1e-6, format_us.load() * 1e-6, wait_s,
-                 write_s, n_threads, seg_bytes, outputType_.c_str(), tableLoadS_);
+                 write_s, n_threads, seg_bytes, callers_, outputType_.c_str(), tableLoadS_);
   }
 
   // VerifyApplyKmerReporter's rows (rep/VerifyApplyKmerReporter.java:42-45) of one segment's
@@ -751,6 +786,7 @@ class ApplyKmerProcessor {
   bool help_ = false;
   int parseThreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   int stagingThreads_ = -1;  // KMA_OPT_HOST_THREADS for this run (-1: the library's default)
+  int callers_ = 2;          // FASTA form: native calls in flight at once
   uint64_t batchResidues_ = 16u << 20;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
@@ -784,7 +820,8 @@ const char* kApplyFastaUsage =
     " --device D        HIP device ordinal (default 0)\n"
     " --threads N       parser / caller threads (default min(16, cores))\n"
     " --staging-threads N  library threads packing a call's residues (default: min(16, cores))\n"
-    " --batch B         bytes of FASTA per segment (one native call each; default 16777216)\n";
+    " --batch B         bytes of FASTA per segment (one native call each; default 16777216)\n"
+    " --callers C       segments' native calls in flight at once (default 2)\n";
 
 int run_apply(const std::vector<std::string>& args, bool fasta = false) {
   ApplyKmerProcessor p(fasta);

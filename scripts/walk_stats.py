@@ -44,13 +44,17 @@ def main():
     torch.cuda.synchronize()
     assert lib.kma_debug_walk_stats(st.ctypes.data_as(C.c_void_p), 1) == 0
     n_win = int(np.maximum(np.diff(offsets).astype(np.int64) - K + 1, 0).sum())
-    names = ["flushes", "queued_walks", "probed_windows", "home_hits", "walk_hits", "walk_hits_step1"]
+    names = ["flushes", "queued_walks", "probed_windows", "home_hits", "walk_hits", "walk_hits_step1",
+             "walk_buckets", "flush_longest_sum"]
     out = {"workload": wl, "load_factor": lf, "windows": n_win, "table": table.stats()
            if hasattr(table, "stats") else None}
     out.update({n: int(st[i]) for i, n in enumerate(names)})
     out["walks_per_probed"] = out["queued_walks"] / max(out["probed_windows"], 1)
     out["walk_hit_frac"] = out["walk_hits"] / max(out["queued_walks"], 1)
     out["walks_per_flush"] = out["queued_walks"] / max(out["flushes"], 1)
+    out["buckets_per_walk"] = out["walk_buckets"] / max(out["queued_walks"], 1)
+    out["walk_buckets_per_probed"] = out["walk_buckets"] / max(out["probed_windows"], 1)
+    out["longest_per_flush"] = out["flush_longest_sum"] / max(out["flushes"], 1)
     print(json.dumps(out), flush=True)
 
 
