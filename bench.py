@@ -39,6 +39,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import subprocess
@@ -238,17 +239,19 @@ def build_table(keys_np, fids_np, t_size, load_factor, dev, sp, rank, world):
             te.record()
             torch.cuda.synchronize()
             st = status.cpu().numpy().astype(np.int64)
-            assert st[0] == 0, "table full"
+            assert st[0] == 0 or m & kmeranno.LAYOUT_TWO_CHOICE, "table full"
             times[m] = tb.elapsed_time(te)
             return st
 
-        # the library creators' rule (size rule, then m = 7 / flat rebuilds by measurement)
+        # the library creators' rule (two-choice placement, else size rule then m = 7 / flat
+        # rebuilds by measurement)
         m, st = kmeranno.choose_layout(K, nb, build)
+        assert st[0] == 0, "table full"
         ms = times[m]
         layout.fill_(m)
         log(f"[rank 0] table: {st[1]} entries, {nb} buckets ({nb * 8 * kmeranno.bucket_slots() / 2**20:.0f} MiB), "
-            f"layout m={m}, longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, "
-            f"built in {ms:.1f} ms")
+            f"layout m={m & 0xFF}{' two-choice' if m & kmeranno.LAYOUT_TWO_CHOICE else ''}, "
+            f"longest chain {st[2]}, displaced {st[3] / max(st[1], 1):.2%}, built in {ms:.1f} ms")
         del winner, keys, fids
     bcast_ms = None
     if world > 1:
@@ -651,8 +654,8 @@ def bench_fasta(args):
                                    "FASTA file of c4's 1M proteins vs the 10^7-row table",
                        "proteins": n_seq, "residues": int(off[-1]), "fasta_bytes": fbytes,
                        "windows": n_win, "table_entries": t_size, "k": K, "min_hits": MIN_HITS,
-                       "line_width": 60, "parallelism": "one GPU; segments of 16 MiB parsed and "
-                                                        "called on 16 host threads"},
+                       "line_width": 60, "parallelism": "one GPU; 4 MiB segments parsed on 16 "
+                                                        "host threads, 2 native calls in flight"},
             "seqs_per_s": n_seq / loop, "fasta_mb_per_s": fbytes / 1e6 / loop,
             "loop": best, "runs_loop_s": [r[0]["loop_s"] for r in runs],
             "apply_format": apply_stats,
@@ -670,15 +673,29 @@ def bench_fasta(args):
         shutil.rmtree(root, ignore_errors=True)
 
 
-def e2e_host(table, residues, offsets, n_fid, reps=3):
+def e2e_host(table, residues, offsets, n_fid, reps=5):
     """kma_annotate_proteins from host memory (H2D + kernel + D2H through the table's pooled
-    pinned staging): best of `reps` calls after one warmup call, in ms."""
-    kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid)
-    best = 1e30
+    pinned staging) into the caller's output arrays, reused across calls as a JNI caller reuses
+    its direct buffers: best of `reps` calls after one warmup call, in ms, with the library's
+    host-side phase profile of that call."""
+    n = len(offsets) - 1
+    out = (np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint8),
+           np.zeros(n_fid, np.uint32))
+    kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid, out=out)
+    best, prof = 1e30, None
+    lib = kmeranno.load()
     for _ in range(reps):
         t0 = time.perf_counter()
-        kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid)
-        best = min(best, time.perf_counter() - t0)
+        kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid, out=out)
+        dt = time.perf_counter() - t0
+        if dt < best:
+            best = dt
+            p = np.zeros(6, np.float64)
+            if hasattr(lib, "kma_debug_host_profile"):
+                lib.kma_debug_host_profile(p.ctypes.data_as(ctypes.c_void_p), 6)
+            prof = dict(zip(("setup", "stage", "launch", "wait", "outputs", "total"),
+                            p.tolist()))
+    e2e_host.profile = prof
     return best * 1e3
 
 
@@ -883,6 +900,7 @@ def main():
                        "table_entries": t_size, "functions": n_fid, "k": K,
                        "load_factor": args.load_factor, "min_hits": MIN_HITS,
                        "table_layout_m": table.info.minimizer_len,
+                       "table_placement": "two-choice" if table.info.two_choice else "chained",
                        "parallelism": (f"input-shard x{world} of one batch" if strong else
                                        f"input-shard x{world}") + collective_note(args, world)},
             "seqs_per_s": seqs * args.steps / elapsed,
@@ -905,7 +923,8 @@ def main():
                     "packed_input": kmeranno.get_option(kmeranno.OPT_PACKED_INPUT),
                     "staging_threads": kmeranno.get_option(kmeranno.OPT_HOST_THREADS) or
                     "min(16, cores)",
-                    "ms": ms, "lookups_per_s": n_win / (ms * 1e-3),
+                    "ms": ms, "library_profile_ms": getattr(e2e_host, "profile", None),
+                    "lookups_per_s": n_win / (ms * 1e-3),
                     "seqs_per_s": n_seq / (ms * 1e-3), "kernel_ratio": ms / ph["annotate_kernel"],
                     "ascii_staging_ms": ms_ascii,
                     "link": link_rates(residues, n_res, dev)}

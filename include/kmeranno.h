@@ -96,6 +96,9 @@ extern "C" {
  * The protein path (kma_annotate_proteins*) takes narrow tables: apply's ProteinKmers keeps
  * K = 8 whatever the table holds (ApplyKmerProcessor.java:108 sets KmerReference's K only). */
 #define KMA_MAX_K 12
+/* Layout codes (kma_table_build_device, kma_table_wrap_device, kma_table_layout_for): the
+ * minimizer length m (0 = flat) | KMA_LAYOUT_TWO_CHOICE for two-choice placement (ABI 6).    */
+#define KMA_LAYOUT_TWO_CHOICE 0x100
 #define KMA_MAX_FID ((1u << 22) - 1u)
 
 
@@ -121,6 +124,10 @@ typedef struct kma_table_info {
   double replicate_ms;   /* ABI 6: wall time of the last kma_table_replicate (its copies run
                             concurrently, one stream per destination); 0 before any         */
   uint64_t replicate_bytes; /* ABI 6: bytes that call copied (slot array x destinations)    */
+  int32_t two_choice;    /* ABI 6: placement. 1 = two-choice (every key in its home bucket or
+                            in one other bucket, a hash of the whole key: a lookup reads at
+                            most 2 buckets); 0 = overflow chains                            */
+  int32_t pad_;
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -165,6 +172,8 @@ int kma_device_count(int* out_n);
  *   KMA_OPT_HOST_SLICE      host protein calls: residues per device call [0: 2^31]; a replica's
  *                           share of a larger batch is annotated as consecutive slices of
  *                           whole proteins (tallies summed); >= 1 (tests set it low)
+ *   KMA_OPT_PLACEMENT       table creators [-1: two-choice placement for K <= 8, chains if that
+ *                           build fails, and for K > 8]; 0 = chains only; 1 = as -1
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -175,6 +184,7 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_PACKED_INPUT 6
 #define KMA_OPT_HOST_THREADS 7
 #define KMA_OPT_HOST_SLICE 8
+#define KMA_OPT_PLACEMENT 9
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);
@@ -202,12 +212,18 @@ int kma_table_destroy(kma_table* table);
  * former; wide, K 9..12: 4 slots of 16 bytes); 0 for an invalid K.                          */
 int kma_bucket_slots(void);
 int kma_bucket_slots_for(int k);
-/* The table's layout choice: minimizer layouts (m = min(K,6) up to 2^25 narrow buckets — 2^24
- * with 16-slot buckets, 2^26 wide ones — else min(K,7)); when more than 15% of the keys land
- * past their home bucket or a chain exceeds 32 buckets (keys that pile onto few minimizers),
- * the creators above also build the table flat (layout 0) and keep it if it halves the
- * displaced keys or the longest chain. kma_table_layout_for gives the size-derived layout
- * (KMA_OPT_LAYOUT = 0 / 6 / 7 forces one).                                                    */
+/* The table's layout choice. Placement (ABI 6): narrow tables (K <= 8) are built with
+ * two-choice placement — every key in its home bucket or in one other bucket, a hash of the
+ * whole key — so a lookup reads at most two buckets; a two-choice minimizer table with more than
+ * 40% of its keys outside their home is also built flat and the flat one kept if it halves them.
+ * When that build fails (a key that finds no place after 2,000 evictions: load factors near 1
+ * with crowded minimizers) and for wide tables, keys overflow along chains: minimizer layouts
+ * (m = min(K,6) up to 2^25 narrow buckets — 2^24 with 16-slot buckets, 2^26 wide ones — else
+ * min(K,7)); when more than 15% of the keys land past their home bucket or a chain exceeds 32
+ * buckets (keys that pile onto few minimizers), the creators also build the table flat (layout 0)
+ * and keep it if it halves the displaced keys or the longest chain. kma_table_layout_for gives
+ * the size-derived layout code (m | KMA_LAYOUT_TWO_CHOICE when the creators try that first;
+ * KMA_OPT_LAYOUT = 0 / 6 / 7 forces m, KMA_OPT_PLACEMENT = 0 chains).                       */
 int kma_table_layout_for(int k, uint64_t n_buckets);
 
 /* ---- replicas (the table replicated on every device of the node) -------------
@@ -232,12 +248,15 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
  *   kma_table_build_device: d_slots (info.bytes: n_buckets * 64 bytes, 128 in the 16-slot build)
  *                           and d_winner (n_buckets * S u32, S = kma_bucket_slots_for(k)) are
  *                           caller scratch; keys/fids are device arrays of K-mers; layout -1 =
- *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7); builds on
- *                           `stream`; d_status (4 u32) receives {table full, entries, longest
- *                           chain, displaced keys} (a caller may rebuild with layout 0 when
- *                           displaced keys are many); fids are masked to 22 bits; keys that
- *                           are 0 or not K-mer keys (>= 2^(5K)) are not stored.
- *   kma_table_wrap_device : adopt an already-built slot array of that layout (not owned).    */
+ *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7), | KMA_LAYOUT_
+ *                           TWO_CHOICE for two-choice placement (K <= 8; d_winner unused; the
+ *                           build allocates its sort buffers and waits for `stream`); builds on
+ *                           `stream`; d_status (4 u32) receives {table full / two-choice build
+ *                           failed, entries, longest chain (two-choice: 1 or 2), displaced
+ *                           keys} (a caller rebuilds chained when [0] is set, and may rebuild
+ *                           with layout 0 when displaced keys are many); fids are masked to 22
+ *                           bits; keys that are 0 or not K-mer keys (>= 2^(5K)) are not stored.
+ *   kma_table_wrap_device : adopt an already-built slot array of that layout code (not owned). */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
 uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k);
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,

@@ -37,8 +37,8 @@ namespace {
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 9;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}};
+constexpr int kNumOpts = 10;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}, {-1}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
@@ -51,6 +51,7 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_PACKED_INPUT: return v >= 0 && v <= 2;
     case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
     case KMA_OPT_HOST_SLICE: return v >= 0;
+    case KMA_OPT_PLACEMENT: return v >= -1 && v <= 1;
     default: return false;
   }
 }
@@ -62,7 +63,7 @@ struct EnvOptions {  // tuning builds: the A/B scripts' variables seed the defau
         {"KMA_MINIMIZER", KMA_OPT_LAYOUT}, {"KMA_BLOCK_PROTEINS", KMA_OPT_BLOCK_PROTEINS},
         {"KMA_DEFER", KMA_OPT_DEFER}, {"KMA_HOST_PIECES", KMA_OPT_HOST_PIECES},
         {"KMA_HASH_SLICE", KMA_OPT_HASH_SLICE}, {"KMA_PACKED_INPUT", KMA_OPT_PACKED_INPUT},
-        {"KMA_HOST_THREADS", KMA_OPT_HOST_THREADS}};
+        {"KMA_HOST_THREADS", KMA_OPT_HOST_THREADS}, {"KMA_PLACEMENT", KMA_OPT_PLACEMENT}};
     for (const auto& [name, opt] : vars)
       if (const char* e = getenv(name); e && *e) {
         const int64_t v = strtoll(e, nullptr, 10);
@@ -76,6 +77,9 @@ int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 // The forced table layout (KMA_OPT_LAYOUT): -1 = not forced.
 int forced_layout() { return (int)opt(KMA_OPT_LAYOUT); }
+// Table creators try two-choice placement first for narrow tables (KMA_OPT_PLACEMENT -1 / 1);
+// 0 builds chains only.
+bool two_choice_first(int k) { return !kma::wide_k(k) && opt(KMA_OPT_PLACEMENT) != 0; }
 
 // Host threads a host call stages (copies or packs) its input with (KMA_OPT_HOST_THREADS; 0:
 // min(16, cores)). Packing 5 bits per residue keeps up with the PCIe link only on ~16 threads.
@@ -440,7 +444,10 @@ struct HostCtx {
   // H2D of piece i + 1 under the kernel of piece i, pieces alternating over two copy streams
   // (two DMA engines: 57 vs 50 GB/s for c5's packed stream, profiles/r04/link_r04g.json)
   hipStream_t copy[2] = {};
+  hipStream_t d2h = nullptr;  // pieces' outputs back while later pieces copy and run
   hipEvent_t piece_ready[kMaxPieces] = {};
+  hipEvent_t piece_done[kMaxPieces] = {};  // piece i's kernel (on `stream`)
+  hipEvent_t out_ready[kMaxPieces] = {};   // piece i's outputs in pinned memory (on d2h)
   kma_workspace* ws = nullptr;
   Grow<uint8_t> d_in;     // residues / DNA (+ padding)
   Grow<uint64_t> d_off;   // offsets
@@ -454,6 +461,7 @@ struct HostCtx {
 struct kma_table {
   int k = 8;
   int mlen = 6;  // layout: minimizer length, 0 = flat
+  bool two_choice = false;  // placement (kma_internal.h alt_bucket): else overflow chains
   uint64_t n_buckets = 0;
   uint8_t lut[256] = {};
   kma_table_info info = {};
@@ -476,8 +484,10 @@ void destroy_ctx(HostCtx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (hipStream_t cs : c->copy)
     if (cs) (void)hipStreamDestroy(cs);
-  for (hipEvent_t e : c->piece_ready)
-    if (e) (void)hipEventDestroy(e);
+  if (c->d2h) (void)hipStreamDestroy(c->d2h);
+  for (hipEvent_t* ev : {c->piece_ready, c->piece_done, c->out_ready})
+    for (int i = 0; i < kMaxPieces; ++i)
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
   c->d_in.release();
   c->d_off.release();
   c->d_out.release();
@@ -506,8 +516,10 @@ int acquire_ctx(kma_table* t, int device, HostCtx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   for (hipStream_t& cs : c->copy)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-  for (int i = 0; i < kMaxPieces && e == hipSuccess; ++i)
-    e = hipEventCreateWithFlags(&c->piece_ready[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
+  for (hipEvent_t* ev : {c->piece_ready, c->piece_done, c->out_ready})
+    for (int i = 0; i < kMaxPieces && e == hipSuccess; ++i)
+      e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     destroy_ctx(c);
     return fail(KMA_E_DEVICE, "stream / event create: %s", hipGetErrorString(e));
@@ -532,6 +544,7 @@ struct CtxGuard {
     // kernels drain before the next call reuses its pinned and device buffers.
     for (hipStream_t cs : c->copy) (void)hipStreamSynchronize(cs);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->d2h);
     release_ctx(t, c);
   }
 };
@@ -570,10 +583,13 @@ int add_replica(kma_table* t, int device, uint64_t* d_slots, bool owned) {
   return KMA_OK;
 }
 
-kma_table* new_table(int device, int k, int m, uint64_t n_buckets, const uint8_t lut[256]) {
+kma_table* new_table(int device, int k, int m, uint64_t n_buckets, const uint8_t lut[256],
+                     bool two_choice = false) {
   kma_table* t = new kma_table();
   t->k = k;
   t->mlen = m;
+  t->two_choice = two_choice;
+  t->info.two_choice = two_choice ? 1 : 0;
   t->n_buckets = n_buckets;
   std::memcpy(t->lut, lut, 256);
   t->info.n_buckets = n_buckets;
@@ -614,11 +630,44 @@ int build_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m, uint32_
   return KMA_OK;
 }
 
-// Table from device-resident keys/fids on `device` (n rows; fids already checked), laid out by
-// the size rule and then by measurement (kma_internal.h, kRetryDisplaced / kMaxDisplaced):
-// an m = 6 table with many displaced keys is rebuilt with m = 7 (kept if it displaces fewer),
-// a still crowded minimizer table is rebuilt flat (kept if that halves the displaced keys or
-// the longest chain). KMA_MINIMIZER forces a layout.
+// Two-choice build (kma_kernels.hip launch_build_two_choice) into zeroed slots on stream s; its
+// sort buffers are allocated here and freed after the stream has drained them.
+int build_two_choice_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int m,
+                               const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n,
+                               uint32_t* d_status, hipStream_t s) {
+  if (n_buckets >= kMaxBuckets) return fail(KMA_E_INVALID, "%llu buckets or more",
+                                           (unsigned long long)kMaxBuckets);
+  if (n_buckets < 2) return fail(KMA_E_INVALID, "two-choice placement needs 2 buckets or more");
+  if (n >= (1ull << 32)) return fail(KMA_E_INVALID, "2^32 rows or more");
+  KMA_HIP(hipMemsetAsync(d_slots, 0, n_buckets * bucket_bytes(k), s));
+  KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
+  if (n == 0) return KMA_OK;
+  size_t temp_bytes = 0;
+  KMA_HIP(kma::launch_build_two_choice(d_slots, (uint32_t)n_buckets, k, m, d_keys, d_fids, n,
+                                       nullptr, nullptr, nullptr, nullptr, &temp_bytes, d_status,
+                                       s));
+  DevBufs tmp;
+  uint64_t* skeys;
+  uint32_t *rows, *srows;
+  void* temp;
+  KMA_HIP(tmp.alloc(&skeys, n * 8));
+  KMA_HIP(tmp.alloc(&rows, n * 4));
+  KMA_HIP(tmp.alloc(&srows, n * 4));
+  KMA_HIP(tmp.alloc(&temp, temp_bytes));
+  KMA_HIP(kma::launch_build_two_choice(d_slots, (uint32_t)n_buckets, k, m, d_keys, d_fids, n,
+                                       skeys, rows, srows, temp, &temp_bytes, d_status, s));
+  KMA_HIP(hipStreamSynchronize(s));  // before DevBufs frees the sort buffers
+  return KMA_OK;
+}
+
+// Table from device-resident keys/fids on `device` (n rows; fids already checked). Narrow tables
+// are built with two-choice placement first (round 5; KMA_OPT_PLACEMENT 0 skips it), at the size
+// rule's layout (a crowded minimizer table also flat, kept if it halves the displaced keys).
+// Chained tables (wide K, or a two-choice build that failed) are laid out by the size rule and
+// then by measurement (kma_internal.h, kRetryDisplaced / kMaxDisplaced): an m = 6 table with
+// many displaced keys is rebuilt with m = 7 (kept if it displaces fewer), a still crowded
+// minimizer table is rebuilt flat (kept if that halves the displaced keys or the longest
+// chain). KMA_OPT_LAYOUT forces a layout.
 int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint64_t n, int k,
                             int device, double lf, const uint8_t lut[256], kma_table** out) {
   const uint64_t nb = buckets_for_k(n, lf, k);
@@ -645,8 +694,61 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
   int m = kma::minimizer_len(k, nb);
   uint64_t* d_slots = nullptr;
   uint32_t st[4] = {};
-  if (int rc = build(m, &d_slots, st)) return rc;
   auto displaced = [](const uint32_t s[4]) { return (double)s[3] / std::max<uint32_t>(s[1], 1); };
+  if (two_choice_first(k) && nb >= 2) {
+    // Two-choice placement at the size rule's (or the forced) layout; a crowded minimizer table
+    // is also built flat and the flat one kept if it halves the displaced keys; a build that
+    // fails (an insertion exceeded kMaxKicks) falls through to the chained rule below.
+    uint32_t s2[4] = {};
+    auto build2 = [&](int m2, uint64_t** slots, uint32_t out[4]) -> int {
+      KMA_HIP(hipMalloc(slots, nb * bucket_bytes(k)));
+      int rc = build_two_choice_on_device(*slots, nb, k, m2, d_keys, d_fids, n, d_status, nullptr);
+      if (rc == KMA_OK) {
+        hipError_t e = hipMemcpy(out, d_status, 16, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(KMA_E_DEVICE, "build: %s", hipGetErrorString(e));
+      }
+      if (rc != KMA_OK || out[0]) {
+        (void)hipFree(*slots);
+        *slots = nullptr;
+      }
+      return rc;
+    };
+    uint64_t* d2 = nullptr;
+    if (int rc = build2(m, &d2, s2)) return rc;
+    if (!s2[0]) {  // built
+      d_slots = d2;
+      std::memcpy(st, s2, sizeof st);
+      if (forced_layout() < 0 && m != 0 && displaced(st) > kma::kMaxDisplacedTwoChoice) {
+        uint64_t* d3 = nullptr;
+        uint32_t s3[4] = {};
+        if (int rc = build2(0, &d3, s3)) {
+          (void)hipFree(d_slots);
+          return rc;
+        }
+        if (d3 && 2ull * s3[3] < st[3]) {
+          (void)hipFree(d_slots);
+          d_slots = d3;
+          std::memcpy(st, s3, sizeof st);
+          m = 0;
+        } else if (d3) {
+          (void)hipFree(d3);
+        }
+      }
+      kma_table* t = new_table(device, k, m, nb, lut, true);
+      if (int rc = add_replica(t, device, d_slots, true)) {
+        (void)hipFree(d_slots);
+        delete t;
+        return rc;
+      }
+      t->info.n_rows = n;
+      t->info.n_entries = st[1];
+      t->info.max_probe = st[2];
+      t->info.n_displaced = st[3];
+      *out = t;
+      return KMA_OK;
+    }
+  }
+  if (int rc = build(m, &d_slots, st)) return rc;
   // Replace the current table (slots, stats, m) by a build with layout m2 when keep() says so.
   auto try_layout = [&](int m2, bool (*keep)(const uint32_t*, const uint32_t*)) -> int {
     uint64_t* d2 = nullptr;
@@ -781,7 +883,10 @@ uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k) {
 
 int kma_bucket_slots_for(int k) { return check_k(k) ? 0 : kma::slots_for_k(k); }
 
-int kma_table_layout_for(int k, uint64_t n_buckets) { return kma::minimizer_len(k, n_buckets); }
+int kma_table_layout_for(int k, uint64_t n_buckets) {
+  return kma::minimizer_len(k, n_buckets) |
+         (two_choice_first(k) && n_buckets >= 2 ? kma::kLayoutTwoChoice : 0);
+}
 
 int kma_bucket_slots(void) { return kma::kSlotsPerBucket; }
 
@@ -950,9 +1055,15 @@ int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
   if (!d_slots || !d_winner || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
     return fail(KMA_E_INVALID, "null argument");
   if (int rc = check_k(k)) return rc;
-  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout;
+  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
+  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout & kma::kLayoutMask;
   if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
     return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
+  if (two) {
+    if (kma::wide_k(k)) return fail(KMA_E_INVALID, "two-choice placement takes K <= 8");
+    return build_two_choice_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, m, d_keys,
+                                      d_fids, n, d_status, static_cast<hipStream_t>(stream));
+  }
   return build_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, m, d_winner, d_keys,
                          d_fids, n, d_status, static_cast<hipStream_t>(stream));
 }
@@ -963,12 +1074,15 @@ int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, 
   if (n_buckets >= kMaxBuckets) return fail(KMA_E_INVALID, "%llu buckets or more",
                                            (unsigned long long)kMaxBuckets);
   if (int rc = check_k(k)) return rc;
-  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout;
+  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
+  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout & kma::kLayoutMask;
   if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
     return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
+  if (two && (kma::wide_k(k) || n_buckets < 2))
+    return fail(KMA_E_INVALID, "two-choice placement takes K <= 8 and 2 buckets or more");
   uint8_t lut[256];
   standard_lut(lut);
-  kma_table* t = new_table(device, k, m, n_buckets, lut);
+  kma_table* t = new_table(device, k, m, n_buckets, lut, two);
   if (int rc = add_replica(t, device, static_cast<uint64_t*>(d_slots), false)) {
     delete t;
     return rc;
@@ -1027,6 +1141,7 @@ int contig_args(const kma_table* t, const Replica& r, kma_workspace* ws, const u
   a.total_bases = n_bases;
   a.k = t->k;
   a.mlen = t->mlen;
+  a.two_choice = t->two_choice ? 1u : 0u;
   a.staging = ws->d_cstage;
   a.block_counts = ws->d_ccounts;
   // An earlier call failed between its probe and its emit: start clean, ordered on this
@@ -1146,6 +1261,7 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.n_residues = (uint32_t)n_residues;
   a.k = t->k;
   a.mlen = t->mlen;
+  a.two_choice = t->two_choice ? 1u : 0u;
   a.min_hits = min_hits;
   a.flags = flags;
   a.out_fid = d_fid;
@@ -1283,15 +1399,46 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   uint8_t* d_st = reinterpret_cast<uint8_t*>(d_cnt + n) + (tally ? n_fid * 4ull : 0);
   if (d_tally) KMA_HIP(hipMemsetAsync(d_tally, 0, n_fid * 4ull, s));
   const int n_pieces = (int)std::max<uint64_t>(1, std::min<uint64_t>(max_pieces, nres / kPieceBytes));
+  // Piece sizes ramp up and down (weights 1, 2, 4, ..., 4, 2, 1): a small first piece starts the
+  // link early and a small last piece shortens the tail behind the last copy (its kernel and
+  // its outputs). Round 4's equal eighths left 0.4 ms of kernel and 0.5 ms of output copies
+  // after the last H2D (profiles/r04/e2e_trace_r04h.json).
+  uint64_t wsum = 0, wcum[kMaxPieces + 1] = {0};
+  for (int i = 0; i < n_pieces; ++i) {
+    const int edge = std::min(i, n_pieces - 1 - i);
+    wsum += n_pieces >= 4 ? (1u << std::min(edge, 2)) : 1u;
+    wcum[i + 1] = wsum;
+  }
   uint32_t pa = 0;  // first protein of the piece (relative to lo)
   uint64_t ga = 0;  // packed: first stream group the piece stages
+  uint32_t pbeg[kMaxPieces + 1] = {0};
+  const uint8_t* hout = c->h_out.p;
+  // piece i's outputs back on the d2h stream once its kernel is done (fid, count, status
+  // slices; the tally with the last piece), while later pieces copy and run
+  auto outputs_back = [&](int i, uint32_t a, uint32_t b) -> int {
+    KMA_HIP(hipEventRecord(c->piece_done[i], s));
+    KMA_HIP(hipStreamWaitEvent(c->d2h, c->piece_done[i], 0));
+    if (b > a) {
+      uint8_t* h = c->h_out.p;
+      KMA_HIP(hipMemcpyAsync(h + a * 4ull, d_fid + a, (b - a) * 4ull, hipMemcpyDeviceToHost, c->d2h));
+      KMA_HIP(hipMemcpyAsync(h + (n + a) * 4ull, d_cnt + a, (b - a) * 4ull, hipMemcpyDeviceToHost,
+                             c->d2h));
+      KMA_HIP(hipMemcpyAsync(h + n * 8ull + (tally ? n_fid * 4ull : 0) + a, d_st + a, b - a,
+                             hipMemcpyDeviceToHost, c->d2h));
+    }
+    if (i + 1 == n_pieces && tally)
+      KMA_HIP(hipMemcpyAsync(c->h_out.p + n * 8ull, d_tally, n_fid * 4ull, hipMemcpyDeviceToHost,
+                             c->d2h));
+    KMA_HIP(hipEventRecord(c->out_ready[i], c->d2h));
+    return KMA_OK;
+  };
   const double t_setup = ms_since(t_call);
   for (int i = 0; i < n_pieces; ++i) {
     hipStream_t cs = c->copy[i & 1];
     const Clock::time_point t_piece = Clock::now();
     uint32_t pb = n;
     if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
-      const uint64_t target = nres * (uint64_t)(i + 1) / n_pieces;
+      const uint64_t target = nres * wcum[i + 1] / wsum;
       pb = (uint32_t)(std::lower_bound(hoff + pa, hoff + n, target) - hoff);
     }
     const uint64_t ra = hoff[pa], rb = i + 1 < n_pieces ? hoff[pb] : nres;
@@ -1318,22 +1465,30 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                                         d_cnt + pa, d_st + pa, d_tally, n_fid, s,
                                         packed ? Input::kStream : Input::kAscii, hoff[pa]))
         return rc;
+    if (int rc = outputs_back(i, pa, pb)) return rc;
     t_launch += ms_since(t_staged);
+    pbeg[i] = pa;
     pa = pb;
   }
-  KMA_HIP(hipMemcpyAsync(c->h_out.p, dout, out_bytes - 16, hipMemcpyDeviceToHost, s));
-  const Clock::time_point t_w = Clock::now();
-  KMA_HIP(hipStreamSynchronize(s));
-  const double t_wait = ms_since(t_w);
+  pbeg[n_pieces] = n;
+  // Pieces' outputs into the caller's arrays as they arrive (the later pieces still copy and
+  // run meanwhile).
+  double t_wait = 0;
   const Clock::time_point t_o = Clock::now();
-  const uint8_t* hout = c->h_out.p;
-  pool_memcpy(out_fid + lo, hout, n * 4ull);
-  pool_memcpy(out_count + lo, hout + n * 4ull, n * 4ull);
-  const uint8_t* ht = hout + n * 8ull;
-  pool_memcpy(out_status + lo, ht + (tally ? n_fid * 4ull : 0), n);
-  if (tally) std::memcpy(tally, ht, n_fid * 4ull);
+  for (int i = 0; i < n_pieces; ++i) {
+    const Clock::time_point t_w = Clock::now();
+    KMA_HIP(hipEventSynchronize(c->out_ready[i]));
+    t_wait += ms_since(t_w);
+    const uint32_t a = pbeg[i], b = pbeg[i + 1];
+    if (b == a) continue;
+    pool_memcpy(out_fid + lo + a, hout + a * 4ull, (b - a) * 4ull);
+    pool_memcpy(out_count + lo + a, hout + (n + a) * 4ull, (b - a) * 4ull);
+    pool_memcpy(out_status + lo + a, hout + n * 8ull + (tally ? n_fid * 4ull : 0) + a, b - a);
+  }
+  if (tally) std::memcpy(tally, hout + n * 8ull, n_fid * 4ull);
   {
-    const double p[6] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o), ms_since(t_call)};
+    const double p[6] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o) - t_wait,
+                         ms_since(t_call)};
     std::lock_guard<std::mutex> g(g_prof_mu);
     std::copy(p, p + 6, g_prof);
   }

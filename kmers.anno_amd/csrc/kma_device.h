@@ -131,9 +131,29 @@ __device__ __forceinline__ void scan_half(const uint4 (&q)[4], int half, uint64_
 #define KMA_WALK_GROUP 1
 #endif
 constexpr int kWalkGroup = KMA_WALK_GROUP;
+// Two-choice tables (two_choice, kma_internal.h alt_bucket): the key's only other bucket is read
+// instead, once; a miss there is definitive.
 __device__ __forceinline__ bool walk_chain(const uint64_t* __restrict__ slots, uint32_t n_buckets,
                                            uint32_t b, uint64_t key, uint32_t& fid,
-                                           uint32_t& sid, uint32_t* walked = nullptr) {
+                                           uint32_t& sid, bool two_choice = false,
+                                           uint32_t* walked = nullptr) {
+  if (two_choice) {
+    const uint32_t ab = alt_bucket(key, b, n_buckets);
+    const uint4* bp = reinterpret_cast<const uint4*>(slots + (uint64_t)ab * kSlotsPerBucket);
+    uint4 q[kBucketQuads];
+#pragma unroll
+    for (int i = 0; i < kBucketQuads; ++i) q[i] = bp[i];
+    bool h = false, e = false;
+    uint32_t slot = 0;
+#pragma unroll
+    for (int half = 0; half < kBucketHalves; ++half) {
+      const uint4 part[4] = {q[4 * half], q[4 * half + 1], q[4 * half + 2], q[4 * half + 3]};
+      scan_half(part, half, key, h, e, fid, slot);
+    }
+    sid = ab * kSlotsPerBucket + slot;
+    if (walked) *walked = 1;
+    return h;
+  }
   bool hit = false, empty = false;
   const uint32_t home = b;
   uint32_t slot = 0, steps = 1;

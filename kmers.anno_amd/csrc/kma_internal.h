@@ -242,6 +242,34 @@ __host__ __device__ inline uint32_t chain_step(uint32_t home, uint32_t b, uint32
   return b >= home ? b - home : b + n_buckets - home;
 }
 
+// ---- two-choice placement (round 5; narrow tables) ------------------------------------------------
+// Chains make a displaced key cost a walk of hashed buckets: at load factor 0.9 (c5, m = 7) a
+// walk loaded 4.05 buckets on average (a miss walks until a bucket with an empty slot, and few
+// buckets have one), 0.40 bucket requests per probed window on top of the 0.67 home lines, and
+// the kernel ran at the request ceiling (1.05 requests per window; profiles/r05/). Two-choice
+// placement (bucketized cuckoo hashing) gives every key exactly two buckets: its home (the
+// minimizer layout's, shared by consecutive windows) and alt_bucket (a hash of the whole key,
+// never the home). The build (build_two_choice_*: keys deduplicated last-wins by a radix sort,
+// then inserted with evictions between the two buckets, then the filters) puts each key in one
+// of them; the filter bits of a home bucket are those of its keys that live in their alt. A
+// lookup that misses its home with every filter position set reads the alt bucket: one request,
+// and a miss there is definitive. A table that cannot be built this way (an insertion exceeds
+// kMaxKicks evictions: load factors near 1 with crowded minimizers) is built with chains.
+__host__ __device__ inline uint32_t alt_bucket(uint64_t key, uint32_t home, uint32_t n_buckets) {
+  const uint32_t h = mix32((uint32_t)key * 0x2C1B3C6Du ^ mix32_lite((uint32_t)(key >> 32) + 0x68E31DA5u));
+  const uint32_t b = (uint32_t)(((uint64_t)h * (n_buckets - 1u)) >> 32);  // any bucket but home
+  return b >= home ? b + 1u : b;
+}
+constexpr uint32_t kMaxKicks = 2000;
+// Layout codes of kma_table_build_device / kma_table_wrap_device / kma_table_layout_for: the
+// minimizer length (0 = flat) | kLayoutTwoChoice for two-choice placement.
+constexpr int kLayoutTwoChoice = KMA_LAYOUT_TWO_CHOICE;
+constexpr int kLayoutMask = 0xFF;
+// A two-choice minimizer table whose displaced share exceeds this is also built flat (keys piling
+// onto few minimizers: their homes' filters fill and most misses read the alt bucket) and the
+// flat one kept if it halves the displaced keys.
+constexpr double kMaxDisplacedTwoChoice = 0.40;
+
 // Layout (minimizer length m, 0 = flat) of a table of n_buckets buckets for K-mers. Keys
 // sharing a minimizer share a bucket, so the m-mer space must stay large against the table,
 // while consecutive windows share their minimizer (and a request) with probability
@@ -340,6 +368,7 @@ struct ProteinArgs {
   // kma_device.h (5 bits per residue, stream residue 0 = residue offsets[0]).
   uint32_t packed;
   uint64_t stream_first;  // packed: stream residue index of residue offsets[0]
+  uint32_t two_choice;    // table placement: 1 = a missed key's only other bucket is alt_bucket
 };
 
 struct ContigArgs {
@@ -369,6 +398,7 @@ struct ContigArgs {
   // pass 2 keeps only hits whose key has exactly one location (strict_pass = 2).
   uint32_t* slot_count;        // n_buckets * kSlotsPerBucket, zeroed before pass 1
   int32_t strict_pass;         // 0 = off
+  uint32_t two_choice;         // table placement (ProteinArgs::two_choice)
   uint8_t codon_codes[64];     // by value (TCAG order): 5-bit aa code, 0 = stop
 };
 #ifndef KMA_CONTIG_POS
@@ -424,6 +454,16 @@ hipError_t launch_build_insert(uint64_t* slots, uint32_t* winner, uint32_t n_buc
 hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const uint32_t* fids,
                                  uint32_t n_buckets, int k, int m, uint32_t* stats,
                                  hipStream_t stream);
+// Two-choice build of a narrow table (slots zeroed by the caller): keys (row order) sorted with
+// their row indices into sorted_keys / sorted_rows (rocPRIM radix sort on the 5K key bits; temp
+// == nullptr: size query into *temp_bytes), the last row of each key inserted with evictions,
+// then the filters; status[0] = an insertion failed, status[1..3] = {entries, longest probe (1
+// or 2), displaced keys}.
+hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, int m,
+                                   const uint64_t* keys, const uint32_t* fids, uint64_t n,
+                                   uint64_t* sorted_keys, uint32_t* rows, uint32_t* sorted_rows,
+                                   void* temp, size_t* temp_bytes, uint32_t* status,
+                                   hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 // ASCII residues [offsets[0], offsets[0] + n) -> the packed stream (packed_bytes(n) bytes; the
 // LUT of the table's replica): pack_residues_kernel.

@@ -130,6 +130,105 @@ __global__ __launch_bounds__(256) void build_finalize_kernel(uint64_t* slots,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Two-choice build (narrow tables; kma_internal.h alt_bucket). The rows are radix-sorted by key
+// with their row index (stable: a key's rows stay in file order), so the last row of every run
+// is the row HashMap.put keeps; each such key is inserted into an empty slot of its home or alt
+// bucket, or evicts a pseudo-random slot of a full one and carries the victim to the victim's
+// other bucket (a random-walk cuckoo insertion; every slot exchange is one 64-bit atomic, so no
+// key is lost or doubled). A key still in hand after kMaxKicks evictions marks the build failed
+// (the caller builds the table with chains instead). The filter pass then sets, for every key
+// stored in its alt bucket, its filter positions in its home bucket, and counts.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t* rows, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    rows[i] = (uint32_t)i;
+}
+
+__device__ __forceinline__ bool claim_empty(uint64_t* slots, uint32_t b, uint64_t v) {
+  uint64_t* sp = slots + (uint64_t)b * kSlotsPerBucket;
+#pragma unroll
+  for (int j = 0; j < kSlotsPerBucket; ++j)
+    if (__hip_atomic_load(sp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull &&
+        atomicCAS((unsigned long long*)(sp + j), 0ull, (unsigned long long)v) == 0ull)
+      return true;
+  return false;
+}
+
+__global__ __launch_bounds__(256) void build_two_choice_insert_kernel(
+    uint64_t* slots, uint32_t n_buckets, int k, int m, const uint64_t* __restrict__ skeys,
+    const uint32_t* __restrict__ srows, const uint32_t* __restrict__ fids, uint64_t n,
+    uint32_t* status) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = skeys[i];
+    if (key == 0 || (key >> (5 * k)) != 0) continue;  // no key / not a K-mer key: never stored
+    if (i + 1 < n && skeys[i + 1] == key) continue;   // a later row of this key wins
+    uint64_t v = slot_make(key, fids[srows[i]]);
+    uint32_t b1 = home_bucket(key, k, m, n_buckets);
+    uint32_t b2 = alt_bucket(key, b1, n_buckets);
+    uint32_t at = b1;  // the bucket to evict from when both are full
+    uint32_t rng = (uint32_t)i * 0x9E3779B1u + 0x7F4A7C15u;
+    bool done = false;
+    for (uint32_t kick = 0; kick <= kMaxKicks; ++kick) {
+      if (claim_empty(slots, b1, v) || claim_empty(slots, b2, v)) {
+        done = true;
+        break;
+      }
+      if (kick == kMaxKicks) break;
+      rng = rng * 1664525u + 1013904223u;
+      const uint32_t j = rng >> (32 - kSlotBits);
+      const uint64_t old = atomicExch((unsigned long long*)(slots + (uint64_t)at * kSlotsPerBucket + j),
+                                      (unsigned long long)v);
+      if (old == 0ull) {  // (slots never empty again once claimed; kept for safety)
+        done = true;
+        break;
+      }
+      // the victim lived in `at`: its other bucket first (then `at`, for a slot freed meanwhile)
+      v = old;
+      const uint64_t vk = slot_key(old);
+      const uint32_t h = home_bucket(vk, k, m, n_buckets);
+      const uint32_t other = at == h ? alt_bucket(vk, h, n_buckets) : h;
+      b1 = other;
+      b2 = at;
+      at = other;
+    }
+    if (!done) atomicOr(status, 1u);
+  }
+}
+
+__global__ __launch_bounds__(256) void build_two_choice_filter_kernel(uint64_t* slots,
+                                                                      uint32_t n_buckets, int k,
+                                                                      int m, uint32_t* stats) {
+  constexpr int S = kSlotsPerBucket;
+  const uint64_t n_slots = (uint64_t)n_buckets * S;
+  uint32_t entries = 0, displaced = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_slots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t v = __hip_atomic_load(slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)v == 0u) continue;
+    const uint64_t key = slot_key(v);
+    const uint32_t b = (uint32_t)(i / S), h = home_bucket(key, k, m, n_buckets);
+    entries++;
+    if (b != h) {  // in its alt bucket: its filter positions in the home bucket
+      displaced++;
+      for (int f = 0; f < kFilterBits; ++f) {
+        const uint32_t pos = filter_pos<S>((uint32_t)key, f);
+        uint32_t* meta = reinterpret_cast<uint32_t*>(slots + (uint64_t)h * S + pos / kFilterBits) + 1;
+        atomicOr(meta, 1u << (kFidBits + pos % kFilterBits));
+      }
+    }
+  }
+  entries = wave_sum(entries);
+  displaced = wave_sum(displaced);
+  if ((threadIdx.x & 63) == 0) {
+    if (entries) atomicAdd(stats + 0, entries);
+    atomicMax(stats + 1, displaced ? 2u : entries ? 1u : 0u);
+    if (displaced) atomicAdd(stats + 2, displaced);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // The protein path (ApplyKmerProcessor.java:122-148 with ProteinKmers at :123): one kernel.
 //
 // A block owns kBlockProteins consecutive proteins. Every window of theirs is probed with
@@ -486,6 +585,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 
   const uint64_t* __restrict__ slots = a.slots;
   const uint32_t nb = a.n_buckets;
+  const bool two_choice = a.two_choice != 0;
   const uint8_t* lut = sm.lut;
   uint32_t* cq = sm.chain_q[wave];
   uint32_t cn = 0;  // wave-uniform queue length
@@ -512,9 +612,10 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       uint32_t fid = 0, sid = 0;
 #ifdef KMA_TUNE_COUNT
       uint32_t walked = 0;
-      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid, &walked);
+      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid, two_choice,
+                                  &walked);
 #else
-      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid);
+      const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid, two_choice);
 #endif
       if (hit) record_hit<P>(sm, a, span_lo, multiset, p, fid, sid);
 #ifdef KMA_TUNE_COUNT
@@ -987,7 +1088,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
         if constexpr (kWide)
           hit = walk_chain_wide(a.slots, nb, bk[h][j], key[h][j], fid, sid);
         else
-          hit = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid, sid);
+          hit = walk_chain(a.slots, nb, bk[h][j], key[h][j], fid, sid, a.two_choice != 0);
       }
       if (a.strict_pass && hit) {  // KmerFactory.Strict: locations counted by slot id
         if (a.strict_pass == 1) atomicAdd(a.slot_count + sid, 1u);
@@ -1397,6 +1498,31 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
   else
     hipLaunchKernelGGL(build_finalize_kernel<false>, g, dim3(256), 0, stream, slots, winner, fids,
                        n_buckets, k, m, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, int m,
+                                   const uint64_t* keys, const uint32_t* fids, uint64_t n,
+                                   uint64_t* sorted_keys, uint32_t* rows, uint32_t* sorted_rows,
+                                   void* temp, size_t* temp_bytes, uint32_t* status,
+                                   hipStream_t stream) {
+  if (wide_k(k) || n_buckets < 2) return hipErrorInvalidValue;
+  // all 64 bits: a row whose key is not a K-mer key (bits above 5K) must not split a run
+  if (!temp)
+    return rocprim::radix_sort_pairs(nullptr, *temp_bytes, keys, sorted_keys, rows, sorted_rows,
+                                     (size_t)n, 0u, 64u, stream);
+  hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n)), dim3(256), 0, stream, rows, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = rocprim::radix_sort_pairs(temp, *temp_bytes, keys, sorted_keys, rows, sorted_rows, (size_t)n,
+                                0u, 64u, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(build_two_choice_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                     slots, n_buckets, k, m, sorted_keys, sorted_rows, fids, n, status);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(build_two_choice_filter_kernel, dim3(grid_for((uint64_t)n_buckets * kSlotsPerBucket)),
+                     dim3(256), 0, stream, slots, n_buckets, k, m, status + 1);
   return hipGetLastError();
 }
 

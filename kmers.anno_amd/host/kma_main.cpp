@@ -348,6 +348,7 @@ class ApplyKmerProcessor {
         stagingThreads_ = std::max(0, std::atoi(need("--staging-threads").c_str()));
       } else if (a == "--batch") {
         batchResidues_ = std::strtoull(need("--batch").c_str(), nullptr, 10);
+        if (fasta_) fastaSegment_ = std::max<size_t>(1, (size_t)batchResidues_);
       } else if (a == "--callers" && fasta_) {
         callers_ = std::max(1, std::atoi(need("--callers").c_str()));
       } else if (!a.empty() && a[0] == '-' && a.size() > 1) {
@@ -603,7 +604,11 @@ class ApplyKmerProcessor {
     log_info("%zu FASTA files to process.", fastaFiles_.size());
     const auto t0 = Clock::now();
     const bool verify = outputType_ == "VERIFY";
-    const size_t seg_bytes = batchResidues_ ? (size_t)batchResidues_ : (size_t)16 << 20;
+    // default segments: 4 MiB (--batch), two native calls in flight (--callers): measured on the
+    // c4 FASTA file (1M proteins, 355 MB) 0.060-0.064 s per file, 16 MiB x 1 caller 0.064-0.071,
+    // 16 MiB x 16 callers 0.24 (concurrent host calls contend for the staging pool and each
+    // allocates its own pinned and device buffers; profiles/r05/fasta_sweep.log)
+    const size_t seg_bytes = fastaSegment_;
     std::atomic<uint64_t> calls{0}, call_us{0}, parse_us{0}, format_us{0};
     uint64_t n_seq = 0, n_res = 0, n_called = 0, n_bytes = 0, n_segs_all = 0;
     double wait_s = 0, write_s = 0;
@@ -787,6 +792,7 @@ class ApplyKmerProcessor {
   int parseThreads_ = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   int stagingThreads_ = -1;  // KMA_OPT_HOST_THREADS for this run (-1: the library's default)
   int callers_ = 2;          // FASTA form: native calls in flight at once
+  size_t fastaSegment_ = (size_t)4 << 20;  // FASTA form: bytes per segment (--batch)
   uint64_t batchResidues_ = 16u << 20;  // 0: a native call per genome on its parse worker
   double tableLoadS_ = 0;
   std::string kmerDbFile_, goodRoleFile_, inDir_;
@@ -820,7 +826,7 @@ const char* kApplyFastaUsage =
     " --device D        HIP device ordinal (default 0)\n"
     " --threads N       parser / caller threads (default min(16, cores))\n"
     " --staging-threads N  library threads packing a call's residues (default: min(16, cores))\n"
-    " --batch B         bytes of FASTA per segment (one native call each; default 16777216)\n"
+    " --batch B         bytes of FASTA per segment (one native call each; default 4194304)\n"
     " --callers C       segments' native calls in flight at once (default 2)\n";
 
 int run_apply(const std::vector<std::string>& args, bool fasta = false) {

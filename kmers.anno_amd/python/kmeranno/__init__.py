@@ -43,14 +43,16 @@ EXPORTS = (
 
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
-OPT_PACKED_INPUT, OPT_HOST_THREADS, OPT_HOST_SLICE = 6, 7, 8
+OPT_PACKED_INPUT, OPT_HOST_THREADS, OPT_HOST_SLICE, OPT_PLACEMENT = 6, 7, 8, 9
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
-                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0, OPT_HOST_SLICE: 0}
+                OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0, OPT_HOST_SLICE: 0,
+                OPT_PLACEMENT: -1}
+LAYOUT_TWO_CHOICE = 0x100  # layout code flag: two-choice placement (include/kmeranno.h)
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
 _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
               "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
               "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS,
-              "host_slice": OPT_HOST_SLICE}
+              "host_slice": OPT_HOST_SLICE, "placement": OPT_PLACEMENT}
 
 
 class KmerAnnoError(RuntimeError):
@@ -66,7 +68,7 @@ class TableInfo(C.Structure):
                 ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32),
                 ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32),
                 ("slots_per_bucket", C.c_int32), ("replicate_ms", C.c_double),
-                ("replicate_bytes", C.c_uint64)]
+                ("replicate_bytes", C.c_uint64), ("two_choice", C.c_int32), ("pad_", C.c_int32)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
@@ -409,28 +411,42 @@ def bucket_slots(k: int = 8) -> int:
 
 
 def layout_for(k: int, n_buckets: int) -> int:
-    """The size-derived table layout (minimizer length; 0 = flat)."""
+    """The size-derived table layout code (minimizer length, 0 = flat; | LAYOUT_TWO_CHOICE when
+    the creators try two-choice placement first)."""
     return int(load().kma_table_layout_for(k, n_buckets))
 
 
 # The creators' layout rule by measurement (kma_internal.h kRetryDisplaced / kMaxDisplaced /
-# kMaxChain; kma_abi.cpp create_from_device_keys).
+# kMaxChain / kMaxDisplacedTwoChoice; kma_abi.cpp create_from_device_keys).
 RETRY_DISPLACED, MAX_DISPLACED, MAX_CHAIN = 0.10, 0.15, 32
+MAX_DISPLACED_TWO_CHOICE = 0.40
 
 
 def choose_layout(k: int, n_buckets: int, build):
     """The library creators' layout choice for hosts that build tables on the device
     themselves (kma_table_build_device into their own buffer, e.g. one RCCL broadcasts):
-    build(m) builds the table with layout m into the caller's buffer and returns its status
-    {full, entries, longest chain, displaced}. Returns (m, status); the kept layout is the one
-    built last. A forced layout (OPT_LAYOUT) is the size rule's answer."""
-    m = layout_for(k, n_buckets)
-    st = build(m)
-    if get_option(OPT_LAYOUT) != -1:
-        return m, st
-
+    build(code) builds the table with that layout code (minimizer length | LAYOUT_TWO_CHOICE)
+    into the caller's buffer and returns its status {failed, entries, longest chain,
+    displaced}. Returns (code, status); the kept layout is the one built last. Two-choice
+    placement first (narrow tables); a failed two-choice build falls back to the chained rule.
+    A forced layout (OPT_LAYOUT) is the size rule's answer."""
     def disp(s):
         return s[3] / max(s[1], 1)
+    forced = get_option(OPT_LAYOUT) != -1
+    code = layout_for(k, n_buckets)
+    m = code & 0xFF
+    if code & LAYOUT_TWO_CHOICE:
+        st = build(code)
+        if st[0] == 0:
+            if not forced and m != 0 and disp(st) > MAX_DISPLACED_TWO_CHOICE:
+                s2 = build(LAYOUT_TWO_CHOICE)
+                if s2[0] == 0 and 2 * s2[3] < st[3]:
+                    return LAYOUT_TWO_CHOICE, s2
+                st = build(code)
+            return code, st
+    st = build(m)
+    if forced:
+        return m, st
     m6, m7 = min(k, 6), min(k, 7)
     if m == m6 and m6 != m7 and disp(st) > RETRY_DISPLACED:
         s2 = build(m7)
@@ -456,13 +472,23 @@ def build_device(d_slots: int, n_buckets: int, d_winner: int, d_keys: int, d_fid
 
 
 def annotate_proteins(table: SignatureTable, residues: np.ndarray, offsets: np.ndarray,
-                      min_hits: int = 5, flags: int = 0, n_fid: int = 0):
-    """Host form of the apply loop: returns (fid, count, status, tally-or-None)."""
+                      min_hits: int = 5, flags: int = 0, n_fid: int = 0, out=None):
+    """Host form of the apply loop: returns (fid, count, status, tally-or-None). out: the
+    caller's (fid, count, status[, tally]) arrays to fill (reused buffers, as a JNI caller
+    passes its direct buffers: fresh arrays cost their first-touch page faults)."""
     residues = np.ascontiguousarray(residues, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     n = len(offsets) - 1
-    fid, cnt, st = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint8)
-    tally = np.zeros(n_fid, np.uint32) if n_fid else None
+    if out is not None:
+        fid, cnt, st = out[:3]
+        assert fid.dtype == np.int32 and cnt.dtype == np.int32 and st.dtype == np.uint8
+        assert len(fid) == len(cnt) == len(st) == n and fid.flags.c_contiguous
+        tally = (out[3] if len(out) > 3 else np.zeros(n_fid, np.uint32)) if n_fid else None
+        if tally is not None:
+            tally[:] = 0
+    else:
+        fid, cnt, st = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint8)
+        tally = np.zeros(n_fid, np.uint32) if n_fid else None
     _check(load().kma_annotate_proteins(table._h, residues, offsets, n, min_hits, flags, fid, cnt,
                                         st, tally.ctypes.data if n_fid else None, n_fid))
     return fid, cnt, st, tally

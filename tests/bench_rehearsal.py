@@ -137,7 +137,8 @@ class _Info:
         self.n_buckets = nb
         self.bytes = nb * 8 * 8
         self.device = 0 if device is None else device
-        self.minimizer_len = m
+        self.minimizer_len = m & 0xFF
+        self.two_choice = 1 if m & 0x100 else 0
         self.k = K
 
 
@@ -180,6 +181,7 @@ class _Workspace:
 class StubKmerAnno(types.ModuleType):
     STATUS_CALLED = 1
     OPT_PACKED_INPUT = 6
+    LAYOUT_TWO_CHOICE = 0x100
     HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
                           ("frame", "u1"), ("pad", "<u2")])
 
@@ -209,7 +211,7 @@ class StubKmerAnno(types.ModuleType):
         return 8
 
     def choose_layout(self, k, nb, build):
-        return 6, build(6)
+        return 6 | 0x100, build(6 | 0x100)
 
     def build_device(self, d_slots, nb, d_winner, d_keys, d_fids, n, d_status, stream, k=8,
                      layout=-1):

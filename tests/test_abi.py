@@ -39,16 +39,17 @@ def test_options_set_get_validate_restore(native_lib):
         assert k.get_option(o) == v
     for o, bad in ((k.OPT_LAYOUT, 5), (k.OPT_BLOCK_PROTEINS, 9), (k.OPT_DEFER, 65),
                    (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 3),
-                   (k.OPT_HOST_THREADS, 65), (k.OPT_HOST_SLICE, -1), (99, 0)):
+                   (k.OPT_HOST_THREADS, 65), (k.OPT_HOST_SLICE, -1), (k.OPT_PLACEMENT, 2),
+                   (99, 0)):
         with pytest.raises(k.KmerAnnoError) as e:
             k.set_option(o, bad)
         assert e.value.code == k.E_INVALID
     with k.options(layout=7, block_proteins=1, defer=0, host_pieces=3, hash_slice=1000,
-                   packed_input=0, host_threads=4, host_slice=12345):
-        assert [k.get_option(o) for o in range(1, 9)] == [7, 1, 0, 3, 1000, 0, 4, 12345]
+                   packed_input=0, host_threads=4, host_slice=12345, placement=0):
+        assert [k.get_option(o) for o in range(1, 10)] == [7, 1, 0, 3, 1000, 0, 4, 12345, 0]
         assert k.layout_for(8, 1000) == 7
-    assert [k.get_option(o) for o in range(1, 9)] == [-1, 0, -1, 0, 0, 1, 0, 0]
-    assert k.layout_for(8, 1000) == 6
+    assert [k.get_option(o) for o in range(1, 10)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1]
+    assert k.layout_for(8, 1000) == 6 | k.LAYOUT_TWO_CHOICE
     src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
     assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src
 
@@ -80,25 +81,35 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
 
 def test_table_layout_host_helper(native_lib, monkeypatch):
     """Layout choice: minimizer m = 6 up to 134M keys at load factor 0.5 (2^28 slots), m = 7
-    beyond; the KMA_OPT_LAYOUT option forces 0 (flat), 6 or 7, read per call."""
+    beyond; the KMA_OPT_LAYOUT option forces 0 (flat), 6 or 7, read per call. Narrow tables are
+    tried with two-choice placement first (the layout code's flag) unless KMA_OPT_PLACEMENT = 0;
+    wide tables never."""
     import kmeranno
+    tc = kmeranno.LAYOUT_TWO_CHOICE
     kmeranno.set_option(kmeranno.OPT_LAYOUT, -1)
     nb6 = (1 << 28) // kmeranno.bucket_slots()
-    assert kmeranno.layout_for(8, nb6) == 6
-    assert kmeranno.layout_for(8, nb6 + 1) == 7
-    assert kmeranno.layout_for(5, 1 << 30) == 5  # m <= K
+    assert kmeranno.layout_for(8, nb6) == 6 | tc
+    assert kmeranno.layout_for(8, nb6 + 1) == 7 | tc
+    assert kmeranno.layout_for(5, 1 << 30) == 5 | tc  # m <= K
+    assert kmeranno.layout_for(10, 1000) == 6  # wide: chains
+    with kmeranno.options(placement=0):
+        assert kmeranno.layout_for(8, nb6) == 6
     kmeranno.set_option(kmeranno.OPT_LAYOUT, 0)
-    assert kmeranno.layout_for(8, 1000) == 0
+    assert kmeranno.layout_for(8, 1000) == 0 | tc
     kmeranno.set_option(kmeranno.OPT_LAYOUT, 7)
-    assert kmeranno.layout_for(8, 1000) == 7
+    assert kmeranno.layout_for(8, 1000) == 7 | tc
 
 
 def test_choose_layout_rule():
-    """kmeranno.choose_layout mirrors the creators' rule (kma_abi.cpp create_from_device_keys)
-    on the round-3 c5 sweep's build statistics {full, entries, longest chain, displaced}: m = 6
-    kept at load factor 0.5, rebuilt m = 7 at 0.75 and 0.9 (flat halves neither), flat for keys
-    piling onto few minimizers; the kept layout is built last."""
+    """kmeranno.choose_layout mirrors the creators' rule (kma_abi.cpp create_from_device_keys).
+    Two-choice placement first: kept when it builds (the size rule's m), rebuilt flat when more
+    than 40% of the keys are outside their home and flat halves them. A failed two-choice build
+    falls back to the chained rule, shown on the round-3 c5 sweep's build statistics {full,
+    entries, longest chain, displaced}: m = 6 kept at load factor 0.5, rebuilt m = 7 at 0.75 and
+    0.9 (flat halves neither), flat for keys piling onto few minimizers; the kept layout is built
+    last."""
     import kmeranno
+    tc = kmeranno.LAYOUT_TWO_CHOICE
     n = 99_821_868
     sweep = {  # load factor -> layout -> status
         0.5: {6: [0, n, 10, int(0.0770 * n)], 7: [0, n, 7, int(0.0239 * n)], 0: [0, n, 6, int(0.0086 * n)]},
@@ -112,9 +123,22 @@ def test_choose_layout_rule():
 
         def build(m):
             built.append(m)
-            return st[m]
+            return [1, 0, 0, 0] if m & tc else st[m]  # the two-choice build fails
         m, s = kmeranno.choose_layout(8, 25_000_000, build)
+        assert built[0] == 6 | tc
         assert m == want[case] and built[-1] == m and s == st[m], (case, built)
+    two = {6 | tc: [0, n, 2, int(0.21 * n)], tc: [0, n, 2, int(0.05 * n)]}
+    for disp6, expect in ((0.21, 6 | tc), (0.45, tc), (0.45 - 1, 6 | tc)):
+        built = []
+        two[6 | tc][3] = int(disp6 * n) if disp6 > 0 else int(0.45 * n)
+        if disp6 < 0:  # crowded, but flat does not halve the displaced keys
+            two[tc][3] = int(0.30 * n)
+
+        def build2(m):
+            built.append(m)
+            return two[m]
+        m, s = kmeranno.choose_layout(8, 25_000_000, build2)
+        assert m == expect and built[-1] == m and s == two[m], (disp6, built)
 
 
 def _pack_reference(res: np.ndarray) -> np.ndarray:

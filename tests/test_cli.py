@@ -171,6 +171,37 @@ def test_kma_apply_corrupt_gto_mid_directory(kma_bin, oracle_c, tmp_path, batch)
     assert out.stdout.splitlines() == exp
 
 
+@pytest.mark.gpu
+def test_kma_apply_verify_rows_in_gto_feature_order(kma_bin, oracle_c, small_gto, apply_inputs,
+                                                    tmp_path):
+    """VERIFY rows follow one documented rule: the order of the GTO's features array (pegs only),
+    which is what Genome.getPegs() is taken to return (the Genome class is
+    external, its order unpinned). A genome whose pegs are shuffled (ids out of order, RNA
+    features in between) reports its called pegs in exactly that file order, not sorted by id."""
+    d, rows, roles, pegs = apply_inputs
+    rng = np.random.default_rng(5)
+    order = rng.permutation(len(pegs))
+    feats = []
+    for j, i in enumerate(order):
+        feats.append(pegs[i])
+        if j % 7 == 0:
+            feats.append({"id": f"fig|97478.30.rna.{j}", "type": "rna", "function": "tRNA"})
+    gto = {"id": "97478.30", "scientific_name": "shuffled", "genetic_code": 11,
+           "features": feats}
+    gdir = tmp_path / "gtos"
+    gdir.mkdir()
+    (gdir / "97478.30.gto").write_text(json.dumps(gto))
+    _, exp_verify = _expected(oracle_c, small_gto, rows, roles, [pegs[i] for i in order], 5)
+    out = subprocess.run([kma_bin, "apply", "--format", "VERIFY", str(d / "kmerdb.tbl"),
+                          str(d / "roles.in.use"), str(gdir)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    got = out.stdout.splitlines()
+    assert got == exp_verify and len(got) > 20
+    ids = [ln.split("\t")[1] for ln in got[1:]]
+    assert ids != sorted(ids)  # file order, not id order
+
+
 def test_kma_apply_errors(kma_bin, apply_inputs, tmp_path):
     d, _, _, _ = apply_inputs
     r = subprocess.run([kma_bin, "apply", str(d / "kmerdb.tbl"), str(d / "roles.in.use"),

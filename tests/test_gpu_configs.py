@@ -125,15 +125,21 @@ def test_config5_load_factor_09(kma, oracle_c, c5data, monkeypatch):
     with kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=0.9) as t:
         i = t.info
         kept = i.minimizer_len
-        print(f"LF 0.9: layout m={kept}, displaced {i.n_displaced / i.n_entries:.2%}, "
-              f"longest chain {i.max_probe}", flush=True)
+        print(f"LF 0.9: layout m={kept} two-choice={i.two_choice}, displaced "
+              f"{i.n_displaced / i.n_entries:.2%}, longest probe {i.max_probe}", flush=True)
         assert i.n_buckets == kma.buckets_for(len(sig.keys), 0.9)
-        # the creators' rule: m = 6 displaces ~24% -> rebuilt m = 7 (~17%, fewer); flat (~13%)
-        # halves neither the displaced keys nor the chain -> m = 7 kept (7.7 ms vs m = 6's 10.0)
-        assert kept == 7
-        assert i.n_displaced > 0.02 * i.n_entries and i.max_probe >= 2
+        # two-choice placement at the size rule's m = 6: every key in its home or its alt bucket
+        assert i.two_choice == 1 and kept == 6 and i.max_probe == 2
+        assert i.n_displaced > 0.02 * i.n_entries
         got = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
     for a, b in zip(got, ref):
+        assert (a == b).all()
+    with kma.options(placement=0):  # chains: m = 6 displaces ~24% -> rebuilt m = 7 (~17%)
+        with kma.SignatureTable.from_packed(sig.keys, sig.fids, K, load_factor=0.9) as t:
+            i = t.info
+            assert i.two_choice == 0 and i.minimizer_len == 7 and i.max_probe >= 2
+            chained = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
+    for a, b in zip(chained, ref):
         assert (a == b).all()
     fid, cnt, st, tally = got
     assert (tally == np.bincount(fid[st == 1], minlength=n_fid)).all()

@@ -21,15 +21,19 @@ pytestmark = pytest.mark.gpu
 K = 8
 
 
-@pytest.fixture(params=["auto", "7", "0"], ids=["m-auto", "m7", "flat"])
+@pytest.fixture(params=["auto", "7", "0", "chained"], ids=["m-auto", "m7", "flat", "chained"])
 def layout(request, monkeypatch):
     """Table layouts: the size-derived minimizer layout (m = 6 up to 134M keys at load factor
     0.5, c5 included), the m = 7 layout of larger tables, and the flat fallback (the KMA_OPT_LAYOUT
-    option, read per table creation)."""
+    option, read per table creation), each with the default two-choice placement; and the
+    size-derived layout with overflow chains (KMA_OPT_PLACEMENT = 0: the placement of wide
+    tables and of a two-choice build that fails)."""
     import kmeranno
     kmeranno.load()
-    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1 if request.param == "auto" else int(request.param))
-    return request.param
+    p = request.param
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1 if p in ("auto", "chained") else int(p))
+    kmeranno.set_option(kmeranno.OPT_PLACEMENT, 0 if p == "chained" else -1)
+    return p
 
 
 @pytest.fixture(params=["direct", "defer"])
@@ -144,10 +148,12 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags, input_mode)
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, flags)
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
         assert t.info.n_entries == ot.size
-        if layout != "auto":
+        if layout in ("7", "0"):
             assert t.info.minimizer_len == int(layout)
         elif lf == 0.5:
             assert t.info.minimizer_len == 6  # size rule, few displaced keys
+        if lf <= 0.9:
+            assert t.info.two_choice == (0 if layout == "chained" else 1)
         if lf == 0.9:
             assert t.info.max_probe >= 2 and t.info.n_displaced > 0
         fid, cnt, st, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, flags)
@@ -446,7 +452,19 @@ def test_device_api_with_torch_buffers(kma):
     st4 = status.cpu().numpy()
     assert st4[0] == 0 and st4[1] == len(np.unique(wl.keys)) and st4[2] >= 1
     t = kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0)
-    assert t.info.minimizer_len == kma.layout_for(K, nb)
+    assert t.info.minimizer_len == kma.layout_for(K, nb) & 0xFF and t.info.two_choice == 0
+    # the same rows with two-choice placement (the layout code's flag) into a second buffer
+    code = kma.layout_for(K, nb)
+    assert code & kma.LAYOUT_TWO_CHOICE
+    slots2 = torch.empty_like(slots)
+    status2 = torch.zeros(4, dtype=torch.int32, device=dev)
+    kma.build_device(slots2.data_ptr(), nb, 0, keys.data_ptr(), fids.data_ptr(), len(wl.keys),
+                     status2.data_ptr(), stream, layout=code)
+    torch.cuda.synchronize()
+    s2 = status2.cpu().numpy()
+    assert s2[0] == 0 and s2[1] == st4[1] and s2[2] in (1, 2)
+    t2 = kma.SignatureTable.wrap_device(slots2.data_ptr(), nb, K, 0, code)
+    assert t2.info.two_choice == 1 and t2.info.minimizer_len == code & 0xFF
     n_res = int(wl.offsets[-1])
     ws = kma.Workspace(0, n_res)
     res = torch.from_numpy(wl.residues).to(dev)
@@ -462,6 +480,10 @@ def test_device_api_with_torch_buffers(kma):
     torch.cuda.synchronize()
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as th:
         hf, hc, hs, ht = kma.annotate_proteins(th, wl.residues, wl.offsets, 5, 0, n_fid=1000)
+    got2 = kma.annotate_proteins(t2, wl.residues, wl.offsets, 5, 0, n_fid=1000)
+    for a, b in zip(got2, (hf, hc, hs, ht)):
+        assert (a == b).all()
+    t2.close()
     assert (fid.cpu().numpy() == hf).all() and (cnt.cpu().numpy() == hc).all()
     assert (st.cpu().numpy() == hs).all()
     assert (tally.cpu().numpy().astype(np.uint32) == ht).all()
