@@ -796,12 +796,16 @@ def main():
                     help="KMA_OPT_PACKED_INPUT: 1 (default) = batches of >= 2^25 residues are "
                          "packed to 5 bits by a pack kernel inside the step, then the packed "
                          "probe; 2 = every batch; 0 = the probe packs ASCII itself")
+    ap.add_argument("--placement", default="auto", choices=("auto", "chained"),
+                    help="KMA_OPT_PLACEMENT: auto (default) = two-choice placement for K <= 8 "
+                         "tables, chains if that build fails; chained = overflow chains (A/B runs)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, check the multi-rank outputs, tally and table against "
                          "single-rank calls on rank 0 (exit 1 on a mismatch)")
     args = ap.parse_args()
 
     kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, args.packed_input)
+    kmeranno.set_option(kmeranno.OPT_PLACEMENT, 0 if args.placement == "chained" else -1)
     if args.workload == "genomes":  # a command-level run: `kma apply` as a child process
         bench_genomes(args)
         return

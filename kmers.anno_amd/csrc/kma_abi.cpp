@@ -1052,10 +1052,11 @@ int kma_table_destroy(kma_table* table) {
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
                            uint32_t* d_winner, const uint64_t* d_keys, const uint32_t* d_fids,
                            uint64_t n, uint32_t* d_status, void* stream) {
-  if (!d_slots || !d_winner || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
+  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
+  // d_winner is the chained build's scratch; a two-choice build does not read it.
+  if (!d_slots || (!two && !d_winner) || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
     return fail(KMA_E_INVALID, "null argument");
   if (int rc = check_k(k)) return rc;
-  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
   const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout & kma::kLayoutMask;
   if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
     return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
@@ -1240,7 +1241,16 @@ enum class Input { kAscii, kPackOnDevice, kStream };
 constexpr uint64_t kPackMinResidues = 1ull << 25;
 bool pack_on_device(uint64_t n_residues) {
   const int64_t v = opt(KMA_OPT_PACKED_INPUT);
-  return v == 2 || (v == 1 && n_residues >= kPackMinResidues);
+  return n_residues > 0 && (v == 2 || (v == 1 && n_residues >= kPackMinResidues));
+}
+
+// The workspace's packed stream for device calls that pack (sized for its reserved residues).
+int ensure_packed(kma_workspace* ws) {
+  if (ws->d_packed) return KMA_OK;
+  DeviceScope ds(ws->device);
+  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
+  KMA_HIP(hipMalloc(&ws->d_packed, kma::packed_bytes(ws->res_cap + kResPad)));
+  return KMA_OK;
 }
 
 // The protein path on one replica (device buffers, asynchronous on s).
@@ -1559,8 +1569,10 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
   free_protein_scratch(ws);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
-  KMA_HIP(hipMalloc(&ws->d_packed, kma::packed_bytes(n_residues + kResPad)));
   ws->res_cap = n_residues;
+  // The device call's packed stream only when a call of this size would pack (host calls and
+  // small device calls never read it); a call that packs later allocates it then.
+  if (pack_on_device(n_residues)) return ensure_packed(ws);
   return KMA_OK;
 }
 
@@ -1665,12 +1677,15 @@ int kma_annotate_proteins_device(const kma_table* t, kma_workspace* ws, const ui
   if (n_residues > ws->res_cap)
     return fail(KMA_E_CAPACITY, "workspace reserved for %llu residues, call needs %llu",
                 (unsigned long long)ws->res_cap, (unsigned long long)n_residues);
+  const bool pack = pack_on_device(n_residues);
+  if (pack)
+    if (int rc = ensure_packed(ws)) return rc;
   DeviceScope ds(r->device);
   if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", r->device);
   return annotate_proteins_on(t, *r, ws, d_residues, d_offsets, n_seq, n_residues, min_hits,
                               flags, d_fid, d_count, d_status, d_tally, n_fid,
                               static_cast<hipStream_t>(stream),
-                              pack_on_device(n_residues) ? Input::kPackOnDevice : Input::kAscii);
+                              pack ? Input::kPackOnDevice : Input::kAscii);
 }
 
 uint64_t kma_packed_bytes(uint64_t n_residues) { return kma::packed_bytes(n_residues); }

@@ -1290,7 +1290,8 @@ __device__ __forceinline__ uint64_t emit_offset(const ContigArgs& a, uint32_t b)
   return s;
 }
 
-// Calls of more than kDirectGroups groups (> 67M bases): one block turns the group sums into
+// Calls of more than kDirectGroups groups (> kDirectGroups x kScanGroup x kContigTile = 268M
+// bases): one block turns the group sums into
 // exclusive prefixes in place, so an emit block reads one value instead of summing every group
 // before its own (which grows as blocks x groups: ~2e9 loads at 1 Gbp).
 __global__ __launch_bounds__(1024) void contigs_group_scan_kernel(uint64_t* sums, uint32_t n) {

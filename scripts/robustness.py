@@ -134,13 +134,12 @@ def main():
         byt[:, :, j] = letters[((pick >> np.uint64(5 * (7 - j))) & np.uint64(31)).astype(np.int64)]
     ares = np.concatenate([byt.reshape(-1), np.zeros(64, np.uint8)])
     aoff = (np.arange(200_001, dtype=np.uint64) * 240)
-    for forced in (None, "7"):
-        if forced:
-            os.environ["KMA_MINIMIZER"] = forced
-        with kmeranno.SignatureTable.from_packed(akeys, afids, K) as t:
+    for forced in (None, 7):
+        with kmeranno.options(**({"layout": forced} if forced else {})):
+            t = kmeranno.SignatureTable.from_packed(akeys, afids, K)
+        with t:
             out({"case": "adversarial", "forced_layout": forced, "keys": len(akeys), **info(t),
                  **time_device(t, ares, aoff)})
-        os.environ.pop("KMA_MINIMIZER", None)
     # 3. per-genome host-entry latency against the c2 table
     n_seq, t_size, n_fid, seed = synth.CONFIGS["c2"]
     sig = synth.make_table(t_size, n_fid, seed, K)

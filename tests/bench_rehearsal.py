@@ -181,6 +181,7 @@ class _Workspace:
 class StubKmerAnno(types.ModuleType):
     STATUS_CALLED = 1
     OPT_PACKED_INPUT = 6
+    OPT_PLACEMENT = 9
     LAYOUT_TWO_CHOICE = 0x100
     HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
                           ("frame", "u1"), ("pad", "<u2")])

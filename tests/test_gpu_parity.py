@@ -499,6 +499,43 @@ def test_device_api_with_torch_buffers(kma):
     t.close()
 
 
+@pytest.mark.parametrize("reserve", [0, 1000, 1 << 20])
+def test_device_call_all_empty_proteins_packed(kma, reserve):
+    """A device call whose proteins are all empty (n_residues = 0) under KMA_OPT_PACKED_INPUT = 2,
+    on a workspace never reserved, reserved small, or reserved for a call that packs: every
+    protein is NONE with count 0, and a packed call on the same workspace afterwards is
+    bit-exact (the packed stream is allocated when a call first packs)."""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_workload(200, 20_000, 300, seed=33)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    n = 7
+    off0 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    res0 = torch.zeros(64, dtype=torch.uint8, device=dev)
+    fid = torch.full((wl.n_seq,), -7, dtype=torch.int32, device=dev)
+    cnt = torch.full((wl.n_seq,), -7, dtype=torch.int32, device=dev)
+    st = torch.full((wl.n_seq,), 9, dtype=torch.uint8, device=dev)
+    with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t, kma.options(packed_input=2):
+        ws = kma.Workspace(0, reserve) if reserve else kma.Workspace(0)
+        kma.annotate_proteins_device(t, ws, res0.data_ptr(), off0.data_ptr(), n, 0, 5, 0,
+                                     fid.data_ptr(), cnt.data_ptr(), st.data_ptr(), 0, 0, stream)
+        torch.cuda.synchronize()
+        assert (st.cpu().numpy()[:n] == kma.STATUS_NONE).all()
+        assert (cnt.cpu().numpy()[:n] == 0).all()
+        n_res = int(wl.offsets[-1])
+        ws.reserve(n_res, wl.n_seq)
+        res = torch.from_numpy(wl.residues).to(dev)
+        off = torch.from_numpy(wl.offsets.view(np.int64)).to(dev)
+        kma.annotate_proteins_device(t, ws, res.data_ptr(), off.data_ptr(), wl.n_seq, n_res, 5, 0,
+                                     fid.data_ptr(), cnt.data_ptr(), st.data_ptr(), 0, 0, stream)
+        torch.cuda.synchronize()
+        hf, hc, hs, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0)
+        assert (fid.cpu().numpy() == hf).all() and (cnt.cpu().numpy() == hc).all()
+        assert (st.cpu().numpy() == hs).all()
+        ws.close()
+
+
 def test_workspace_timing(kma):
     """kma_workspace_timing: hipEvent durations of device calls (the pack kernel and the
     protein kernel; the protein kernel alone on ASCII input)."""
