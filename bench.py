@@ -64,7 +64,7 @@ MALL_BYTES = 256 << 20  # Infinity Cache: a table below it is served on-die (MI3
 GATHER_BIN = os.path.join(ROOT, "kmers.anno_amd", "build", "kma_gather_bench")
 # Per-launch PMC traffic of the dominant kernels of this build (scripts/gpu_traffic.sh +
 # scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05_traffic.json")
 METRIC = "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs roofline"
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "

@@ -99,6 +99,15 @@ class StagingPool {
  public:
   template <class F>
   void run(uint64_t n, size_t width, F&& fn) {
+    run_with(n, width, std::forward<F>(fn), [](auto& help) { while (help()) {} });
+  }
+  // run() whose calling thread runs caller(help) instead of draining the job: help() makes one
+  // of the job's calls (in index order with the pool threads) on the calling thread and returns
+  // false once every call has been taken. The calling thread can so act on the job's progress
+  // (the host call issues each segment's copy as soon as its chunks are packed) and help
+  // whenever it would otherwise wait. Returns after every call has returned.
+  template <class F, class C>
+  void run_with(uint64_t n, size_t width, F&& fn, C&& caller) {
     width = std::max<size_t>(1, std::min<size_t>(width, n));
     Job j;
     j.n = n;
@@ -112,6 +121,13 @@ class StagingPool {
       jobs_.push_back(&j);
       cv_.notify_all();
     }
+    auto help = [&j]() {
+      const uint64_t i = j.next.fetch_add(1);
+      if (i >= j.n) return false;
+      j.call(j.fn, i);
+      return true;
+    };
+    caller(help);
     drain(j);
     if (width > 1) {
       std::unique_lock<std::mutex> lk(mu_);
@@ -1308,10 +1324,11 @@ int check_protein_call(const kma_table* t, int min_hits, uint32_t flags) {
 
 // One shard [lo, hi) of a host protein call on replica r (host buffers, synchronous).
 // Host bytes -> pinned staging -> device, pipelined: the input is cut into pieces of whole
-// proteins; the staging pool fills piece i's part of the pinned buffer (copying or packing in
-// 2 MiB chunks) and ONE copy per piece goes on the copy stream, so piece i + 1 is staged while
-// piece i's copy and kernel run. One large copy per piece: r04g's trace of 153 chunk-sized
-// copies (c5) kept the DMA engine idle a quarter of the time (profiles/r04/e2e_trace_r04g.json).
+// proteins, one kernel per piece. ASCII input (stage_h2d): the staging pool copies piece i's
+// part of the pinned buffer in 2 MiB chunks and ONE copy per piece goes on the copy stream, so
+// piece i + 1 is staged while piece i's copy and kernel run (r04g's trace of 153 chunk-sized
+// copies kept the DMA engine idle a quarter of the time, profiles/r04/e2e_trace_r04g.json).
+// Packed input (the default): streamed segments, below in protein_shard.
 hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size_t len,
                      int device, hipStream_t s) {
   constexpr size_t kChunk = 2u << 20;
@@ -1324,13 +1341,14 @@ hipError_t stage_h2d(uint8_t* d_dst, uint8_t* h_pinned, const uint8_t* src, size
   return len ? hipMemcpyAsync(d_dst, h_pinned, len, hipMemcpyHostToDevice, s) : hipSuccess;
 }
 
-// The packed form of stage_h2d: stream groups [ga, gb) (64 residues, 40 bytes each) packed from
-// src (residue 64 ga onwards; residues past n_res read as no code) into the pinned buffer in
-// chunks of 2^15 groups (2M residues) on the staging pool, then copied to d_stream in one
-// copy; `tail` extra zero bytes (the kernel's read padding) follow the last group.
+// The packed form of stage_h2d (piece-wise copies, kStreamedCopies = 0): stream groups [ga, gb)
+// (64 residues, 40 bytes each) packed from src (residue 64 ga onwards; residues past n_res read
+// as no code) into the pinned buffer in chunks of 2^15 groups (2M residues) on the staging
+// pool, then copied to d_stream in one copy; `tail` extra zero bytes (the kernel's read
+// padding) follow the last group.
 hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* lut,
                           const uint8_t* residues, uint64_t n_res, uint64_t ga, uint64_t gb,
-                          uint64_t tail, int device, hipStream_t s) {
+                          uint64_t tail, hipStream_t s) {
   constexpr uint64_t kChunkGroups = 1u << 15;
   const uint64_t n_chunks = std::max<uint64_t>(1, (gb - ga + kChunkGroups - 1) / kChunkGroups);
   staging_pool().run(n_chunks, staging_threads(), [&](uint64_t i) {
@@ -1339,12 +1357,19 @@ hipError_t stage_pack_h2d(uint8_t* d_stream, uint8_t* h_stream, const uint8_t* l
     const uint64_t bytes = 40 * (g1 - g0) + (g1 == gb ? tail : 0);
     kma::pack_residues_host(lut, residues + r0, r1 > r0 ? r1 - r0 : 0, h_stream + 40 * g0, bytes);
   });
-  (void)device;
   const uint64_t bytes = 40 * (gb - ga) + tail;
   return bytes ? hipMemcpyAsync(d_stream + 40 * ga, h_stream + 40 * ga, bytes,
                                 hipMemcpyHostToDevice, s)
                : hipSuccess;
 }
+
+// Streamed copies of packed input (protein_shard): the stream is copied in segments as soon as
+// they are packed, instead of one copy per piece after the whole piece is packed (KMA_HOST_STREAM
+// = 0 builds the piece-wise pipeline for A/B runs).
+#ifndef KMA_HOST_STREAM
+#define KMA_HOST_STREAM 1
+#endif
+constexpr bool kStreamedCopies = KMA_HOST_STREAM != 0;
 
 // Host-side phase times of the last host protein shard call (kma_debug_host_profile, for the
 // host-call measurements in scripts/e2e_host.py): ms in setup (context, reservations, offsets),
@@ -1388,15 +1413,19 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   KMA_HIP(c->h_out.reserve(out_bytes));
   if (int rc = kma_workspace_reserve_batch(c->ws, nres, n)) return rc;
   // Stage: rebased offsets, then the residues (and, with the last piece, their zero padding)
-  // in pieces of whole proteins, in one pinned buffer. Piece i's copy goes on copy stream
+  // in pieces of whole proteins, in one pinned buffer. Piece i's copies go on copy stream
   // i % 2 (the offsets with piece 0); the kernel of piece i waits for piece i's event on the
   // compute stream, so the staging and transfer of piece i + 1 run under the kernel of piece i,
   // and two pieces' copies may run at once on two DMA engines (pieces of >= kPieceBytes residues,
-  // at most KMA_HOST_PIECES (default 8, <= kMaxPieces; read per call); a small call is one
-  // piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (profiles/r02r_host_pipeline/).
+  // at most KMA_HOST_PIECES (default 12 streamed / 8 piece-wise, <= kMaxPieces; read per call);
+  // a small call is one piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (round 2,
+  // profiles/r02r_host_pipeline/).
   constexpr uint64_t kPieceBytes = 16ull << 20;
   const int64_t po = opt(KMA_OPT_HOST_PIECES);
-  const uint64_t max_pieces = po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : 8;
+  // packed input: the stream is copied in segments as it is packed (kStreamedCopies)
+  const bool streamed = packed && kStreamedCopies;
+  const uint64_t max_pieces =
+      po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : streamed ? 12 : 8;
   uint8_t* hin = c->h_in.p;
   hipStream_t s = c->stream;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
@@ -1409,19 +1438,20 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   uint8_t* d_st = reinterpret_cast<uint8_t*>(d_cnt + n) + (tally ? n_fid * 4ull : 0);
   if (d_tally) KMA_HIP(hipMemsetAsync(d_tally, 0, n_fid * 4ull, s));
   const int n_pieces = (int)std::max<uint64_t>(1, std::min<uint64_t>(max_pieces, nres / kPieceBytes));
-  // Piece sizes ramp up and down (weights 1, 2, 4, ..., 4, 2, 1): a small first piece starts the
-  // link early and a small last piece shortens the tail behind the last copy (its kernel and
-  // its outputs). Round 4's equal eighths left 0.4 ms of kernel and 0.5 ms of output copies
-  // after the last H2D (profiles/r04/e2e_trace_r04h.json).
+  // Piece sizes. Piece-wise copies: ramp up and down (weights 1, 2, 4, ..., 4, 2, 1): a small
+  // first piece starts the link early and a small last piece shortens the tail behind the last
+  // copy (round 4's equal eighths left 0.4 ms of kernel and 0.5 ms of output copies after the
+  // last H2D, profiles/r04/e2e_trace_r04h.json). Streamed copies: the link no longer waits for
+  // a piece, only the kernels do, and those keep up with the link (0.155 vs 0.18 ms per 1/22 of
+  // c5), so equal pieces: the tail is one small piece's kernel (a ramp down's halving pieces
+  // left kernels queued behind the last copy: 0.78 ms, profiles/r05/e2e_streamed_ramp_r05f).
   uint64_t wsum = 0, wcum[kMaxPieces + 1] = {0};
   for (int i = 0; i < n_pieces; ++i) {
     const int edge = std::min(i, n_pieces - 1 - i);
-    wsum += n_pieces >= 4 ? (1u << std::min(edge, 2)) : 1u;
+    wsum += streamed || n_pieces < 4 ? 1u : (1u << std::min(edge, 2));
     wcum[i + 1] = wsum;
   }
-  uint32_t pa = 0;  // first protein of the piece (relative to lo)
-  uint64_t ga = 0;  // packed: first stream group the piece stages
-  uint32_t pbeg[kMaxPieces + 1] = {0};
+  uint32_t pbeg[kMaxPieces + 1] = {0};  // first protein of each piece (relative to lo)
   const uint8_t* hout = c->h_out.p;
   // piece i's outputs back on the d2h stream once its kernel is done (fid, count, status
   // slices; the tally with the last piece), while later pieces copy and run
@@ -1443,44 +1473,123 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
     return KMA_OK;
   };
   const double t_setup = ms_since(t_call);
-  for (int i = 0; i < n_pieces; ++i) {
-    hipStream_t cs = c->copy[i & 1];
-    const Clock::time_point t_piece = Clock::now();
-    uint32_t pb = n;
-    if (i + 1 < n_pieces) {  // first protein starting at or after the piece's residue target
-      const uint64_t target = nres * wcum[i + 1] / wsum;
-      pb = (uint32_t)(std::lower_bound(hoff + pa, hoff + n, target) - hoff);
-    }
-    const uint64_t ra = hoff[pa], rb = i + 1 < n_pieces ? hoff[pb] : nres;
-    if (packed) {  // the group holding the piece boundary goes with the earlier piece
-      const uint64_t gb = i + 1 < n_pieces ? std::min(n_groups, (rb + 63) / 64) : n_groups;
-      KMA_HIP(stage_pack_h2d(c->d_in.p, hin, t->lut, residues + base, nres, ga, gb,
-                             i + 1 == n_pieces ? in_bytes - 40 * n_groups : 0, r.device, cs));
-      ga = gb;
-    } else {
-      KMA_HIP(stage_h2d(c->d_in.p + ra, hin + ra, residues + base + ra, rb - ra, r.device, cs));
-      if (i + 1 == n_pieces) {
-        std::memset(hin + nres, 0, in_bytes - nres);
-        KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres,
-                               hipMemcpyHostToDevice, cs));
-      }
-    }
-    KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
-    const Clock::time_point t_staged = Clock::now();
-    t_stage += std::chrono::duration<double, std::milli>(t_staged - t_piece).count();
-    KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
-    if (pb > pa)
-      if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + pa, pb - pa,
-                                        hoff[pb] - hoff[pa], min_hits, flags, d_fid + pa,
-                                        d_cnt + pa, d_st + pa, d_tally, n_fid, s,
-                                        packed ? Input::kStream : Input::kAscii, hoff[pa]))
-        return rc;
-    if (int rc = outputs_back(i, pa, pb)) return rc;
-    t_launch += ms_since(t_staged);
-    pbeg[i] = pa;
-    pa = pb;
+  // Piece boundaries: the first protein starting at or after each piece's residue target.
+  for (int i = 1; i < n_pieces; ++i) {
+    const uint64_t target = nres * wcum[i] / wsum;
+    pbeg[i] = (uint32_t)(std::lower_bound(hoff + pbeg[i - 1], hoff + n, target) - hoff);
   }
   pbeg[n_pieces] = n;
+  // Piece i's kernel (after its input is on the device: piece_ready[i] on copy stream cs) and
+  // the copy of its outputs.
+  auto launch_piece = [&](int i, hipStream_t cs) -> int {
+    const uint32_t a = pbeg[i], b = pbeg[i + 1];
+    KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
+    KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
+    if (b > a)
+      if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + a, b - a,
+                                        hoff[b] - hoff[a], min_hits, flags, d_fid + a,
+                                        d_cnt + a, d_st + a, d_tally, n_fid, s,
+                                        packed ? Input::kStream : Input::kAscii, hoff[a]))
+        return rc;
+    return outputs_back(i, a, b);
+  };
+  if (streamed) {
+    // Streamed staging: the whole stream is packed by ONE staging-pool job in chunks of
+    // kChunkGroups groups, in stream order, and the calling thread copies it in segments (at most
+    // kSegGroups groups, never across a piece boundary) as soon as a segment's chunks are all
+    // packed, packing chunks itself while it waits; a piece's kernel follows its last segment.
+    // Round 4 packed a whole piece before its one copy: the link idled while each piece was
+    // packed (0.24 and 0.30 ms gaps while the pieces ramped up, profiles/r05/e2e_trace_r05d.txt).
+    // Segments of >= 2.6 MB keep the copies near the one-copy rate (2 MiB copies: 42 vs 51 GB/s).
+    constexpr uint64_t kChunkGroups = 1u << 12, kSegGroups = 1u << 18, kFirstSegGroups = 1u << 16;
+    const uint64_t tail = in_bytes - 40 * n_groups;  // the kernel's read padding, zeroed
+    struct Seg {
+      uint64_t g0, g1;
+      int piece;
+      bool last;  // the piece's last segment: its kernel follows the copy
+      uint32_t chunks;
+    };
+    std::vector<Seg> segs;
+    std::vector<uint32_t> chunk_seg;  // chunk -> segment
+    std::vector<uint64_t> chunk_g0;   // chunk -> first group
+    uint64_t g = 0;
+    for (int i = 0; i < n_pieces; ++i) {  // the group holding a boundary goes with the earlier piece
+      const uint64_t g1 = i + 1 < n_pieces
+                              ? std::max(g, std::min(n_groups, (hoff[pbeg[i + 1]] + 63) / 64))
+                              : n_groups;
+      do {
+        const uint64_t want = std::min(kSegGroups, kFirstSegGroups << std::min<size_t>(segs.size(), 2));
+        const uint64_t e = std::min(g1, g + want);
+        uint32_t nch = 0;
+        for (uint64_t ch = g; ch < e; ch += kChunkGroups, ++nch) {
+          chunk_seg.push_back((uint32_t)segs.size());
+          chunk_g0.push_back(ch);
+        }
+        segs.push_back({g, e, i, e == g1, nch});
+        g = e;
+      } while (g < g1);
+    }
+    std::unique_ptr<std::atomic<uint32_t>[]> left(new std::atomic<uint32_t>[segs.size()]);
+    for (size_t k = 0; k < segs.size(); ++k) left[k].store(segs[k].chunks, std::memory_order_relaxed);
+    int rc_copy = KMA_OK;
+    staging_pool().run_with(
+        chunk_seg.size(), staging_threads(),
+        [&](uint64_t ci) {
+          const Seg& sg = segs[chunk_seg[ci]];
+          const uint64_t g0 = chunk_g0[ci], g1 = std::min(sg.g1, g0 + kChunkGroups);
+          const uint64_t r0 = 64 * g0, r1 = std::min(64 * g1, nres);
+          const uint64_t bytes = 40 * (g1 - g0) + (g1 == n_groups ? tail : 0);
+          kma::pack_residues_host(t->lut, residues + base + r0, r1 > r0 ? r1 - r0 : 0,
+                                  hin + 40 * g0, bytes);
+          left[chunk_seg[ci]].fetch_sub(1, std::memory_order_release);
+        },
+        [&](auto& help) {
+          for (size_t k = 0; k < segs.size() && rc_copy == KMA_OK; ++k) {
+            const Clock::time_point t_w = Clock::now();
+            while (left[k].load(std::memory_order_acquire) != 0)
+              if (!help()) std::this_thread::yield();
+            const Clock::time_point t_issue = Clock::now();
+            t_stage += std::chrono::duration<double, std::milli>(t_issue - t_w).count();
+            const Seg& sg = segs[k];
+            hipStream_t cs = c->copy[sg.piece & 1];
+            const uint64_t bytes = 40 * (sg.g1 - sg.g0) + (sg.g1 == n_groups ? tail : 0);
+            if (sg.g1 == n_groups && sg.chunks == 0) std::memset(hin + 40 * n_groups, 0, tail);
+            if (bytes) {
+              const hipError_t e = hipMemcpyAsync(c->d_in.p + 40 * sg.g0, hin + 40 * sg.g0, bytes,
+                                                  hipMemcpyHostToDevice, cs);
+              if (e != hipSuccess) rc_copy = fail(KMA_E_DEVICE, "hipMemcpyAsync: %s", hipGetErrorString(e));
+            }
+            if (rc_copy == KMA_OK && sg.last) rc_copy = launch_piece(sg.piece, cs);
+            t_launch += ms_since(t_issue);
+          }
+          while (help()) {}  // (after an error: the job still completes)
+        });
+    if (rc_copy) return rc_copy;
+  } else {
+    uint64_t ga = 0;  // packed: first stream group the piece stages
+    for (int i = 0; i < n_pieces; ++i) {
+      hipStream_t cs = c->copy[i & 1];
+      const Clock::time_point t_piece = Clock::now();
+      const uint64_t ra = hoff[pbeg[i]], rb = i + 1 < n_pieces ? hoff[pbeg[i + 1]] : nres;
+      if (packed) {  // the group holding the piece boundary goes with the earlier piece
+        const uint64_t gb = i + 1 < n_pieces ? std::min(n_groups, (rb + 63) / 64) : n_groups;
+        KMA_HIP(stage_pack_h2d(c->d_in.p, hin, t->lut, residues + base, nres, ga, gb,
+                               i + 1 == n_pieces ? in_bytes - 40 * n_groups : 0, cs));
+        ga = gb;
+      } else {
+        KMA_HIP(stage_h2d(c->d_in.p + ra, hin + ra, residues + base + ra, rb - ra, r.device, cs));
+        if (i + 1 == n_pieces) {
+          std::memset(hin + nres, 0, in_bytes - nres);
+          KMA_HIP(hipMemcpyAsync(c->d_in.p + nres, hin + nres, in_bytes - nres,
+                                 hipMemcpyHostToDevice, cs));
+        }
+      }
+      const Clock::time_point t_staged = Clock::now();
+      t_stage += std::chrono::duration<double, std::milli>(t_staged - t_piece).count();
+      if (int rc = launch_piece(i, cs)) return rc;
+      t_launch += ms_since(t_staged);
+    }
+  }
   // Pieces' outputs into the caller's arrays as they arrive (the later pieces still copy and
   // run meanwhile).
   double t_wait = 0;

@@ -6,7 +6,7 @@
 #   stats    rocprofv3 --kernel-trace --stats of the c5 and c3 bench commands
 #   bench    the bench lines: c5 (headline, with the CPU baseline), c2, c3, c4
 #   sq       SQ counters of c5 and c3 (VALU / LDS / wait split)
-# Usage: SECTIONS="traffic stats bench sq" TRAFFIC=profiles/r04_traffic.json \
+# Usage: SECTIONS="traffic stats bench sq" TRAFFIC=profiles/r05_traffic.json \
 #          bash scripts/gpu_measure.sh <out-subdir>
 # Stops at the first step that does not exit 0.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2

@@ -1,15 +1,17 @@
 #!/bin/bash
 # End-of-round pass on one box: GPU tests + smoke, then the measurement pass of the shipped build
 # (PMC traffic -> profiles/<round>_traffic.json copy under gpurun_out, kernel stats, bench lines,
-# SQ counters) and the genome-directory line. The traffic summary is written to $TRAFFIC on the
+# SQ counters), the genome-directory line and the FASTA line. The traffic summary is written to $TRAFFIC on the
 # box before the bench lines run, so they carry it (copy it back from gpurun_out/<out>/traffic.json).
 # Usage: TRAFFIC=profiles/r05_traffic.json [SKIP_TESTS=1] bash scripts/gpu_round_end.sh <out-subdir>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 OUT=${1:-round_end}
 [ -n "$SKIP_TESTS" ] || bash scripts/gpu_tests.sh $OUT || exit $?
-SECTIONS="traffic stats bench sq" TRAFFIC=${TRAFFIC:-profiles/r04_traffic.json} bash scripts/gpu_measure.sh $OUT || exit $?
-cp ${TRAFFIC:-profiles/r04_traffic.json} gpurun_out/$OUT/traffic.json
+SECTIONS="traffic stats bench sq" TRAFFIC=${TRAFFIC:-profiles/r05_traffic.json} bash scripts/gpu_measure.sh $OUT || exit $?
+cp ${TRAFFIC:-profiles/r05_traffic.json} gpurun_out/$OUT/traffic.json
 timeout -k 10 600 python bench.py --workload genomes > gpurun_out/$OUT/bench_genomes.log 2> gpurun_out/$OUT/bench_genomes.err
 echo "genomes rc=$?" >> gpurun_out/$OUT/steps.log
+timeout -k 10 600 python bench.py --workload fasta > gpurun_out/$OUT/bench_fasta.log 2> gpurun_out/$OUT/bench_fasta.err
+echo "fasta rc=$?" >> gpurun_out/$OUT/steps.log
 cat gpurun_out/$OUT/steps.log

@@ -183,6 +183,27 @@ def test_pack_residues_staging_pool_concurrent(native_lib):
     assert np.array_equal(want[0][:len(head)], head)
 
 
+@pytest.mark.parametrize("shift", [0, 8, 20, 40])
+@pytest.mark.parametrize("n", [511, 512, 4096, 4096 + 520, 100_003])
+def test_pack_residues_output_alignment(native_lib, n, shift):
+    """kma_pack_residues writes 64-byte aligned outputs in 512-residue blocks by non-temporal
+    stores (then the overlapping-store AVX2 steps and the scalar tail) and other outputs by the
+    overlapping stores alone: the same stream, no byte written past out_cap."""
+    import kmeranno
+    rng = np.random.default_rng(n + shift)
+    pool = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWYXZ*az-\xff", np.uint8)
+    res = pool[rng.integers(0, len(pool), n)]
+    need = kmeranno.packed_bytes(n)
+    raw = np.full(need + 256, 0xEE, np.uint8)
+    base = (-raw.ctypes.data) % 64 + shift  # 64-byte aligned + shift
+    out = raw[base:base + need]
+    rc = kmeranno.load().kma_pack_residues(None, res, n, out, need)
+    assert rc == 0
+    want = _pack_reference(res)
+    assert (out[:len(want)] == want).all() and not out[len(want):].any()
+    assert (raw[:base] == 0xEE).all() and (raw[base + need:] == 0xEE).all()
+
+
 @pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 63, 64, 65, 200, 4096 + 37, 100_003])
 def test_pack_residues_host_matches_bitwise_reference(native_lib, n):
     """kma_pack_residues (AVX2 body + scalar tail, chosen by the CPU) against a bitwise numpy
