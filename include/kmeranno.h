@@ -300,9 +300,11 @@ int kma_workspace_phases_read(kma_workspace* ws, uint32_t* n_calls, int* n_phase
  * min_hits >= 1 (ApplyKmerProcessor.java:91-92). out_tally (optional, length n_fid) receives
  * += 1 per CALLED protein at its fid (the APPLY report's role counts before column mapping).
  * Host form: synchronous, host buffers. A batch of >= 32 MiB of residues is cut into pieces of
- * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16) whose staging (packing, under
- * KMA_OPT_PACKED_INPUT, on KMA_OPT_HOST_THREADS threads) and H2D run on the context's copy
- * stream under the previous piece's kernel. A replica's share of more than 2^31 residues
+ * whole proteins (up to 8; KMA_OPT_HOST_PIECES overrides, 1..16), one kernel each. Packed input
+ * (KMA_OPT_PACKED_INPUT, the default) is packed on KMA_OPT_HOST_THREADS threads in stream order
+ * and copied in segments as soon as each is packed, on the context's two copy streams; a
+ * piece's kernel follows its last segment (ASCII input: each piece staged, then copied, under
+ * the previous piece's kernel). A replica's share of more than 2^31 residues
  * (KMA_OPT_HOST_SLICE) is annotated as consecutive slices of whole proteins, one device call
  * each; only a single protein longer than 2^32 - 128 residues is refused (KMA_E_INVALID).     */
 int kma_annotate_proteins(const kma_table* table, const uint8_t* residues,

@@ -462,6 +462,7 @@ struct HostCtx {
   hipStream_t copy[2] = {};
   hipStream_t d2h = nullptr;  // pieces' outputs back while later pieces copy and run
   hipEvent_t piece_ready[kMaxPieces] = {};
+  hipEvent_t piece_ready2[kMaxPieces] = {};  // streamed copies: piece i's data on copy[1]
   hipEvent_t piece_done[kMaxPieces] = {};  // piece i's kernel (on `stream`)
   hipEvent_t out_ready[kMaxPieces] = {};   // piece i's outputs in pinned memory (on d2h)
   kma_workspace* ws = nullptr;
@@ -501,7 +502,7 @@ void destroy_ctx(HostCtx* c) {
   for (hipStream_t cs : c->copy)
     if (cs) (void)hipStreamDestroy(cs);
   if (c->d2h) (void)hipStreamDestroy(c->d2h);
-  for (hipEvent_t* ev : {c->piece_ready, c->piece_done, c->out_ready})
+  for (hipEvent_t* ev : {c->piece_ready, c->piece_ready2, c->piece_done, c->out_ready})
     for (int i = 0; i < kMaxPieces; ++i)
       if (ev[i]) (void)hipEventDestroy(ev[i]);
   c->d_in.release();
@@ -533,7 +534,7 @@ int acquire_ctx(kma_table* t, int device, HostCtx** out) {
   for (hipStream_t& cs : c->copy)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking);
-  for (hipEvent_t* ev : {c->piece_ready, c->piece_done, c->out_ready})
+  for (hipEvent_t* ev : {c->piece_ready, c->piece_ready2, c->piece_done, c->out_ready})
     for (int i = 0; i < kMaxPieces && e == hipSuccess; ++i)
       e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -1417,7 +1418,8 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   // i % 2 (the offsets with piece 0); the kernel of piece i waits for piece i's event on the
   // compute stream, so the staging and transfer of piece i + 1 run under the kernel of piece i,
   // and two pieces' copies may run at once on two DMA engines (pieces of >= kPieceBytes residues,
-  // at most KMA_HOST_PIECES (default 12 streamed / 8 piece-wise, <= kMaxPieces; read per call);
+  // at most KMA_HOST_PIECES (default 8, <= kMaxPieces; read per call: streamed c5 calls took
+  // 5.6-5.7 / 6.0 / 6.1 ms at 8 / 12 / 16 pieces, profiles/r05/e2e_streamed_alt_r05j);
   // a small call is one piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (round 2,
   // profiles/r02r_host_pipeline/).
   constexpr uint64_t kPieceBytes = 16ull << 20;
@@ -1425,7 +1427,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   // packed input: the stream is copied in segments as it is packed (kStreamedCopies)
   const bool streamed = packed && kStreamedCopies;
   const uint64_t max_pieces =
-      po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : streamed ? 12 : 8;
+      po > 0 ? std::min<uint64_t>((uint64_t)po, kMaxPieces) : 8;
   uint8_t* hin = c->h_in.p;
   hipStream_t s = c->stream;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hin + in_bytes);
@@ -1479,12 +1481,16 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
     pbeg[i] = (uint32_t)(std::lower_bound(hoff + pbeg[i - 1], hoff + n, target) - hoff);
   }
   pbeg[n_pieces] = n;
-  // Piece i's kernel (after its input is on the device: piece_ready[i] on copy stream cs) and
-  // the copy of its outputs.
-  auto launch_piece = [&](int i, hipStream_t cs) -> int {
+  // Piece i's kernel (after its input is on the device: piece_ready[i] on copy stream cs, and
+  // with both_copies, piece_ready2[i] on copy[1] as well) and the copy of its outputs.
+  auto launch_piece = [&](int i, hipStream_t cs, bool both_copies = false) -> int {
     const uint32_t a = pbeg[i], b = pbeg[i + 1];
     KMA_HIP(hipEventRecord(c->piece_ready[i], cs));
     KMA_HIP(hipStreamWaitEvent(s, c->piece_ready[i], 0));
+    if (both_copies) {
+      KMA_HIP(hipEventRecord(c->piece_ready2[i], c->copy[1]));
+      KMA_HIP(hipStreamWaitEvent(s, c->piece_ready2[i], 0));
+    }
     if (b > a)
       if (int rc = annotate_proteins_on(t, r, c->ws, c->d_in.p, c->d_off.p + a, b - a,
                                         hoff[b] - hoff[a], min_hits, flags, d_fid + a,
@@ -1499,7 +1505,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
     // kSegGroups groups, never across a piece boundary) as soon as a segment's chunks are all
     // packed, packing chunks itself while it waits; a piece's kernel follows its last segment.
     // Round 4 packed a whole piece before its one copy: the link idled while each piece was
-    // packed (0.24 and 0.30 ms gaps while the pieces ramped up, profiles/r05/e2e_trace_r05d.txt).
+    // packed (0.24 and 0.30 ms gaps while the pieces ramped up, profiles/r05/e2e_piecewise_r05d/events.jsonl).
     // Segments of >= 2.6 MB keep the copies near the one-copy rate (2 MiB copies: 42 vs 51 GB/s).
     constexpr uint64_t kChunkGroups = 1u << 12, kSegGroups = 1u << 18, kFirstSegGroups = 1u << 16;
     const uint64_t tail = in_bytes - 40 * n_groups;  // the kernel's read padding, zeroed
@@ -1551,7 +1557,14 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
             const Clock::time_point t_issue = Clock::now();
             t_stage += std::chrono::duration<double, std::milli>(t_issue - t_w).count();
             const Seg& sg = segs[k];
-            hipStream_t cs = c->copy[sg.piece & 1];
+            // Segments alternate over the two copy streams (two DMA engines: 52 vs 44 GB/s on
+            // one stream, profiles/r05/e2e_streamed_fifo_r05i), in stream order on each, and a
+            // piece's kernel waits for both: a piece's data lands as early as the link allows.
+            // (Round 5's first build put whole pieces on alternate streams: consecutive pieces
+            // shared the link and every other kernel waited ~0.09 ms for its data,
+            // profiles/r05/e2e_streamed_r05h.)
+            hipStream_t cs = c->copy[0];
+            if (k & 1) cs = c->copy[1];
             const uint64_t bytes = 40 * (sg.g1 - sg.g0) + (sg.g1 == n_groups ? tail : 0);
             if (sg.g1 == n_groups && sg.chunks == 0) std::memset(hin + 40 * n_groups, 0, tail);
             if (bytes) {
@@ -1559,7 +1572,7 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
                                                   hipMemcpyHostToDevice, cs);
               if (e != hipSuccess) rc_copy = fail(KMA_E_DEVICE, "hipMemcpyAsync: %s", hipGetErrorString(e));
             }
-            if (rc_copy == KMA_OK && sg.last) rc_copy = launch_piece(sg.piece, cs);
+            if (rc_copy == KMA_OK && sg.last) rc_copy = launch_piece(sg.piece, c->copy[0], true);
             t_launch += ms_since(t_issue);
           }
           while (help()) {}  // (after an error: the job still completes)
