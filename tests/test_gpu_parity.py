@@ -433,6 +433,49 @@ def test_contigs_small_gto_vs_oracle(kma, oracle_c, small_gto, layout, gcode, ex
     assert len(hits) > 100_000
 
 
+@pytest.mark.parametrize("fill", [1.0, 0.98])
+def test_two_choice_build_full_table_reports_or_places_every_key(kma, oracle_c, fill):
+    """The two-choice build at (nearly) every slot used, where an insertion can run out of
+    evictions: it either reports failure (status[0], the creators' cue to build chained) or
+    has placed every row's key (entries = distinct keys, at most one probe beyond home, and
+    every protein's vote equals the oracle's); at 98% the chained build of the same rows (the
+    fallback) succeeds and votes the same. (At 100% a chained table has no empty slot to stop
+    a miss's walk: not a table the creators build.)"""
+    torch = pytest.importorskip("torch")
+    from kmeranno import synth
+    wl = synth.make_workload(1500, 60_000, 500, seed=41)
+    dev = torch.device("cuda", 0)
+    n_keys = len(np.unique(wl.keys))
+    nb = int(np.ceil(n_keys / fill / kma.bucket_slots()))
+    keys = torch.from_numpy(wl.keys.view(np.int64)).to(dev)
+    fids = torch.from_numpy(wl.fids.view(np.int32)).to(dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+    efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
+    m = kma.layout_for(K, nb) & 0xFF
+    results = {}
+    builds = [("two", m | kma.LAYOUT_TWO_CHOICE)] + ([("chained", m)] if fill < 1 else [])
+    for name, code in builds:
+        slots = torch.empty(nb * kma.bucket_slots(), dtype=torch.int64, device=dev)
+        winner = torch.empty(nb * kma.bucket_slots(), dtype=torch.int32, device=dev)
+        status = torch.zeros(4, dtype=torch.int32, device=dev)
+        kma.build_device(slots.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(),
+                         fids.data_ptr(), len(wl.keys), status.data_ptr(), stream, layout=code)
+        torch.cuda.synchronize()
+        st = status.cpu().numpy()
+        results[name] = st.tolist()
+        if name == "two" and st[0] != 0:
+            continue  # reported: a creator would build chained
+        assert st[0] == 0 and st[1] == n_keys
+        if name == "two":
+            assert st[2] in (1, 2)
+        with kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0, code) as t:
+            fid, cnt, stt, _ = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0)
+        assert (stt == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+    print(f"fill {fill}: {nb} buckets, {n_keys} keys, status {results}")
+
+
 def test_device_api_with_torch_buffers(kma):
     """_device entry points on torch-allocated HBM (the bench path), same results as host."""
     torch = pytest.importorskip("torch")
