@@ -5,8 +5,9 @@
                   their functions): layout, displaced keys, longest chain; the protein path on
                   small.gto's pegs repeated to ~1M proteins (device entry point, hipEvent timed)
   adversarial     2.4M keys built to share 2,000 minimizers (every key holds one of the 2,000
-                  lowest-hash 6-mers): the creator's flat fallback vs the forced m=7 layout, each
-                  timed on 200k proteins assembled from the keys
+                  6-mers lowest in the shipped m-mer order, so it is the key's minimizer): the
+                  creators' choice (two-choice placement, rebuilt flat when crowded) vs the
+                  forced m=7 layout, each timed on 200k proteins assembled from the keys
   per_genome      kma_annotate_proteins (host entry point: pinned staging, H2D, kernel, D2H on the
                   table's pooled stream) on ONE genome (small.gto's 712 pegs) against the 10^7-row
                   c2 table: the drop-in's per-genome call latency (median of 50)
@@ -94,17 +95,12 @@ def main():
     rng = np.random.default_rng(23)
     aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
 
-    def mix32(h):
-        h = h ^ (h >> np.uint64(16))
-        h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
-        h = h ^ (h >> np.uint64(13))
-        h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
-        return h ^ (h >> np.uint64(16))
     cand = aa[rng.integers(0, 20, (2_000_000, 6))]
     packed = np.zeros(len(cand), np.uint64)
     for j in range(6):
         packed = (packed << np.uint64(5)) | (cand[:, j].astype(np.uint64) - np.uint64(64))
-    h = mix32((packed * np.uint64(0x9E3779B1) + np.uint64(0x7F4A7C15)) & np.uint64(0xFFFFFFFF))
+    # the shipped m-mer order (kma_internal.h mmer_hash, KMA_HASH_LITE): one 32-bit multiply
+    h = (packed * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
     cores = cand[np.argsort(h)[:2000]]
     codes = np.arange(1, 21, dtype=np.uint64)[rng.integers(0, 20, (2000, 3, 400, 2))]
     keyset = set()
