@@ -714,8 +714,9 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
   auto displaced = [](const uint32_t s[4]) { return (double)s[3] / std::max<uint32_t>(s[1], 1); };
   if (two_choice_first(k) && nb >= 2) {
     // Two-choice placement at the size rule's (or the forced) layout; a crowded minimizer table
-    // is also built flat and the flat one kept if it halves the displaced keys; a build that
-    // fails (an insertion exceeded kMaxKicks) falls through to the chained rule below.
+    // is also built flat and the flat one kept if it halves the displaced keys; a minimizer build
+    // that fails (an insertion exceeded kMaxKicks) is retried flat; a build that still fails
+    // falls through to the chained rule below.
     uint32_t s2[4] = {};
     auto build2 = [&](int m2, uint64_t** slots, uint32_t out[4]) -> int {
       KMA_HIP(hipMalloc(slots, nb * bucket_bytes(k)));
@@ -732,6 +733,15 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
     };
     uint64_t* d2 = nullptr;
     if (int rc = build2(m, &d2, s2)) return rc;
+    if (s2[0] && m != 0 && forced_layout() < 0) {
+      // A minimizer table whose insertions ran out of evictions (keys piling onto few
+      // minimizers: their homes full, so they all compete for alternates) is built flat with
+      // two-choice placement before falling back to chains: adversarial keys sharing 2,000
+      // minimizers at LF 0.9 got a flat chained table with chains of 30 buckets
+      // (profiles/r05/robustness_r05k.jsonl).
+      if (int rc = build2(0, &d2, s2)) return rc;
+      if (!s2[0]) m = 0;  // (else the chained rule below starts from the size rule's m)
+    }
     if (!s2[0]) {  // built
       d_slots = d2;
       std::memcpy(st, s2, sizeof st);

@@ -421,17 +421,21 @@ constexpr int kContigPos = KMA_CONTIG_POS;
 constexpr int kContigSeq = KMA_CONTIG_SEQ;
 static_assert(kContigSeq == 1 || kContigPos == 1, "sequential slices take one position per lane");
 constexpr int kContigTile = 256 * kContigPos * kContigSeq;  // forward positions per block
-// KMA_CONTIG_STREAM=1 (tuning builds): keys of the 6-frame probe from per-frame 5-bit codon
-// streams in LDS (one funnel shift and a borrow test per strand instead of K byte loads,
-// compares and shifts per strand: 64 fewer VALU and 12 fewer LDS instructions per position and
-// slice). Measured slower at c3 both ways it was built (round 5, ABAB on one box each): the
-// streams built by a second pass over the codes, probe 0.0789 vs 0.0745 ms
-// (profiles/r05/c3_stream_ab_r05e.log); the codes ORed into the streams by the translation pass
-// (LDS atomics, ~10 lanes per word), 0.0766 vs 0.0748 ms (c3_stream_ab_r05f.log). The VALU
-// saved is not on the probe's critical path; the per-block phases are.
-#ifndef KMA_CONTIG_STREAM
-#define KMA_CONTIG_STREAM 0
-#endif
+// Round 5 also built the probe's keys from per-frame 5-bit codon streams in LDS (one funnel
+// shift and a borrow test per strand instead of K byte loads, compares and shifts per strand:
+// 64 fewer VALU and 12 fewer LDS instructions per position and slice) and measured it slower
+// both ways it was built (ABAB on one box each): streams built by a second pass over the codes,
+// probe 0.0789 vs 0.0745 ms (profiles/r05/c3_stream_ab_r05e.log); codes ORed into the streams
+// by the translation pass (LDS atomics), 0.0766 vs 0.0748 ms (c3_stream_ab_r05f.log). The VALU
+// saved was not on the probe's critical path, the per-block phases were (the variant is in the
+// history of kma_kernels.hip).
+// A persistent 6-frame grid (one resident wave of blocks striding over the tiles, each block
+// loading its next tile's DNA under the current tile's probes) was also built in round 5 and
+// measured slower: probe 0.0796-0.0803 vs 0.0772-0.0773 ms for a block per tile, ABAB on one
+// box (profiles/r05/c3_persistent_ab_r05m.log). The round-4 block clocks had put the tile load
+// at 7.2 of a 20.6 us block, but that time is queueing behind the other blocks' bucket
+// gathers: a tile costs the same with its DNA prefetched, and the static assignment (2 or 3
+// tiles per block) lost the dispatcher's balancing of the last tiles.
 constexpr uint32_t kScanGroup = 256;  // probe blocks per emit-offset group sum
 // Up to this many groups (16 loads per lane, one round trip) an emit block sums the group sums
 // before its own; beyond, a one-block scan turns them into prefixes first.

@@ -911,17 +911,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
   constexpr int kQ = kWide ? 4 : kBucketQuads;                // dwordx4 per bucket
   constexpr int kH = kWide ? 1 : kBucketHalves;               // 64-byte pieces per bucket
   constexpr int kSpan = kContigTile + 3 * K;
-  [[maybe_unused]] constexpr uint64_t kKeyMask = (1ull << (5 * K)) - 1;
-  [[maybe_unused]] constexpr uint64_t kFieldLo = kKeyMask / 31u;  // bit 0 of every 5-bit field
-  [[maybe_unused]] constexpr uint64_t kFieldHi = kFieldLo << 4;    // bit 4 of every field
   __shared__ uint8_t bases[kSpan];
-#if KMA_CONTIG_STREAM
-  // codes per frame <= kSpan / 3 + 1; a key reads words w and w + 1 of its stream
-  constexpr int kStreamWords = ((kSpan / 3 + 1) * 5 + 63) / 64 + 1;
-  __shared__ uint64_t streams[6][kStreamWords];
-#else
   __shared__ uint8_t aa_p[kSpan], aa_m[kSpan];
-#endif
   __shared__ uint64_t offc[kOffCache + 1];
   __shared__ uint32_t crange[2];
   constexpr int CP = kContigPos * kContigSeq;  // slices of 256 positions per block
@@ -947,9 +938,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
     tb[j] = i < kSpan && g < end ? a.dna[g] : (uint8_t)'N';
   }
   if (wave == 3) codon[lane] = a.codon_codes[lane];  // LDS copy of the kernel-argument table
-#if KMA_CONTIG_STREAM
-  for (int i = t; i < 6 * kStreamWords; i += blockDim.x) (&streams[0][0])[i] = 0u;
-#endif
   if (a.n_contig < (uint32_t)kOffCache) {
     // Every offset fits the cache: wave 0 loads them once and finds the tile's first / last
     // contig by ballot (the largest c with offsets[c] <= g is a prefix count; offsets[0] = base).
@@ -985,40 +973,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
   __syncthreads();
   KMA_CLK(1);  // tile loaded, contigs found
   const uint32_t c_lo = crange[0], nc = crange[1] - c_lo + 1;  // contigs meeting the tile
-#if KMA_CONTIG_STREAM
-  // Codon streams: each frame's amino-acid codes as a 5-bit stream, '+' first code most
-  // significant (bits [5c, 5c + 5) of frame f's stream hold the code of position 3c + f, MSB
-  // first) and '-' least significant first, so that a window's key is one funnel shift of two
-  // LDS words and a stop or ambiguous codon one borrow test, where round 4 read K codes per
-  // strand and compared and shifted each. Translation ORs each code into its stream word(s)
-  // (zeroed with the tile load): the same one pass over the bases, no byte arrays.
-  for (int i = t; i < kSpan - 2; i += blockDim.x) {
-    const uint32_t b0 = bases[i], b1 = bases[i + 1], b2 = bases[i + 2];
-    if ((b0 | b1 | b2) & 4u) continue;  // 'X': code 0
-    const uint64_t cp = codon[b0 * 16 + b1 * 4 + b2];
-    const uint64_t cm = codon[(b2 ^ 2u) * 16 + (b1 ^ 2u) * 4 + (b0 ^ 2u)];  // complement: x ^ 2
-    const uint32_t c = ((uint32_t)i * 0xAAABu) >> 17, f = (uint32_t)i - 3u * c;  // i / 3, i % 3
-    const uint32_t bit = 5u * c, w = bit >> 6, o = bit & 63u;
-    uint64_t* sp = streams[f] + w;
-    uint64_t* sm = streams[3 + f] + w;
-    if (cp) {  // big-endian: the code's last bit at word bit 59 - o
-      if (o <= 59u) {
-        __hip_atomic_fetch_or(sp, cp << (59u - o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        __hip_atomic_fetch_or(sp, cp >> (o - 59u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(sp + 1, cp << (123u - o), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    if (cm) {  // little-endian: the code's first bit at word bit o
-      __hip_atomic_fetch_or(sm, cm << o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (o > 59u)
-        __hip_atomic_fetch_or(sm + 1, cm >> (64u - o), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  __syncthreads();
-#else
   for (int i = t; i < kSpan - 2; i += blockDim.x) {
     const uint32_t b0 = bases[i], b1 = bases[i + 1], b2 = bases[i + 2];
     if ((b0 | b1 | b2) & 4u) {
@@ -1029,7 +983,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
     }
   }
   __syncthreads();
-#endif
   KMA_CLK(2);  // translated
 
   // Each lane owns positions tp + 256 h (h < kContigPos): both windows of every one of them are
@@ -1078,19 +1031,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
     int64_t x = 0, len = 0;
     if (g < end) locate(tt, contig[h], x, len);
     bool pv = g < end && x + 3 * K + 3 <= len, mv = g < end && x >= 3 && x + 3 * K <= len;
-#if KMA_CONTIG_STREAM
-    {
-      const uint32_t ci = (tt * 0xAAABu) >> 17;  // tt / 3 (tt < 2^15)
-      const uint32_t f = tt - 3u * ci, b = 5u * ci, w = b >> 6, off = b & 63u;
-      const uint64_t p0 = streams[f][w], p1 = streams[f][w + 1];
-      const uint64_t m0 = streams[3 + f][w], m1 = streams[3 + f][w + 1];
-      key[h][0] = ((p0 << off) | ((p1 >> 1) >> (63u - off))) >> (64 - 5 * K);
-      key[h][1] = ((m0 >> off) | ((m1 << 1) << (63u - off))) & kKeyMask;
-      // a zero (stop or ambiguous) code: a borrow into that 5-bit field's top bit
-      pv = pv && ((key[h][0] - kFieldLo) & ~key[h][0] & kFieldHi) == 0u;
-      mv = mv && ((key[h][1] - kFieldLo) & ~key[h][1] & kFieldHi) == 0u;
-    }
-#else
     key[h][0] = key[h][1] = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -1100,7 +1040,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMA_CONTIG_
       key[h][0] = (key[h][0] << 5) | cp;
       key[h][1] |= (uint64_t)cm << (5 * j);
     }
-#endif
     // invalid windows gather bucket 0 (one shared line; their verdicts are dropped)
     ok[h][0] = pv;
     ok[h][1] = mv;

@@ -428,7 +428,8 @@ def choose_layout(k: int, n_buckets: int, build):
     build(code) builds the table with that layout code (minimizer length | LAYOUT_TWO_CHOICE)
     into the caller's buffer and returns its status {failed, entries, longest chain,
     displaced}. Returns (code, status); the kept layout is the one built last. Two-choice
-    placement first (narrow tables); a failed two-choice build falls back to the chained rule.
+    placement first (narrow tables; a failed minimizer build is retried flat); a failed
+    two-choice build falls back to the chained rule.
     A forced layout (OPT_LAYOUT) is the size rule's answer."""
     def disp(s):
         return s[3] / max(s[1], 1)
@@ -437,6 +438,10 @@ def choose_layout(k: int, n_buckets: int, build):
     m = code & 0xFF
     if code & LAYOUT_TWO_CHOICE:
         st = build(code)
+        if st[0] != 0 and m != 0 and not forced:  # out of evictions: retried flat
+            s2 = build(LAYOUT_TWO_CHOICE)
+            if s2[0] == 0:
+                return LAYOUT_TWO_CHOICE, s2
         if st[0] == 0:
             if not forced and m != 0 and disp(st) > MAX_DISPLACED_TWO_CHOICE:
                 s2 = build(LAYOUT_TWO_CHOICE)

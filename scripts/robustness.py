@@ -38,7 +38,8 @@ def info(t):
     i = t.info
     return {"entries": int(i.n_entries), "buckets": int(i.n_buckets), "layout_m": int(i.minimizer_len),
             "displaced": int(i.n_displaced), "displaced_frac": i.n_displaced / max(i.n_entries, 1),
-            "longest_chain": int(i.max_probe), "table_MiB": i.bytes / 2**20}
+            "longest_chain": int(i.max_probe), "two_choice": int(i.two_choice),
+            "table_MiB": i.bytes / 2**20}
 
 
 def time_device(t, res, off, reps=20):
@@ -130,12 +131,12 @@ def main():
         byt[:, :, j] = letters[((pick >> np.uint64(5 * (7 - j))) & np.uint64(31)).astype(np.int64)]
     ares = np.concatenate([byt.reshape(-1), np.zeros(64, np.uint8)])
     aoff = (np.arange(200_001, dtype=np.uint64) * 240)
-    for forced in (None, 7):
+    for lf, forced in ((0.5, None), (0.9, None), (0.5, 6), (0.5, 7)):
         with kmeranno.options(**({"layout": forced} if forced else {})):
-            t = kmeranno.SignatureTable.from_packed(akeys, afids, K)
+            t = kmeranno.SignatureTable.from_packed(akeys, afids, K, load_factor=lf)
         with t:
-            out({"case": "adversarial", "forced_layout": forced, "keys": len(akeys), **info(t),
-                 **time_device(t, ares, aoff)})
+            out({"case": "adversarial", "load_factor": lf, "forced_layout": forced,
+                 "keys": len(akeys), **info(t), **time_device(t, ares, aoff)})
     # 3. per-genome host-entry latency against the c2 table
     n_seq, t_size, n_fid, seed = synth.CONFIGS["c2"]
     sig = synth.make_table(t_size, n_fid, seed, K)

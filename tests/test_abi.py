@@ -103,8 +103,8 @@ def test_table_layout_host_helper(native_lib, monkeypatch):
 def test_choose_layout_rule():
     """kmeranno.choose_layout mirrors the creators' rule (kma_abi.cpp create_from_device_keys).
     Two-choice placement first: kept when it builds (the size rule's m), rebuilt flat when more
-    than 40% of the keys are outside their home and flat halves them. A failed two-choice build
-    falls back to the chained rule, shown on the round-3 c5 sweep's build statistics {full,
+    than 40% of the keys are outside their home and flat halves them; a minimizer build that fails
+    is retried flat. A failed two-choice build falls back to the chained rule, shown on the round-3 c5 sweep's build statistics {full,
     entries, longest chain, displaced}: m = 6 kept at load factor 0.5, rebuilt m = 7 at 0.75 and
     0.9 (flat halves neither), flat for keys piling onto few minimizers; the kept layout is built
     last."""
@@ -139,6 +139,15 @@ def test_choose_layout_rule():
             return two[m]
         m, s = kmeranno.choose_layout(8, 25_000_000, build2)
         assert m == expect and built[-1] == m and s == two[m], (disp6, built)
+    # the minimizer two-choice build runs out of evictions (keys piling onto few minimizers):
+    # retried flat with two-choice placement, kept when that builds, chains only after both fail
+    built = []
+
+    def build3(m):
+        built.append(m)
+        return [1, 0, 0, 0] if m == 6 | tc else [0, n, 2, int(0.12 * n)]
+    m, s = kmeranno.choose_layout(8, 25_000_000, build3)
+    assert m == tc and built == [6 | tc, tc] and s[0] == 0
 
 
 def _pack_reference(res: np.ndarray) -> np.ndarray:
