@@ -147,6 +147,11 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
   return mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
 #endif
 }
+// Measured and not kept (round 5, profiles/r05/syncmer_ab_r05s/): a closed-syncmer order (an
+// m-mer whose smallest 3-mer hash sits at its first or last position ranks before all others),
+// density 0.452 vs 0.500 for random order at K = 8, m = 6 (simulated), parity green. The ~30
+// extra VALU per window cost more than the saved home requests except at c5: c5 kernel
+// 3.088 -> 3.03 ms, c3 0.0815 -> 0.0888 ms, c2 0.0464 -> 0.0487 ms (ABAB, one box).
 __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
   const uint32_t mask = (uint32_t)((1ull << (5 * m)) - 1);
   uint32_t best = 0xFFFFFFFFu;

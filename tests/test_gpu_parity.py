@@ -356,15 +356,20 @@ def test_config2_size_vs_oracle(kma, oracle_c, path, monkeypatch):
 
 
 @pytest.mark.timeout(300)
-def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c):
-    """A host call of ~48M residues runs as 2-3 pieces whose H2D overlaps the previous
-    piece's kernel (kma_abi.cpp protein_shard): every protein, including those next to piece
-    boundaries, and the tally (summed over the pieces' launches) equal the oracle's."""
+@pytest.mark.parametrize("opts", [{}, {"host_pieces": 16, "host_threads": 1},
+                                  {"host_pieces": 3, "host_threads": 3}, {"packed_input": 0}],
+                         ids=["default", "16pieces-1thread", "3pieces-3threads", "ascii"])
+def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c, opts):
+    """A host call of ~48M residues runs as 2-16 pieces whose H2D overlaps the previous
+    piece's kernel (kma_abi.cpp protein_shard): packed input streamed out in segments as the
+    staging pool packs it (the calling thread alone with one staging thread), ASCII input piece
+    by piece: every protein, including those next to piece and segment boundaries, and the
+    tally (summed over the pieces' launches) equal the oracle's."""
     from kmeranno import synth
     sig = synth.make_table(1_000_000, 2000, 41, K)
     res, off, _, _ = synth.make_queries(sig, 160_000, 41 * 1_000_003 + 17)
     assert off[-1] >= 2 * (16 << 20)  # at least two pieces
-    with _config_table(kma, sig) as t:
+    with _config_table(kma, sig) as t, kma.options(**opts):
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=2000)
     ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, res)
     efid, ecnt, est = oracle_c.apply_mt(ot, res, off, K, 5, 0, threads=8)
