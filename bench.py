@@ -799,6 +799,9 @@ def main():
     ap.add_argument("--placement", default="auto", choices=("auto", "chained"),
                     help="KMA_OPT_PLACEMENT: auto (default) = two-choice placement for K <= 8 "
                          "tables, chains if that build fails; chained = overflow chains (A/B runs)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a library option through the ABI before the run (tuning runs "
+                         "only; names as kmeranno._OPT_NAMES, e.g. block_proteins=6)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, check the multi-rank outputs, tally and table against "
                          "single-rank calls on rank 0 (exit 1 on a mismatch)")
@@ -806,6 +809,9 @@ def main():
 
     kmeranno.set_option(kmeranno.OPT_PACKED_INPUT, args.packed_input)
     kmeranno.set_option(kmeranno.OPT_PLACEMENT, 0 if args.placement == "chained" else -1)
+    for o in args.option:
+        name, _, value = o.partition("=")
+        kmeranno.set_option(kmeranno._OPT_NAMES[name], int(value))
     if args.workload == "genomes":  # a command-level run: `kma apply` as a child process
         bench_genomes(args)
         return
@@ -905,6 +911,7 @@ def main():
                        "load_factor": args.load_factor, "min_hits": MIN_HITS,
                        "table_layout_m": table.info.minimizer_len,
                        "table_placement": "two-choice" if table.info.two_choice else "chained",
+                       **({"options": args.option} if args.option else {}),
                        "parallelism": (f"input-shard x{world} of one batch" if strong else
                                        f"input-shard x{world}") + collective_note(args, world)},
             "seqs_per_s": seqs * args.steps / elapsed,

@@ -1229,7 +1229,12 @@ const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 // Round 3 (interleaved A/B, profiles/r03_session2/r03bp_steps.log): c5 (10^8 rows, 1.5 GiB
 // table in HBM) 3.59-3.63 / 3.69-3.71 / 3.80-3.81 ms at 6 / 7 / 8; c4 (10^7 rows, a 153 MiB
 // table inside the 256 MiB Infinity Cache) 2.752 vs 2.819 ms at 4 vs 6: 6 only for tables
-// larger than the Infinity Cache.
+// larger than the Infinity Cache. Round 5, c2 (profiles/r05/c2_opts_r05t/, two runs each):
+// 46.6 us at 4 proteins (two-pass grid), 52.4 / 50.0 / 48.0 / 53.9 / 56.6 us at 2 / 3 / 5 / 6 / 8,
+// 52.8 without the two-pass grid; and a tapered tail (the batch's last groups of half size, then
+// single proteins, so the last blocks to start end sooner; profiles/r05/c2_taper_r05u/) 47.0 /
+// 49.3 / 54.0 / 55.1 us for tails of 1/4, 1/2, 1 and 2 resident waves: each group's fixed chain
+// (offsets, first residues, final walks, vote) costs more than the shorter tail saves.
 constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes) {
   const int64_t f = ws->opt_block_proteins != kOptUnset ? ws->opt_block_proteins
