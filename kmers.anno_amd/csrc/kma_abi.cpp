@@ -198,6 +198,26 @@ void rebase_offsets(uint64_t* dst, const uint64_t* src, uint64_t n, uint64_t bas
                      });
 }
 
+// The first s < n with offsets[s + 1] < offsets[s], or n: chunks on the staging pool, each a
+// branch-free (vectorized) pass (c5's 1M offsets: a serial scan with an early exit per element
+// ran ~0.5 ms before the call's first copy).
+uint32_t offsets_decrease_at(const uint64_t* offsets, uint32_t n) {
+  constexpr uint64_t kChunk = 1u << 16;
+  const uint64_t n_chunks = (n + kChunk - 1) / kChunk;
+  std::vector<uint8_t> bad(n_chunks);
+  staging_pool().run(n_chunks, n >= 4 * kChunk ? staging_threads() : 1, [&](uint64_t c) {
+    const uint64_t e = std::min<uint64_t>(n, (c + 1) * kChunk);
+    uint64_t b = 0;
+    for (uint64_t i = c * kChunk; i < e; ++i) b |= offsets[i + 1] < offsets[i];
+    bad[c] = b != 0;
+  });
+  for (uint64_t c = 0; c < n_chunks; ++c)
+    if (bad[c])
+      for (uint64_t i = c * kChunk; i < n; ++i)
+        if (offsets[i + 1] < offsets[i]) return (uint32_t)i;
+  return n;
+}
+
 // memcpy on the staging pool in 1 MiB chunks (the outputs of a large host call).
 void pool_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kChunk = 1u << 20;
@@ -1462,6 +1482,10 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   // a piece, only the kernels do, and those keep up with the link (0.155 vs 0.18 ms per 1/22 of
   // c5), so equal pieces: the tail is one small piece's kernel (a ramp down's halving pieces
   // left kernels queued behind the last copy: 0.78 ms, profiles/r05/e2e_streamed_ramp_r05f).
+  // (Also measured on streamed calls: the last four pieces shrinking geometrically, weights 0.6,
+  // 0.36, 0.22, 0.13 of the others, cut the kernel after the last copy from ~0.6 to ~0.3 ms but
+  // the calls were no faster on two boxes: 5.8-6.7 vs 5.6-7.3 ms and 6.1-6.3 vs 5.6-6.7 ms,
+  // profiles/r05/e2e_taper_r05w, r05y.)
   uint64_t wsum = 0, wcum[kMaxPieces + 1] = {0};
   for (int i = 0; i < n_pieces; ++i) {
     const int edge = std::min(i, n_pieces - 1 - i);
@@ -1885,8 +1909,8 @@ int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const ui
   if (n_seq == 0) return KMA_OK;
   if (!residues || !offsets || !out_fid || !out_count || !out_status)
     return fail(KMA_E_INVALID, "null argument");
-  for (uint32_t s = 0; s < n_seq; ++s)
-    if (offsets[s + 1] < offsets[s]) return fail(KMA_E_INVALID, "offsets decrease at %u", s);
+  if (const uint32_t s = offsets_decrease_at(offsets, n_seq); s < n_seq)
+    return fail(KMA_E_INVALID, "offsets decrease at %u", s);
   const bool tally = out_tally && n_fid;
   const std::vector<Replica> reps = replicas(t);
   const int nr = (int)std::min<uint64_t>(reps.size(), n_seq);

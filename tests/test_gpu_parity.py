@@ -123,6 +123,23 @@ def test_min_hits_must_be_positive(kma):
     assert e.value.code == kma.E_INVALID  # ApplyKmerProcessor.java:91-92
 
 
+@pytest.mark.parametrize("at", [0, 65_535, 65_536, 199_998])
+def test_host_call_rejects_decreasing_offsets(kma, at):
+    """The host entry checks the offsets in chunks on the staging pool: a decrease anywhere (in
+    the first chunk, at a chunk's last or first offset, at the end) fails with its index, before
+    anything is staged; the untouched offsets still run."""
+    t = kma.SignatureTable.from_rows(["ACDEFGHI"], [0], K)
+    res, off = kma.pack_strings(["ACDEFGHIK"] * 199_999)
+    good = kma.annotate_proteins(t, res, off, 1)
+    assert (good[2] == 1).all()
+    bad = off.copy()
+    bad[at] = bad[at + 1] + 1
+    with pytest.raises(kma.KmerAnnoError) as e:
+        kma.annotate_proteins(t, res, bad, 1)
+    assert e.value.code == kma.E_INVALID and f"offsets decrease at {at}" in str(e.value)
+    t.close()
+
+
 @pytest.mark.parametrize("flags", [0, 1, 2])
 def test_config1_golden(kma, layout, flags, path, input_mode):
     z = np.load(os.path.join(GOLDEN, "apply_c1.npz"))
