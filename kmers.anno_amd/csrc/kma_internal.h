@@ -419,7 +419,9 @@ constexpr int kContigPos = KMA_CONTIG_POS;
 // those of one slice (kContigPos = 2 holds two slices' loads at once: 97 VGPRs, 4 waves/SIMD,
 // measured slower).
 // Round 4: 2 slices (c3 0.124 -> 0.099 ms, profiles/r04/c3_seq_r04c.log), then 4 (0.0916 ->
-// 0.087 ms against 3 slices' 0.088, ABAB, profiles/r04/c3_seq_ab_r04final.log).
+// 0.087 ms against 3 slices' 0.088, ABAB, profiles/r04/c3_seq_ab_r04final.log). Round 5: 5 / 6 /
+// 8 slices 0.0824 / 0.0829 / 0.0868 vs 0.0813 ms (probe 74.4 us at 4; ABAB,
+// profiles/r05/c3_seq_ab_r05z/; parity green at 6 and 8).
 #ifndef KMA_CONTIG_SEQ
 #define KMA_CONTIG_SEQ 4
 #endif
