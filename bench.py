@@ -926,6 +926,7 @@ def main():
         if world == 1:
             if not args.no_extras:
                 ms = e2e_host(table, residues, offsets, n_fid)
+                prof = e2e_host.profile  # (the ASCII call below replaces it)
                 with kmeranno.options(packed_input=0):
                     ms_ascii = e2e_host(table, residues, offsets, n_fid)
                 out["e2e_host_call"] = {
@@ -934,7 +935,7 @@ def main():
                     "packed_input": kmeranno.get_option(kmeranno.OPT_PACKED_INPUT),
                     "staging_threads": kmeranno.get_option(kmeranno.OPT_HOST_THREADS) or
                     "min(16, cores)",
-                    "ms": ms, "library_profile_ms": getattr(e2e_host, "profile", None),
+                    "ms": ms, "library_profile_ms": prof,
                     "lookups_per_s": n_win / (ms * 1e-3),
                     "seqs_per_s": n_seq / (ms * 1e-3), "kernel_ratio": ms / ph["annotate_kernel"],
                     "ascii_staging_ms": ms_ascii,
