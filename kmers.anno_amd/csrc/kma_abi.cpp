@@ -680,9 +680,10 @@ int build_two_choice_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int
   KMA_HIP(hipMemsetAsync(d_status, 0, 4 * sizeof(uint32_t), s));
   if (n == 0) return KMA_OK;
   size_t temp_bytes = 0;
+  kma::TwoChoiceScratch x;
   KMA_HIP(kma::launch_build_two_choice(d_slots, (uint32_t)n_buckets, k, m, d_keys, d_fids, n,
-                                       nullptr, nullptr, nullptr, nullptr, &temp_bytes, d_status,
-                                       s));
+                                       nullptr, nullptr, nullptr, x, nullptr, &temp_bytes,
+                                       d_status, s));
   DevBufs tmp;
   uint64_t* skeys;
   uint32_t *rows, *srows;
@@ -691,8 +692,12 @@ int build_two_choice_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int
   KMA_HIP(tmp.alloc(&rows, n * 4));
   KMA_HIP(tmp.alloc(&srows, n * 4));
   KMA_HIP(tmp.alloc(&temp, temp_bytes));
+  KMA_HIP(tmp.alloc(&x.home, n * 4));  // home-first placement (kma_kernels.hip)
+  KMA_HIP(tmp.alloc(&x.sorted_home, n * 4));
+  KMA_HIP(tmp.alloc(&x.sorted_idx, n * 4));
+  KMA_HIP(tmp.alloc(&x.away, n));
   KMA_HIP(kma::launch_build_two_choice(d_slots, (uint32_t)n_buckets, k, m, d_keys, d_fids, n,
-                                       skeys, rows, srows, temp, &temp_bytes, d_status, s));
+                                       skeys, rows, srows, x, temp, &temp_bytes, d_status, s));
   KMA_HIP(hipStreamSynchronize(s));  // before DevBufs frees the sort buffers
   return KMA_OK;
 }

@@ -481,11 +481,19 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
 // == nullptr: size query into *temp_bytes), the last row of each key inserted with evictions,
 // then the filters; status[0] = an insertion failed, status[1..3] = {entries, longest probe (1
 // or 2), displaced keys}.
+// Home-first placement's buffers (n entries each; all null: insertion order decides which keys
+// of a crowded home live in their alt).
+struct TwoChoiceScratch {
+  uint32_t* home = nullptr;
+  uint32_t* sorted_home = nullptr;
+  uint32_t* sorted_idx = nullptr;
+  uint8_t* away = nullptr;
+};
 hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, int m,
                                    const uint64_t* keys, const uint32_t* fids, uint64_t n,
                                    uint64_t* sorted_keys, uint32_t* rows, uint32_t* sorted_rows,
-                                   void* temp, size_t* temp_bytes, uint32_t* status,
-                                   hipStream_t stream);
+                                   const TwoChoiceScratch& x, void* temp, size_t* temp_bytes,
+                                   uint32_t* status, hipStream_t stream);
 hipError_t launch_annotate(const ProteinArgs& a, hipStream_t stream);  // the protein path
 // ASCII residues [offsets[0], offsets[0] + n) -> the packed stream (packed_bytes(n) bytes; the
 // LUT of the table's replica): pack_residues_kernel.

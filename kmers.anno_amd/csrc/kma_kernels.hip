@@ -158,9 +158,10 @@ __device__ __forceinline__ bool claim_empty(uint64_t* slots, uint32_t b, uint64_
 __global__ __launch_bounds__(256) void build_two_choice_insert_kernel(
     uint64_t* slots, uint32_t n_buckets, int k, int m, const uint64_t* __restrict__ skeys,
     const uint32_t* __restrict__ srows, const uint32_t* __restrict__ fids, uint64_t n,
-    uint32_t* status) {
+    const uint8_t* __restrict__ away, uint8_t phase, uint32_t* status) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
+    if (away && away[i] != phase) continue;  // phase 0: the keys kept home; 1: the others
     const uint64_t key = skeys[i];
     if (key == 0 || (key >> (5 * k)) != 0) continue;  // no key / not a K-mer key: never stored
     if (i + 1 < n && skeys[i + 1] == key) continue;   // a later row of this key wins
@@ -194,6 +195,69 @@ __global__ __launch_bounds__(256) void build_two_choice_insert_kernel(
       at = other;
     }
     if (!done) atomicOr(status, 1u);
+  }
+}
+
+// Home-first placement (KMA_TC_SELECT): the keys of a home bucket that cannot all live there are
+// chosen before any insertion. home_kernel: the home of every key the insert kernel stores (the
+// last row of its run, a K-mer key), else kNoHome, with its sorted-key index; the pairs are then
+// radix-sorted by home, and select_kernel takes each home's run: up to kSlotsPerBucket keys stay
+// (away = 0: inserted first, into the home, where they all fit), the others go away (away = 1:
+// inserted after every home is filled, so into their alt buckets, evicting only where an alt
+// is full). The keys sent away are chosen greedily to set few filter positions in the home: each
+// next one adds the fewest positions not yet set (first 64 keys of a run; the rest go away as
+// they come). Against insertion order: c5 (10^8 keys, m = 6) simulated 2.8% -> 1.35% false
+// filter hits per missed window; measured displaced keys 7.50 -> 7.18% (a key sent to a full
+// alt still evicts), c5 kernel 3.124 -> 3.085 ms, LF 0.75 3.42 -> 3.37 ms (ABAB,
+// profiles/r05/tc_select_ab/; KMA_TC_SELECT=0 restores insertion order).
+constexpr uint32_t kNoHome = 0xFFFFFFFFu;
+__global__ __launch_bounds__(256) void build_two_choice_home_kernel(
+    const uint64_t* __restrict__ skeys, uint64_t n, int k, int m, uint32_t n_buckets,
+    uint32_t* __restrict__ home, uint32_t* __restrict__ idx) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = skeys[i];
+    const bool stored = key != 0 && (key >> (5 * k)) == 0 && !(i + 1 < n && skeys[i + 1] == key);
+    home[i] = stored ? home_bucket(key, k, m, n_buckets) : kNoHome;
+    idx[i] = (uint32_t)i;
+  }
+}
+__global__ __launch_bounds__(256) void build_two_choice_select_kernel(
+    const uint32_t* __restrict__ hs, const uint32_t* __restrict__ ids,
+    const uint64_t* __restrict__ skeys, uint64_t n, uint8_t* __restrict__ away) {
+  constexpr uint32_t S = kSlotsPerBucket;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = hs[i];
+    if (h == kNoHome) {
+      away[ids[i]] = 2;  // not stored: neither phase
+      continue;
+    }
+    if (i > 0 && hs[i - 1] == h) continue;  // a run's first thread does the run
+    uint64_t e = i + 1;
+    while (e < n && hs[e] == h) ++e;
+    const uint32_t L = (uint32_t)(e - i), W = L < 64u ? L : 64u;
+    for (uint64_t j = i; j < e; ++j) away[ids[j]] = j - i >= W ? 1 : 0;
+    if (L <= S) continue;
+    uint64_t chosen = 0;
+    uint32_t set = 0;
+    for (uint32_t it = 0; it < W - S; ++it) {
+      uint32_t best = 0, best_new = 64, best_mask = 0;
+      for (uint32_t j = 0; j < W; ++j) {
+        if (chosen >> j & 1ull) continue;
+        const uint32_t mask = filter_need<S>((uint32_t)skeys[ids[i + j]]);
+        const uint32_t fresh = (uint32_t)__popc(mask & ~set);
+        if (fresh < best_new) {
+          best = j;
+          best_new = fresh;
+          best_mask = mask;
+          if (fresh == 0) break;
+        }
+      }
+      chosen |= 1ull << best;
+      set |= best_mask;
+      away[ids[i + best]] = 1;
+    }
   }
 }
 
@@ -1505,26 +1569,51 @@ hipError_t launch_build_finalize(uint64_t* slots, const uint32_t* winner, const 
   return hipGetLastError();
 }
 
+#ifndef KMA_TC_SELECT
+#define KMA_TC_SELECT 1
+#endif
 hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, int m,
                                    const uint64_t* keys, const uint32_t* fids, uint64_t n,
                                    uint64_t* sorted_keys, uint32_t* rows, uint32_t* sorted_rows,
-                                   void* temp, size_t* temp_bytes, uint32_t* status,
-                                   hipStream_t stream) {
+                                   const TwoChoiceScratch& x, void* temp, size_t* temp_bytes,
+                                   uint32_t* status, hipStream_t stream) {
   if (wide_k(k) || n_buckets < 2) return hipErrorInvalidValue;
   // all 64 bits: a row whose key is not a K-mer key (bits above 5K) must not split a run
-  if (!temp)
-    return rocprim::radix_sort_pairs(nullptr, *temp_bytes, keys, sorted_keys, rows, sorted_rows,
-                                     (size_t)n, 0u, 64u, stream);
+  if (!temp) {
+    size_t t1 = 0, t2 = 0;
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, t1, keys, sorted_keys, rows, sorted_rows,
+                                             (size_t)n, 0u, 64u, stream);
+    if (e != hipSuccess) return e;
+    e = rocprim::radix_sort_pairs(nullptr, t2, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0u, 32u,
+                                  stream);
+    *temp_bytes = KMA_TC_SELECT ? std::max(t1, t2) : t1;
+    return e;
+  }
   hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n)), dim3(256), 0, stream, rows, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = rocprim::radix_sort_pairs(temp, *temp_bytes, keys, sorted_keys, rows, sorted_rows, (size_t)n,
                                 0u, 64u, stream);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(build_two_choice_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
-                     slots, n_buckets, k, m, sorted_keys, sorted_rows, fids, n, status);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (KMA_TC_SELECT && x.home) {
+    hipLaunchKernelGGL(build_two_choice_home_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                       sorted_keys, n, k, m, n_buckets, x.home, rows);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    e = rocprim::radix_sort_pairs(temp, *temp_bytes, x.home, x.sorted_home, rows, x.sorted_idx,
+                                  (size_t)n, 0u, 32u, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(build_two_choice_select_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                       x.sorted_home, x.sorted_idx, sorted_keys, n, x.away);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  const uint8_t* away = KMA_TC_SELECT ? x.away : nullptr;
+  for (uint8_t phase = 0; phase < (away ? 2 : 1); ++phase) {
+    hipLaunchKernelGGL(build_two_choice_insert_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                       slots, n_buckets, k, m, sorted_keys, sorted_rows, fids, n, away, phase,
+                       status);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(build_two_choice_filter_kernel, dim3(grid_for((uint64_t)n_buckets * kSlotsPerBucket)),
                      dim3(256), 0, stream, slots, n_buckets, k, m, status + 1);
   return hipGetLastError();
