@@ -1601,6 +1601,13 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
             const Clock::time_point t_issue = Clock::now();
             t_stage += std::chrono::duration<double, std::milli>(t_issue - t_w).count();
             const Seg& sg = segs[k];
+            // (The copies run at ~57 GB/s until the first piece kernel starts, then at ~36 GB/s:
+            // the engines' writes into HBM share the fabric with the probe's gathers at their
+            // request ceiling. Measured and not kept: the piece kernels reading the packed stream
+            // from the pinned buffer over PCIe instead, 5.5 vs 3.4 ms of kernels, calls 7.1-7.7
+            // vs 5.3-7.0 ms; the pool packing straight into fine-grained device memory through the
+            // BAR, 44 GB/s alone and 7.9 ms beside a DMA that takes 3.4 ms alone, where packing
+            // into pinned memory beside it takes 3.4 ms: profiles/r05/host_paths_r05/.)
             // Segments alternate over the two copy streams (two DMA engines: 52 vs 44 GB/s on
             // one stream, profiles/r05/e2e_streamed_fifo_r05i), in stream order on each, and a
             // piece's kernel waits for both: a piece's data lands as early as the link allows.
