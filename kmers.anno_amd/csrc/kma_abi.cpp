@@ -1607,7 +1607,10 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
             // from the pinned buffer over PCIe instead, 5.5 vs 3.4 ms of kernels, calls 7.1-7.7
             // vs 5.3-7.0 ms; the pool packing straight into fine-grained device memory through the
             // BAR, 44 GB/s alone and 7.9 ms beside a DMA that takes 3.4 ms alone, where packing
-            // into pinned memory beside it takes 3.4 ms: profiles/r05/host_paths_r05/.)
+            // into pinned memory beside it takes 3.4 ms: profiles/r05/host_paths_r05/; and the
+            // piece kernels but the last on a CU-masked stream (half the CUs), to leave the copies
+            // fabric: no effect in one process alternating both, 5.22-5.47 vs 5.25-5.39 ms,
+            // profiles/r05/host_cu_mask/.)
             // Segments alternate over the two copy streams (two DMA engines: 52 vs 44 GB/s on
             // one stream, profiles/r05/e2e_streamed_fifo_r05i), in stream order on each, and a
             // piece's kernel waits for both: a piece's data lands as early as the link allows.
