@@ -696,6 +696,10 @@ int build_two_choice_on_device(uint64_t* d_slots, uint64_t n_buckets, int k, int
   KMA_HIP(tmp.alloc(&x.sorted_home, n * 4));
   KMA_HIP(tmp.alloc(&x.sorted_idx, n * 4));
   KMA_HIP(tmp.alloc(&x.away, n));
+#ifndef KMA_TC_ALT_LOAD
+#define KMA_TC_ALT_LOAD 1
+#endif
+  if (KMA_TC_ALT_LOAD) KMA_HIP(tmp.alloc(&x.load, n_buckets));
   KMA_HIP(kma::launch_build_two_choice(d_slots, (uint32_t)n_buckets, k, m, d_keys, d_fids, n,
                                        skeys, rows, srows, x, temp, &temp_bytes, d_status, s));
   KMA_HIP(hipStreamSynchronize(s));  // before DevBufs frees the sort buffers

@@ -488,6 +488,7 @@ struct TwoChoiceScratch {
   uint32_t* sorted_home = nullptr;
   uint32_t* sorted_idx = nullptr;
   uint8_t* away = nullptr;
+  uint8_t* load = nullptr;  // n_buckets: keys homed per bucket (null: alt loads not considered)
 };
 hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, int m,
                                    const uint64_t* keys, const uint32_t* fids, uint64_t n,

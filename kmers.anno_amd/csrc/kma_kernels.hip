@@ -209,7 +209,10 @@ __global__ __launch_bounds__(256) void build_two_choice_insert_kernel(
 // they come). Against insertion order: c5 (10^8 keys, m = 6) simulated 2.8% -> 1.35% false
 // filter hits per missed window; measured displaced keys 7.50 -> 7.18% (a key sent to a full
 // alt still evicts), c5 kernel 3.124 -> 3.085 ms, LF 0.75 3.42 -> 3.37 ms (ABAB,
-// profiles/r05/tc_select_ab/; KMA_TC_SELECT=0 restores insertion order).
+// profiles/r05/tc_select_ab/; KMA_TC_SELECT=0 restores insertion order). Keys whose alt is
+// already filled by that bucket's own home keys go away last (each would evict one of them, a
+// second displaced key): displaced 7.18 -> 6.99% at LF 0.5 and 17.55 -> 15.49% at 0.75, c5
+// kernel 3.095 -> 3.084 and 3.374 -> 3.283 ms (profiles/r05/tc_alt_load_ab/; KMA_TC_ALT_LOAD=0).
 constexpr uint32_t kNoHome = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void build_two_choice_home_kernel(
     const uint64_t* __restrict__ skeys, uint64_t n, int k, int m, uint32_t n_buckets,
@@ -222,9 +225,22 @@ __global__ __launch_bounds__(256) void build_two_choice_home_kernel(
     idx[i] = (uint32_t)i;
   }
 }
+// Keys homed per bucket (capped at 255), from the runs of the sorted homes (zeroed before).
+__global__ __launch_bounds__(256) void build_two_choice_load_kernel(
+    const uint32_t* __restrict__ hs, uint64_t n, uint8_t* __restrict__ load) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = hs[i];
+    if (h == kNoHome || (i > 0 && hs[i - 1] == h)) continue;
+    uint64_t e = i + 1;
+    while (e < n && hs[e] == h && e - i < 255) ++e;
+    load[h] = (uint8_t)(e - i);
+  }
+}
 __global__ __launch_bounds__(256) void build_two_choice_select_kernel(
     const uint32_t* __restrict__ hs, const uint32_t* __restrict__ ids,
-    const uint64_t* __restrict__ skeys, uint64_t n, uint8_t* __restrict__ away) {
+    const uint64_t* __restrict__ skeys, uint64_t n, const uint8_t* __restrict__ load,
+    uint32_t n_buckets, uint8_t* __restrict__ away) {
   constexpr uint32_t S = kSlotsPerBucket;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -245,8 +261,12 @@ __global__ __launch_bounds__(256) void build_two_choice_select_kernel(
       uint32_t best = 0, best_new = 64, best_mask = 0;
       for (uint32_t j = 0; j < W; ++j) {
         if (chosen >> j & 1ull) continue;
-        const uint32_t mask = filter_need<S>((uint32_t)skeys[ids[i + j]]);
-        const uint32_t fresh = (uint32_t)__popc(mask & ~set);
+        const uint64_t key = skeys[ids[i + j]];
+        const uint32_t mask = filter_need<S>((uint32_t)key);
+        // a key whose alt is filled by its own home keys would evict one of them (a second key
+        // displaced): such keys go last
+        const bool alt_full = load && load[alt_bucket(key, h, n_buckets)] >= S;
+        const uint32_t fresh = (uint32_t)__popc(mask & ~set) + (alt_full ? 32u : 0u);
         if (fresh < best_new) {
           best = j;
           best_new = fresh;
@@ -1603,8 +1623,14 @@ hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, i
     e = rocprim::radix_sort_pairs(temp, *temp_bytes, x.home, x.sorted_home, rows, x.sorted_idx,
                                   (size_t)n, 0u, 32u, stream);
     if (e != hipSuccess) return e;
+    if (x.load) {
+      if ((e = hipMemsetAsync(x.load, 0, n_buckets, stream)) != hipSuccess) return e;
+      hipLaunchKernelGGL(build_two_choice_load_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                         x.sorted_home, n, x.load);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(build_two_choice_select_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
-                       x.sorted_home, x.sorted_idx, sorted_keys, n, x.away);
+                       x.sorted_home, x.sorted_idx, sorted_keys, n, x.load, n_buckets, x.away);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   const uint8_t* away = KMA_TC_SELECT ? x.away : nullptr;
