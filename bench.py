@@ -39,7 +39,6 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import subprocess
@@ -367,6 +366,11 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
             rate = reqs / (kernel_ms * 1e-3)
             out["line_requests_per_s"] = rate
             out["requests_frac_of_ceiling"] = rate / ceil["lines_per_s"]
+            # the kernel's real bound: fabric line requests against the live
+            # random-line ceiling; `frac` keeps SURVEY §8(d)'s algorithmic rule, which exceeds 1
+            # for minimizer layouts (windows sharing a home share its line)
+            out["frac_requests"] = rate / ceil["lines_per_s"]
+            out["bound_by"] = "random line requests (frac_requests)"
     return out
 
 
@@ -683,18 +687,13 @@ def e2e_host(table, residues, offsets, n_fid, reps=5):
            np.zeros(n_fid, np.uint32))
     kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid, out=out)
     best, prof = 1e30, None
-    lib = kmeranno.load()
     for _ in range(reps):
         t0 = time.perf_counter()
         kmeranno.annotate_proteins(table, residues, offsets, MIN_HITS, 0, n_fid=n_fid, out=out)
         dt = time.perf_counter() - t0
         if dt < best:
             best = dt
-            p = np.zeros(6, np.float64)
-            if hasattr(lib, "kma_debug_host_profile"):
-                lib.kma_debug_host_profile(p.ctypes.data_as(ctypes.c_void_p), 6)
-            prof = dict(zip(("setup", "stage", "launch", "wait", "outputs", "total"),
-                            p.tolist()))
+            prof = kmeranno.host_profile()
     e2e_host.profile = prof
     return best * 1e3
 
@@ -897,7 +896,9 @@ def main():
         total_lookups = (batch_windows if strong else n_win * world) * args.steps
         value = total_lookups / elapsed
         seqs = batch_seqs if strong else n_seq * world
-        m = table.info.minimizer_len
+        # the kernels' minimizer code (length | order bit): their template name in rocprof
+        m = table.info.minimizer_len | (kmeranno.LAYOUT_MOD_SAMPLING
+                                        if table.info.minimizer_order else 0)
         out = {
             "metric": METRIC, "value": value, "unit": "kmer lookups/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -910,6 +911,8 @@ def main():
                        "table_entries": t_size, "functions": n_fid, "k": K,
                        "load_factor": args.load_factor, "min_hits": MIN_HITS,
                        "table_layout_m": table.info.minimizer_len,
+                       "table_minimizer_order": "mod-sampling" if table.info.minimizer_order
+                       else "random",
                        "table_placement": "two-choice" if table.info.two_choice else "chained",
                        **({"options": args.option} if args.option else {}),
                        "parallelism": (f"input-shard x{world} of one batch" if strong else
@@ -934,7 +937,7 @@ def main():
                              "D2H, on the table's pooled stream)",
                     "packed_input": kmeranno.get_option(kmeranno.OPT_PACKED_INPUT),
                     "staging_threads": kmeranno.get_option(kmeranno.OPT_HOST_THREADS) or
-                    "min(16, cores)",
+                    f"min(16, host cores = {kmeranno.host_cores()})",
                     "ms": ms, "library_profile_ms": prof,
                     "lookups_per_s": n_win / (ms * 1e-3),
                     "seqs_per_s": n_seq / (ms * 1e-3), "kernel_ratio": ms / ph["annotate_kernel"],

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KMA_ABI_VERSION 6
+#define KMA_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define KMA_OK 0
@@ -97,8 +97,13 @@ extern "C" {
  * K = 8 whatever the table holds (ApplyKmerProcessor.java:108 sets KmerReference's K only). */
 #define KMA_MAX_K 12
 /* Layout codes (kma_table_build_device, kma_table_wrap_device, kma_table_layout_for): the
- * minimizer length m (0 = flat) | KMA_LAYOUT_TWO_CHOICE for two-choice placement (ABI 6).    */
+ * minimizer length m (0 = flat) | KMA_LAYOUT_TWO_CHOICE for two-choice placement (ABI 6)
+ * | KMA_LAYOUT_MOD_SAMPLING for the mod-sampling minimizer order (ABI 7; K = 8, m = 6 only: a
+ * key's minimizer is its m-mer at the position of its smallest 3-mer hash modulo K - m + 1,
+ * where the default order takes the m-mer of smallest hash; the creators use it for tables
+ * larger than the 256 MiB Infinity Cache, where it cuts the probe's bucket requests).         */
 #define KMA_LAYOUT_TWO_CHOICE 0x100
+#define KMA_LAYOUT_MOD_SAMPLING 0x40
 #define KMA_MAX_FID ((1u << 22) - 1u)
 
 
@@ -127,7 +132,15 @@ typedef struct kma_table_info {
   int32_t two_choice;    /* ABI 6: placement. 1 = two-choice (every key in its home bucket or
                             in one other bucket, a hash of the whole key: a lookup reads at
                             most 2 buckets); 0 = overflow chains                            */
-  int32_t pad_;
+  int32_t minimizer_order; /* ABI 7: how a key's minimizer is chosen among its m-mers (layout
+                            code bit KMA_LAYOUT_MOD_SAMPLING): 0 = smallest m-mer hash;
+                            1 = mod-sampling (the m-mer at the position of the smallest 3-mer
+                            hash modulo K - m + 1)                                           */
+  int32_t replicate_peer;  /* ABI 7: copies of the last kma_table_replicate made with peer
+                            access enabled (the destination GPU reads replica 0 over xGMI)  */
+  int32_t replicate_local; /* ABI 7: copies of that call on replica 0's own device; the rest
+                            (replicate_bytes / bytes - peer - local) were left to the runtime
+                            without peer access (it may stage them through host memory)     */
 } kma_table_info;
 
 /* One 6-frame hit: the kmer at forward 1-based left edge `left` on `strand` ('+' or '-') of
@@ -153,7 +166,8 @@ int kma_device_count(int* out_n);
  * variables; tuning builds compiled with -DKMA_TUNING_ENV=1 seed these from KMA_MINIMIZER,
  * KMA_BLOCK_PROTEINS, KMA_DEFER, KMA_HOST_PIECES and KMA_HASH_SLICE). Defaults in brackets.
  *   KMA_OPT_LAYOUT          table creators' layout [-1: size rule + measurement, see
- *                           kma_table_layout_for]; 0 = flat, 6 / 7 = minimizer m = min(K, value)
+ *                           kma_table_layout_for]; 0 = flat, 6 / 7 = minimizer m = min(K, value);
+ *                           6 | KMA_LAYOUT_MOD_SAMPLING = m 6 in the mod-sampling order (K = 8)
  *   KMA_OPT_BLOCK_PROTEINS  proteins per annotate_kernel block [0: by batch and table size];
  *                           1..8
  *   KMA_OPT_DEFER           the protein kernel's two-pass grid [-1: automatic for grids of 1-4
@@ -167,13 +181,18 @@ int kma_device_count(int* out_n);
  *                           (the H2D moves 0.625 B per residue) under 1 and 2; device calls
  *                           with a pack kernel into the workspace under 2, and under 1 for
  *                           batches of >= 2^25 residues; 0 = the probe packs ASCII itself
- *   KMA_OPT_HOST_THREADS    host calls: threads staging (copying / packing) the input
- *                           [0: min(16, cores)]; 1..64
+ *   KMA_OPT_HOST_THREADS    host calls: threads staging (copying / packing) the input, the
+ *                           whole call's budget split over the replicas it fans out to [0: each
+ *                           of n replicas min(16, cores / n), cores = the process's CPUs bounded
+ *                           by its cgroup CPU quota]; 1..64
  *   KMA_OPT_HOST_SLICE      host protein calls: residues per device call [0: 2^31]; a replica's
  *                           share of a larger batch is annotated as consecutive slices of
- *                           whole proteins (tallies summed); >= 1 (tests set it low)
+ *                           whole proteins (tallies summed); 1 .. 2^32 - 128 (tests set it low)
  *   KMA_OPT_PLACEMENT       table creators [-1: two-choice placement for K <= 8, chains if that
  *                           build fails, and for K > 8]; 0 = chains only; 1 = as -1
+ *   KMA_OPT_HOST_PIECE_MIN  host protein calls: fewest residues per pipeline piece [0: 2^24]; a
+ *                           call runs min(KMA_OPT_HOST_PIECES, residues / this) pieces (ABI 7;
+ *                           tests set it low to run many pieces on small batches)
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -185,6 +204,7 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_HOST_THREADS 7
 #define KMA_OPT_HOST_SLICE 8
 #define KMA_OPT_PLACEMENT 9
+#define KMA_OPT_HOST_PIECE_MIN 10
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);
@@ -248,7 +268,10 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
  *   kma_table_build_device: d_slots (info.bytes: n_buckets * 64 bytes, 128 in the 16-slot build)
  *                           and d_winner (n_buckets * S u32, S = kma_bucket_slots_for(k)) are
  *                           caller scratch; keys/fids are device arrays of K-mers; layout -1 =
- *                           kma_table_layout_for, else 0 / min(K,6) / min(K,7), | KMA_LAYOUT_
+ *                           kma_table_layout_for's code (in both build and wrap: a table built
+ *                           with -1 wraps with -1, unless the caller rebuilt it with an explicit
+ *                           code after a failed two-choice build: then it wraps with that code),
+ *                           else 0 / min(K,6) / min(K,7) (| KMA_LAYOUT_MOD_SAMPLING), | KMA_LAYOUT_
  *                           TWO_CHOICE for two-choice placement (K <= 8; d_winner unused; the
  *                           build allocates its sort buffers and waits for `stream`); builds on
  *                           `stream`; d_status (4 u32) receives {table full / two-choice build
@@ -256,7 +279,9 @@ int kma_table_replicas(const kma_table* table, int* n, int* device_ids, int cap)
  *                           keys} (a caller rebuilds chained when [0] is set, and may rebuild
  *                           with layout 0 when displaced keys are many); fids are masked to 22
  *                           bits; keys that are 0 or not K-mer keys (>= 2^(5K)) are not stored.
- *   kma_table_wrap_device : adopt an already-built slot array of that layout code (not owned). */
+ *   kma_table_wrap_device : adopt an already-built slot array of that layout code (not owned;
+ *                           the placement and order are not stored in the slots: the code must be
+ *                           the one the table was built with).                                   */
 uint64_t kma_table_buckets_for(uint64_t n_keys, double load_factor);
 uint64_t kma_table_buckets_for_k(uint64_t n_keys, double load_factor, int k);
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,

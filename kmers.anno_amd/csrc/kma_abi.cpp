@@ -11,6 +11,7 @@
 // stream only). A table may be replicated on several devices; a host call then cuts its batch
 // into residue-balanced contiguous shards, one host thread per replica.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -37,20 +38,21 @@ namespace {
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 10;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}, {-1}};
+constexpr int kNumOpts = 11;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}, {-1}, {0}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
   switch (opt) {
-    case KMA_OPT_LAYOUT: return v == -1 || v == 0 || v == 6 || v == 7;
+    case KMA_OPT_LAYOUT: return v == -1 || v == 0 || v == 6 || v == 7 || v == (6 | kma::kOrderMod);
     case KMA_OPT_BLOCK_PROTEINS: return v >= 0 && v <= kma::kBlockProteins;
     case KMA_OPT_DEFER: return v >= -1 && v <= 64;
     case KMA_OPT_HOST_PIECES: return v >= 0 && v <= 16;
     case KMA_OPT_HASH_SLICE: return v >= 0;
     case KMA_OPT_PACKED_INPUT: return v >= 0 && v <= 2;
     case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
-    case KMA_OPT_HOST_SLICE: return v >= 0;
+    case KMA_OPT_HOST_SLICE: return v >= 0 && v <= (int64_t)((1ull << 32) - 128);  // a call's limit
+    case KMA_OPT_HOST_PIECE_MIN: return v >= 0 && v <= (int64_t)(1ull << 32);
     case KMA_OPT_PLACEMENT: return v >= -1 && v <= 1;
     default: return false;
   }
@@ -75,26 +77,80 @@ struct EnvOptions {  // tuning builds: the A/B scripts' variables seed the defau
 
 int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
+// MI355X's Infinity Cache (MALL): tables larger than this are probed from HBM.
+constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
+
 // The forced table layout (KMA_OPT_LAYOUT): -1 = not forced.
 int forced_layout() { return (int)opt(KMA_OPT_LAYOUT); }
 // Table creators try two-choice placement first for narrow tables (KMA_OPT_PLACEMENT -1 / 1);
 // 0 builds chains only.
 bool two_choice_first(int k) { return !kma::wide_k(k) && opt(KMA_OPT_PLACEMENT) != 0; }
 
-// Host threads a host call stages (copies or packs) its input with (KMA_OPT_HOST_THREADS; 0:
-// min(16, cores)). Packing 5 bits per residue keeps up with the PCIe link only on ~16 threads.
-size_t staging_threads() {
-  const int64_t o = opt(KMA_OPT_HOST_THREADS);
-  return o > 0 ? (size_t)o : std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+// CPUs this process may use: its affinity mask, bounded by a cgroup CPU quota (a container or a
+// GPU box granted a share of a machine lists every CPU of the machine in the mask).
+long cgroup_quota_cpus() {
+  auto ceil_div = [](long long q, long long p) { return (long)((q + p - 1) / p); };
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // v2: "<quota|max> <period>"
+    char q[32] = {};
+    long long period = 0;
+    const bool ok = fscanf(f, "%31s %lld", q, &period) == 2;
+    fclose(f);
+    if (ok && strcmp(q, "max") != 0 && period > 0 && atoll(q) > 0) return ceil_div(atoll(q), period);
+    return 0;
+  }
+  long long quota = -1, period = 0;
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // v1
+    if (fscanf(f, "%lld", &quota) != 1) quota = -1;
+    fclose(f);
+  }
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+    if (fscanf(f, "%lld", &period) != 1) period = 0;
+    fclose(f);
+  }
+  return quota > 0 && period > 0 ? ceil_div(quota, period) : 0;
 }
+size_t host_cores() {
+  static const size_t n = [] {
+    size_t c = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) c = (size_t)CPU_COUNT(&set);
+    const long q = cgroup_quota_cpus();
+    return q > 0 ? std::min(c, (size_t)q) : c;
+  }();
+  return n;
+}
+
+// Host threads one staging job (a replica's share of a host call) stages (copies or packs) its
+// input with. KMA_OPT_HOST_THREADS is the whole call's budget, split over the replicas the call
+// fans out to; by default each of n replicas takes host_cores() / n, at most 16 (packing 5 bits
+// per residue keeps up with one PCIe link on ~16 threads). Round 5 gave every replica min(16,
+// cores): an 8-replica call ran 8 jobs of 16 on one pool of at most 63 threads.
+size_t staging_width(int n_replicas) {
+  const size_t n = (size_t)std::max(1, n_replicas);
+  const int64_t o = opt(KMA_OPT_HOST_THREADS);
+  if (o > 0) return std::max<size_t>(1, (size_t)o / n);
+  return std::clamp<size_t>(host_cores() / n, 1, 16);
+}
+// The width of the staging jobs of the calling thread: set for a replica's shard thread by the
+// host call that fans out (ShardWidth), else a one-replica call's.
+thread_local size_t t_shard_width = 0;
+size_t staging_threads() { return t_shard_width ? t_shard_width : staging_width(1); }
+struct ShardWidth {
+  explicit ShardWidth(size_t w) { t_shard_width = w; }
+  ~ShardWidth() { t_shard_width = 0; }
+};
 
 // Library-wide pool of staging threads (grown on demand, never shrunk; threads sleep when idle).
 // run(n, width, fn) calls fn(0..n-1) on the calling thread plus up to width - 1 pool threads and
 // returns when every call has returned. Several host calls may run jobs at once (kma apply's
-// workers each stage their own batch): pool threads take the oldest job with free width, and a
-// caller always works on its own job, so every job finishes even when the pool is busy. Round 3
-// and early round 4 spawned threads per staging piece: a c5 host call spent milliseconds
-// creating ~120 threads, and pieces of 5 chunks kept 5 of 16 threads busy.
+// workers each stage their own batch; a replicated table's host call stages every replica's
+// share at once): pool threads take the oldest job with free width, and a caller always works on
+// its own job, so every job finishes even when the pool is busy. The pool grows to the summed
+// width of the jobs running at once (round 5 grew it to one job's width: 8 replicas' jobs of 16
+// shared at most 63 threads). Round 3 and early round 4 spawned threads per staging piece: a c5
+// host call spent milliseconds creating ~120 threads, and pieces of 5 chunks kept 5 of 16
+// threads busy.
 class StagingPool {
  public:
   template <class F>
@@ -116,7 +172,8 @@ class StagingPool {
     j.fn = (void*)&fn;
     if (width > 1) {
       std::lock_guard<std::mutex> g(mu_);
-      while (threads_.size() < width - 1 && threads_.size() < kMaxThreads)
+      demand_ += width - 1;
+      while (threads_.size() < demand_ && threads_.size() < kMaxThreads)
         threads_.emplace_back([this] { worker(); });
       jobs_.push_back(&j);
       cv_.notify_all();
@@ -132,6 +189,7 @@ class StagingPool {
     if (width > 1) {
       std::unique_lock<std::mutex> lk(mu_);
       jobs_.erase(std::remove(jobs_.begin(), jobs_.end(), &j), jobs_.end());
+      demand_ -= width - 1;
       done_cv_.wait(lk, [&] { return j.active == 0; });
     }
   }
@@ -145,7 +203,7 @@ class StagingPool {
   }
 
  private:
-  static constexpr size_t kMaxThreads = 63;
+  static constexpr size_t kMaxThreads = 255;
   struct Job {
     uint64_t n = 0;
     size_t width = 1;
@@ -179,6 +237,7 @@ class StagingPool {
   std::condition_variable cv_, done_cv_;
   std::vector<Job*> jobs_;
   std::vector<std::thread> threads_;
+  size_t demand_ = 0;  // summed width - 1 of the jobs running (guarded by mu_)
   bool stop_ = false;
 };
 
@@ -230,14 +289,22 @@ void pool_memcpy(void* dst, const void* src, size_t n) {
 }
 }  // namespace
 
+// The size rule's minimizer code (m | order): m = min(K, 6) up to kMinimizer6Buckets buckets,
+// else min(K, 7); K = 8, m = 6 tables larger than the Infinity Cache take the mod-sampling order
+// (kma_internal.h kOrderMod: fewer home-line requests per window where every request goes to
+// HBM; its extra VALU per window slows the cache-resident configs). KMA_OPT_LAYOUT forces a code.
 int kma::minimizer_len(int k, uint64_t n_buckets) {
   const int m6 = k < 6 ? k : 6, m7 = k < 7 ? k : 7;
   const int f = forced_layout();
   if (f == 0) return 0;
   if (f == 6) return m6;
   if (f == 7) return m7;
+  if (f == (6 | kma::kOrderMod)) return kma::order_mod_valid(k, 6) ? 6 | kma::kOrderMod : m6;
   const uint64_t lim = kma::wide_k(k) ? kma::kMinimizer6BucketsWide : kma::kMinimizer6Buckets;
-  return n_buckets <= lim ? m6 : m7;
+  const int m = n_buckets <= lim ? m6 : m7;
+  const uint64_t bb = kma::wide_k(k) ? 64u : (uint64_t)kma::kBucketBytes;
+  const bool beyond_cache = n_buckets * bb > kInfinityCacheBytes;
+  return kma::order_mod_valid(k, m) && beyond_cache ? m | kma::kOrderMod : m;
 }
 
 namespace {
@@ -383,7 +450,7 @@ void pack_rows(const uint8_t* lut, const char* text, const uint64_t* off, uint64
 
 template <class F>
 void parallel_rows(uint64_t n, F f) {
-  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  unsigned nt = (unsigned)std::min<size_t>(16, host_cores());
   if (n < (1u << 16)) nt = 1;
   std::vector<std::thread> th;
   const uint64_t chunk = (n + nt - 1) / nt;
@@ -440,6 +507,7 @@ struct kma_workspace {
   int n_cu = 256;
   uint32_t* d_gset = nullptr;  // protein sets that do not fit in LDS: 2 u32 per residue
   uint8_t* d_packed = nullptr; // the call's residues packed (kma_internal.h packed_bytes)
+  bool host_ctx = false;       // a host context's workspace: no d_packed (kma_annotate_proteins)
   uint64_t res_cap = 0;        // residues per call
   // 6-frame path (kma_workspace_reserve_contigs): staged hits, block counts, scan.
   kma_hit* d_cstage = nullptr;
@@ -565,6 +633,7 @@ int acquire_ctx(kma_table* t, int device, HostCtx** out) {
     destroy_ctx(c);
     return rc;
   }
+  c->ws->host_ctx = true;
   *out = c;
   return KMA_OK;
 }
@@ -634,7 +703,8 @@ kma_table* new_table(int device, int k, int m, uint64_t n_buckets, const uint8_t
   t->info.slots_per_bucket = kma::slots_for_k(k);
   t->info.k = k;
   t->info.device = device;
-  t->info.minimizer_len = m;
+  t->info.minimizer_len = m & kma::kMinimizerMask;
+  t->info.minimizer_order = (m & kma::kOrderMod) ? 1 : 0;
   int ne = 0;
   for (int c = 0; c < 256; ++c)
     if (lut[c] >= 28) t->info.extra_syms[lut[c] - 28] = (uint8_t)c, ++ne;
@@ -824,7 +894,7 @@ int create_from_device_keys(const uint64_t* d_keys, const uint32_t* d_fids, uint
   };
   const int m6 = std::min(k, 6), m7 = std::min(k, 7);
   if (forced_layout() < 0) {
-    if (m == m6 && m6 != m7 && displaced(st) > kma::kRetryDisplaced)
+    if ((m & kma::kMinimizerMask) == m6 && m6 != m7 && displaced(st) > kma::kRetryDisplaced)
       if (int rc = try_layout(m7, [](const uint32_t* a, const uint32_t* b) { return b[3] < a[3]; }))
         return rc;
     const bool crowded = displaced(st) > kma::kMaxDisplaced || st[2] > kma::kMaxChain;
@@ -892,6 +962,29 @@ int fan_out(int n, F f) {
       g_err = msg[i];
       return rc[i];
     }
+  return KMA_OK;
+}
+
+// A layout code (kma_table_build_device / kma_table_wrap_device) -> minimizer code (m | order)
+// and placement. -1 is kma_table_layout_for's code for (k, n_buckets) in both entry points, so a
+// table built with -1 and wrapped with -1 agree (a caller whose -1 build reports a failed
+// two-choice insertion rebuilds with an explicit chained code and wraps with that code).
+int resolve_layout(int k, uint64_t n_buckets, int layout, int* m, bool* two) {
+  const int code = layout < 0 ? kma::minimizer_len(k, n_buckets) |
+                                    (two_choice_first(k) && n_buckets >= 2 ? kma::kLayoutTwoChoice : 0)
+                              : layout;
+  if (code & ~(kma::kLayoutMask | kma::kLayoutTwoChoice))
+    return fail(KMA_E_INVALID, "layout code %d has unknown bits", layout);
+  *m = code & kma::kLayoutMask;
+  *two = (code & kma::kLayoutTwoChoice) != 0;
+  const int mm = *m & kma::kMinimizerMask;
+  if ((*m & ~kma::kMinimizerMask) & ~kma::kOrderMod)
+    return fail(KMA_E_INVALID, "layout code %d has unknown bits", layout);
+  if ((*m & kma::kOrderMod) ? !kma::order_mod_valid(k, *m)
+                            : (mm != 0 && mm != std::min(k, 6) && mm != std::min(k, 7)))
+    return fail(KMA_E_INVALID,
+                "layout %d is not 0, min(K, 6) or min(K, 7) (| mod-sampling: K = 8, m = 6)", layout);
+  if (*two && kma::wide_k(k)) return fail(KMA_E_INVALID, "two-choice placement takes K <= 8");
   return KMA_OK;
 }
 
@@ -1011,6 +1104,7 @@ int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
     int dev;
     uint64_t* d = nullptr;
     hipStream_t s = nullptr;
+    bool peer = false;  // the destination reads replica 0 directly (peer access enabled)
   };
   std::vector<Dest> dst(n_devices);
   auto cleanup = [&](bool free_slots) {
@@ -1028,6 +1122,17 @@ int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
     hipError_t e = ds.err;
     if (e == hipSuccess) e = hipMalloc(&x.d, bytes);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking);
+    if (e == hipSuccess && x.dev != src.device) {
+      // Peer access from the destination to replica 0's device, once per pair (an enabled pair
+      // stays enabled): its copy engine then pulls the slot array over xGMI. Without it the
+      // runtime may stage a peer copy through host memory.
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, x.dev, src.device) == hipSuccess && can) {
+        const hipError_t pe = hipDeviceEnablePeerAccess(src.device, 0);
+        if (pe == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        x.peer = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
+      }
+    }
     if (e != hipSuccess) {
       cleanup(true);
       return fail(e == hipErrorOutOfMemory ? KMA_E_NOMEM : KMA_E_DEVICE,
@@ -1065,6 +1170,12 @@ int kma_table_replicate(kma_table* t, int n_devices, const int* device_ids) {
   std::lock_guard<std::mutex> g(t->reps_mu);
   t->info.replicate_ms = ms;
   t->info.replicate_bytes = bytes * (uint64_t)n_devices;
+  t->info.replicate_peer = 0;
+  t->info.replicate_local = 0;
+  for (const Dest& x : dst) {
+    t->info.replicate_peer += x.peer ? 1 : 0;
+    t->info.replicate_local += x.dev == src.device ? 1 : 0;
+  }
   return KMA_OK;
 }
 
@@ -1108,16 +1219,15 @@ int kma_table_destroy(kma_table* table) {
 int kma_table_build_device(void* d_slots, uint64_t n_buckets, int k, int layout,
                            uint32_t* d_winner, const uint64_t* d_keys, const uint32_t* d_fids,
                            uint64_t n, uint32_t* d_status, void* stream) {
-  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
-  // d_winner is the chained build's scratch; a two-choice build does not read it.
-  if (!d_slots || (!two && !d_winner) || !d_status || (n && (!d_keys || !d_fids)) || !n_buckets)
-    return fail(KMA_E_INVALID, "null argument");
   if (int rc = check_k(k)) return rc;
-  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout & kma::kLayoutMask;
-  if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
-    return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
+  if (!n_buckets) return fail(KMA_E_INVALID, "null argument");
+  int m = 0;
+  bool two = false;
+  if (int rc = resolve_layout(k, n_buckets, layout, &m, &two)) return rc;
+  // d_winner is the chained build's scratch; a two-choice build does not read it.
+  if (!d_slots || (!two && !d_winner) || !d_status || (n && (!d_keys || !d_fids)))
+    return fail(KMA_E_INVALID, "null argument");
   if (two) {
-    if (kma::wide_k(k)) return fail(KMA_E_INVALID, "two-choice placement takes K <= 8");
     return build_two_choice_on_device(static_cast<uint64_t*>(d_slots), n_buckets, k, m, d_keys,
                                       d_fids, n, d_status, static_cast<hipStream_t>(stream));
   }
@@ -1131,11 +1241,10 @@ int kma_table_wrap_device(void* d_slots, uint64_t n_buckets, int k, int layout, 
   if (n_buckets >= kMaxBuckets) return fail(KMA_E_INVALID, "%llu buckets or more",
                                            (unsigned long long)kMaxBuckets);
   if (int rc = check_k(k)) return rc;
-  const bool two = layout >= 0 && (layout & kma::kLayoutTwoChoice);
-  const int m = layout < 0 ? kma::minimizer_len(k, n_buckets) : layout & kma::kLayoutMask;
-  if (m != 0 && m != std::min(k, 6) && m != std::min(k, 7))
-    return fail(KMA_E_INVALID, "layout %d is not 0, min(K, 6) or min(K, 7)", layout);
-  if (two && (kma::wide_k(k) || n_buckets < 2))
+  int m = 0;
+  bool two = false;
+  if (int rc = resolve_layout(k, n_buckets, layout, &m, &two)) return rc;
+  if (two && n_buckets < 2)
     return fail(KMA_E_INVALID, "two-choice placement takes K <= 8 and 2 buckets or more");
   uint8_t lut[256];
   standard_lut(lut);
@@ -1264,7 +1373,6 @@ const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 // single proteins, so the last blocks to start end sooner; profiles/r05/c2_taper_r05u/) 47.0 /
 // 49.3 / 54.0 / 55.1 us for tails of 1/4, 1/2, 1 and 2 resident waves: each group's fixed chain
 // (offsets, first residues, final walks, vote) costs more than the shorter tail saves.
-constexpr uint64_t kInfinityCacheBytes = 256ull << 20;
 uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes) {
   const int64_t f = ws->opt_block_proteins != kOptUnset ? ws->opt_block_proteins
                                                          : opt(KMA_OPT_BLOCK_PROTEINS);
@@ -1305,13 +1413,11 @@ bool pack_on_device(uint64_t n_residues) {
   return n_residues > 0 && (v == 2 || (v == 1 && n_residues >= kPackMinResidues));
 }
 
-// The workspace's packed stream for device calls that pack (sized for its reserved residues).
-int ensure_packed(kma_workspace* ws) {
+// The workspace's packed stream for device calls that pack: allocated by
+// kma_workspace_reserve_batch (never here: the device entry points do not allocate).
+int ensure_packed(const kma_workspace* ws) {
   if (ws->d_packed) return KMA_OK;
-  DeviceScope ds(ws->device);
-  if (ds.err != hipSuccess) return fail(KMA_E_DEVICE, "hipSetDevice(%d)", ws->device);
-  KMA_HIP(hipMalloc(&ws->d_packed, kma::packed_bytes(ws->res_cap + kResPad)));
-  return KMA_OK;
+  return fail(KMA_E_CAPACITY, "workspace has no packed stream (kma_workspace_reserve_batch first)");
 }
 
 // The protein path on one replica (device buffers, asynchronous on s).
@@ -1419,15 +1525,18 @@ constexpr bool kStreamedCopies = KMA_HOST_STREAM != 0;
 // Host-side phase times of the last host protein shard call (kma_debug_host_profile, for the
 // host-call measurements in scripts/e2e_host.py): ms in setup (context, reservations, offsets),
 // staging (packing / copying into pinned memory and queueing the copies), launches, the final
-// wait for the stream, the output copies, and the whole call.
+// wait for the stream, the output copies, and the whole call; then the staging width and the
+// pieces. Also per replica (the first kProfReplicas of a fanned-out call).
+constexpr int kProfFields = 8, kProfReplicas = 64;
 std::mutex g_prof_mu;
-double g_prof[6] = {};
+double g_prof[kProfFields] = {};
+double g_prof_rep[kProfReplicas][kProfFields] = {};
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point a) {
   return std::chrono::duration<double, std::milli>(Clock::now() - a).count();
 }
 
-int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
+int protein_shard(kma_table* t, const Replica& r, int rep, const uint8_t* residues,
                   const uint64_t* offsets, uint32_t lo, uint32_t hi, int min_hits,
                   uint32_t flags, int32_t* out_fid, int32_t* out_count, uint8_t* out_status,
                   uint32_t* tally, uint32_t n_fid) {
@@ -1466,7 +1575,8 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   // 5.6-5.7 / 6.0 / 6.1 ms at 8 / 12 / 16 pieces, profiles/r05/e2e_streamed_alt_r05j);
   // a small call is one piece). c5 whole batch: 12.5 ms as one piece, 8.6 ms in 8 (round 2,
   // profiles/r02r_host_pipeline/).
-  constexpr uint64_t kPieceBytes = 16ull << 20;
+  const int64_t pm = opt(KMA_OPT_HOST_PIECE_MIN);
+  const uint64_t kPieceBytes = pm > 0 ? (uint64_t)pm : 16ull << 20;
   const int64_t po = opt(KMA_OPT_HOST_PIECES);
   // packed input: the stream is copied in segments as it is packed (kStreamedCopies)
   const bool streamed = packed && kStreamedCopies;
@@ -1677,10 +1787,11 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
   }
   if (tally) std::memcpy(tally, hout + n * 8ull, n_fid * 4ull);
   {
-    const double p[6] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o) - t_wait,
-                         ms_since(t_call)};
+    const double p[kProfFields] = {t_setup, t_stage, t_launch, t_wait, ms_since(t_o) - t_wait,
+                                   ms_since(t_call), (double)staging_threads(), (double)n_pieces};
     std::lock_guard<std::mutex> g(g_prof_mu);
-    std::copy(p, p + 6, g_prof);
+    std::copy(p, p + kProfFields, g_prof);
+    if (rep < kProfReplicas) std::copy(p, p + kProfFields, g_prof_rep[rep]);
   }
   return KMA_OK;
 }
@@ -1688,13 +1799,23 @@ int protein_shard(kma_table* t, const Replica& r, const uint8_t* residues,
 
 extern "C" {
 
-// Not in kmeranno.h: measurement hook (see g_prof).
+// Not in kmeranno.h: measurement hooks (see g_prof). kma_debug_host_profile: the last shard
+// call's phases; kma_debug_host_profile_replica: the last shard call of replica `rep` (its index
+// in the table's replica list) of a fanned-out host call.
 int kma_debug_host_profile(double* out, int n) {
   if (!out || n < 0) return KMA_E_INVALID;
   std::lock_guard<std::mutex> g(g_prof_mu);
-  std::copy(g_prof, g_prof + std::min(n, 6), out);
+  std::copy(g_prof, g_prof + std::min(n, kProfFields), out);
   return KMA_OK;
 }
+int kma_debug_host_profile_replica(int rep, double* out, int n) {
+  if (!out || n < 0 || rep < 0 || rep >= kProfReplicas) return KMA_E_INVALID;
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  std::copy(g_prof_rep[rep], g_prof_rep[rep] + std::min(n, kProfFields), out);
+  return KMA_OK;
+}
+// Not in kmeranno.h: the CPUs the library sizes its staging jobs by (host_cores).
+int kma_debug_host_cores(void) { return (int)host_cores(); }
 
 int kma_workspace_reserve_contigs(kma_workspace* ws, uint64_t n_bases) {
   if (!ws) return fail(KMA_E_INVALID, "null workspace");
@@ -1750,9 +1871,10 @@ int kma_workspace_reserve_batch(kma_workspace* ws, uint64_t n_residues, uint64_t
   free_protein_scratch(ws);
   KMA_HIP(hipMalloc(&ws->d_gset, 2 * (n_residues + kResPad) * 4));
   ws->res_cap = n_residues;
-  // The device call's packed stream only when a call of this size would pack (host calls and
-  // small device calls never read it); a call that packs later allocates it then.
-  if (pack_on_device(n_residues)) return ensure_packed(ws);
+  // The device calls' packed stream (0.625 B per residue), whatever KMA_OPT_PACKED_INPUT is now:
+  // a device call that packs must not allocate (it may be graph-captured). Host
+  // contexts' workspaces never pack on the device (their calls stage the stream themselves).
+  if (!ws->host_ctx) KMA_HIP(hipMalloc(&ws->d_packed, kma::packed_bytes(n_residues + kResPad)));
   return KMA_OK;
 }
 
@@ -1939,7 +2061,9 @@ int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const ui
   // proteins, one device call each (the kernels index residues with 32 bits); slice tallies add.
   const int64_t so = opt(KMA_OPT_HOST_SLICE);
   const uint64_t slice = so > 0 ? (uint64_t)so : 1ull << 31;
+  const size_t width = staging_width(nr);  // each replica's staging jobs
   const int rc = fan_out(nr, [&](int i) {
+    ShardWidth sw(width);
     std::vector<uint32_t> st(tally ? n_fid : 0);
     for (uint32_t lo = b[i]; lo < b[i + 1];) {
       uint32_t hi = (uint32_t)(std::upper_bound(offsets + lo + 1, offsets + b[i + 1] + 1,
@@ -1947,8 +2071,8 @@ int kma_annotate_proteins(const kma_table* tc, const uint8_t* residues, const ui
       if (hi <= lo) hi = lo + 1;  // one protein longer than a slice: a call of its own
       const bool whole = lo == b[i] && hi == b[i + 1];
       uint32_t* tl = !tally ? nullptr : whole ? part[i].data() : st.data();
-      if (int rc = protein_shard(t, reps[i], residues, offsets, lo, hi, min_hits, flags, out_fid,
-                                 out_count, out_status, tl, n_fid))
+      if (int rc = protein_shard(t, reps[i], i, residues, offsets, lo, hi, min_hits, flags,
+                                 out_fid, out_count, out_status, tl, n_fid))
         return rc;
       if (tally && !whole)
         for (uint32_t f = 0; f < n_fid; ++f) part[i][f] += st[f];
@@ -2124,7 +2248,9 @@ int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offs
   std::vector<std::vector<uint32_t>> tal(tally ? nr : 0);
   for (int i = 0; i < (tally ? nr : 0); ++i)
     tal[i].assign(out_tally + (uint64_t)b[i] * n_fid, out_tally + (uint64_t)b[i + 1] * n_fid);
+  const size_t width = staging_width(nr);
   int rc = fan_out(nr, [&](int i) {
+    ShardWidth sw(width);
     return contig_shard(t, reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
                         nullptr, &nh[i], tally ? tal[i].data() : nullptr, n_fid);
   });
@@ -2140,6 +2266,7 @@ int annotate_contigs_host(kma_table* t, const uint8_t* dna, const uint64_t* offs
   if (total == 0) return KMA_OK;
   std::vector<std::vector<kma_hit>> hv(nr);
   rc = fan_out(nr, [&](int i) {
+    ShardWidth sw(width);
     if (nh[i] == 0) return KMA_OK;
     return contig_shard(t, reps[i], dna, offsets, b[i], b[i + 1], genetic_code, strict,
                         &hv[i], &nh[i], nullptr, 0);

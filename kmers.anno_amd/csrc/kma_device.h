@@ -316,7 +316,8 @@ __device__ __forceinline__ uint32_t set_slot(uint32_t key, uint32_t cap) {
 }  // namespace
 
 // Kernels are instantiated per (K, layout): the minimizer length is a template parameter so
-// that the m-mer loop unrolls; layouts are m = min(K, 6), min(K, 7) and 0 (flat). K = 9..12
+// that the m-mer loop unrolls; layouts are m = min(K, 6), min(K, 7) and 0 (flat), and for K = 8
+// m = 6 in the mod-sampling order (6 | kOrderMod). K = 9..12
 // are wide tables (16-byte slots); kernels that take only narrow tables reject them.
 template <int K, template <int, int> class Launch, typename... Args>
 inline hipError_t dispatch_m(int m, Args&&... args) {
@@ -325,6 +326,8 @@ inline hipError_t dispatch_m(int m, Args&&... args) {
   if (m == 0) return Launch<K, 0>::run(args...);
   if (m == M6) return Launch<K, M6>::run(args...);
   if (m == M7) return Launch<K, M7>::run(args...);
+  if constexpr (order_mod_valid(K, 6))  // the mod-sampling order (kma_internal.h): K = 8, m = 6
+    if (m == (6 | kOrderMod)) return Launch<K, 6 | kOrderMod>::run(args...);
   return hipErrorInvalidValue;
 }
 template <template <int, int> class Launch, typename... Args>

@@ -147,12 +147,50 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
   return mix32(sub * 0x9E3779B1u + 0x7F4A7C15u);
 #endif
 }
-// Measured and not kept (round 5, profiles/r05/syncmer_ab_r05s/): a closed-syncmer order (an
-// m-mer whose smallest 3-mer hash sits at its first or last position ranks before all others),
-// density 0.452 vs 0.500 for random order at K = 8, m = 6 (simulated), parity green. The ~30
-// extra VALU per window cost more than the saved home requests except at c5: c5 kernel
-// 3.088 -> 3.03 ms, c3 0.0815 -> 0.0888 ms, c2 0.0464 -> 0.0487 ms (ABAB, one box).
+// Minimizer ORDER (round 6; a table property, a bit of the layout code and of the kernels' M):
+// how a key picks the m-mer its home is a hash of. Consecutive windows of a protein share their
+// home line when they pick the same m-mer, so the order's density (the fraction of windows whose
+// pick differs from the previous window's) is the probe's home-line requests per window.
+//   random (default): the m-mer of smallest multiplicative hash; density 2/(w + 1) = 0.50 for
+//          K = 8, m = 6 (w = K - m + 1 = 3 m-mers per key).
+//   mod-sampling (kOrderMod; Groot Koerkamp & Pibiri, "The mod-minimizer", WABI 2024) with
+//          t = 3: x = the position of the smallest 3-mer hash among the key's K - 2 3-mers (ties:
+//          the first), the m-mer at x mod w is picked; density (2 + (m - t) / w) / (w + m - t + 1)
+//          = 3/7 = 0.43. Simulated on c5's 10^8-key table (scripts/order_sim.py): density 0.430
+//          vs 0.502, keys beyond a bucket's 8 slots 7.5% vs 6.1% (more keys in their alternate).
+//          Its ~20 more VALU per window cost the Infinity-Cache-resident configs more than they
+//          save (round 5's closed-syncmer order, density 0.454, cost c3 +9% and c2 +5% while it
+//          cut c5's kernel 1.9%: profiles/r05/syncmer_ab_r05s/), so it is a size rule: K = 8,
+//          m = 6 tables larger than the Infinity Cache (kma_abi.cpp minimizer_len).
+// The order bit rides in the minimizer length m of layout codes and kernel templates; the
+// minimizer length proper is m & kMinimizerMask.
+constexpr int kOrderMod = KMA_LAYOUT_MOD_SAMPLING;
+constexpr int kMinimizerMask = 0x3F;
+__host__ __device__ constexpr bool order_mod_valid(int k, int m) {
+  return k == 8 && (m & kMinimizerMask) == 6;  // the instantiated kernels (kma_device.h)
+}
+__host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {  // a, b < 2^24
+#ifdef __HIP_DEVICE_COMPILE__
+  return __umul24(a, b);
+#else
+  return a * b;
+#endif
+}
+// The picked m-mer's code itself is the minimizer value (home_from_min mixes it).
+__host__ __device__ inline uint32_t mod_sample(uint64_t key, int k, int m) {
+  const int nt = k - 2, w = k - m + 1;  // 3-mers of the key (<= 6: positions fit 3 bits)
+  uint32_t best = 0xFFFFFFFFu;
+  for (int i = 0; i < nt; ++i) {
+    const uint32_t t3 = (uint32_t)(key >> (5 * (nt - 1 - i))) & 0x7FFFu;
+    // an odd 24-bit multiplier: a bijection of the 15-bit 3-mer codes; position in the low bits
+    const uint32_t g = (mul24(t3, 0x9E3779u) & ~7u) | (uint32_t)i;
+    best = best < g ? best : g;
+  }
+  const int p = (int)(best & 7u) % w;
+  return (uint32_t)(key >> (5 * (k - m - p))) & (uint32_t)((1ull << (5 * m)) - 1);
+}
 __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
+  if (m & kOrderMod) return mod_sample(key, k, m & kMinimizerMask);
   const uint32_t mask = (uint32_t)((1ull << (5 * m)) - 1);
   uint32_t best = 0xFFFFFFFFu;
   for (int p = 0; p <= k - m; ++p) {

@@ -44,15 +44,18 @@ EXPORTS = (
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
 OPT_PACKED_INPUT, OPT_HOST_THREADS, OPT_HOST_SLICE, OPT_PLACEMENT = 6, 7, 8, 9
+OPT_HOST_PIECE_MIN = 10
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
                 OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0, OPT_HOST_SLICE: 0,
-                OPT_PLACEMENT: -1}
+                OPT_PLACEMENT: -1, OPT_HOST_PIECE_MIN: 0}
 LAYOUT_TWO_CHOICE = 0x100  # layout code flag: two-choice placement (include/kmeranno.h)
+LAYOUT_MOD_SAMPLING = 0x40  # layout code flag: the mod-sampling minimizer order (K = 8, m = 6)
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
 _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer": OPT_DEFER,
               "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
               "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS,
-              "host_slice": OPT_HOST_SLICE, "placement": OPT_PLACEMENT}
+              "host_slice": OPT_HOST_SLICE, "placement": OPT_PLACEMENT,
+              "host_piece_min": OPT_HOST_PIECE_MIN}
 
 
 class KmerAnnoError(RuntimeError):
@@ -68,7 +71,9 @@ class TableInfo(C.Structure):
                 ("extra_syms", C.c_uint8 * 4), ("minimizer_len", C.c_int32),
                 ("n_displaced", C.c_uint64), ("n_replicas", C.c_int32),
                 ("slots_per_bucket", C.c_int32), ("replicate_ms", C.c_double),
-                ("replicate_bytes", C.c_uint64), ("two_choice", C.c_int32), ("pad_", C.c_int32)]
+                ("replicate_bytes", C.c_uint64), ("two_choice", C.c_int32),
+                ("minimizer_order", C.c_int32), ("replicate_peer", C.c_int32),
+                ("replicate_local", C.c_int32)]
 
 
 HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
@@ -453,7 +458,7 @@ def choose_layout(k: int, n_buckets: int, build):
     if forced:
         return m, st
     m6, m7 = min(k, 6), min(k, 7)
-    if m == m6 and m6 != m7 and disp(st) > RETRY_DISPLACED:
+    if m & 0x3F == m6 and m6 != m7 and disp(st) > RETRY_DISPLACED:
         s2 = build(m7)
         if s2[3] < st[3]:
             m, st = m7, s2
@@ -506,6 +511,27 @@ def annotate_proteins_device(table: SignatureTable, ws: Workspace, d_residues: i
     _check(load().kma_annotate_proteins_device(table._h, ws._h, d_residues, d_offsets, n_seq,
                                                n_residues, min_hits, flags, d_fid, d_count,
                                                d_status, d_tally or None, n_fid, stream or None))
+
+
+HOST_PROFILE_FIELDS = ("setup_ms", "stage_ms", "launch_ms", "wait_ms", "outputs_ms", "call_ms",
+                       "staging_threads", "pieces")
+
+
+def host_profile(replica: int | None = None) -> dict:
+    """The library's host-side phase profile (measurement hook, not in kmeranno.h) of the last
+    host protein shard call, or of replica `replica`'s last shard of a fanned-out call."""
+    L = load()
+    p = (C.c_double * len(HOST_PROFILE_FIELDS))()
+    if replica is None:
+        _check(L.kma_debug_host_profile(p, len(p)))
+    else:
+        _check(L.kma_debug_host_profile_replica(replica, p, len(p)))
+    return dict(zip(HOST_PROFILE_FIELDS, list(p)))
+
+
+def host_cores() -> int:
+    """CPUs the library sizes its staging jobs by (affinity mask bounded by the cgroup quota)."""
+    return int(load().kma_debug_host_cores())
 
 
 def packed_bytes(n_residues: int) -> int:

@@ -1,0 +1,129 @@
+"""Host simulation of home-bucket orders for the protein probe (round 6).
+
+For a K = 8 table of T random 8-mers over the 20 standard amino acids at load factor 0.5 (c5:
+T = 10^8, 25M buckets, a minimizer picks a 128-byte pair of buckets and the key's parity the
+bucket), and for random query proteins of small.gto's CDS lengths, reports per order:
+  density  : fraction of probed windows whose home LINE (bucket pair) differs from the previous
+             window's in the same protein (the minimizer layout's line requests per window)
+  overflow : keys beyond 8 per bucket / T (the keys a two-choice build must place in their
+             alternate bucket at least; the build's evictions add to it)
+Orders (kma_internal.h minimizer_hash and its round-6 alternatives):
+  random   : smallest multiplicative hash of the K - m + 1 m-mers (the shipped order, m = 6)
+  syncmer  : closed syncmers first (an m-mer whose smallest 3-mer hash sits at its first or last
+             position), then by hash (round 5's measured variant)
+  mod      : mod-sampling (Groot Koerkamp & Pibiri 2024): x = position of the smallest 3-mer hash
+             among the key's K - 2 3-mers, the m-mer at x mod (K - m + 1) is the minimizer
+  m5       : random order with m = 5 (128-byte homes of a lower density)
+Usage: python scripts/order_sim.py [T] [n_proteins]
+"""
+import sys
+
+import numpy as np
+
+U32 = np.uint32
+M32 = np.uint64(0xFFFFFFFF)
+
+
+def mul32(a, c):
+    return ((a.astype(np.uint64) * np.uint64(c)) & M32).astype(U32)
+
+
+def mmer_hash(sub):
+    return mul32(sub, 0x9E3779B1)
+
+
+def mix32_lite(h):
+    h = h ^ (h >> U32(16))
+    h = mul32(h, 0x7FEB352D)
+    return h ^ (h >> U32(15))
+
+
+def sub_at(keys, k, m, p):
+    return ((keys >> np.uint64(5 * (k - m - p))) & np.uint64((1 << (5 * m)) - 1)).astype(U32)
+
+
+def order_value(keys, order, k=8):
+    if order in ("random", "m5"):
+        m = 6 if order == "random" else 5
+        v = np.full(len(keys), 0xFFFFFFFF, U32)
+        for p in range(k - m + 1):
+            v = np.minimum(v, mmer_hash(sub_at(keys, k, m, p)))
+        return v
+    m, s = 6, 3
+    g = [mmer_hash(sub_at(keys, k, s, i)) for i in range(k - s + 1)]  # 3-mer hashes
+    if order == "syncmer":
+        v = np.full(len(keys), 0xFFFFFFFF, U32)
+        for p in range(k - m + 1):
+            ends = np.minimum(g[p], g[p + m - s])
+            mids = np.minimum.reduce([g[p + i] for i in range(1, m - s)])
+            closed = ends <= mids
+            h = mmer_hash(sub_at(keys, k, m, p)) >> U32(1)
+            v = np.minimum(v, np.where(closed, h, h | U32(0x80000000)))
+        return v
+    if order == "mod":  # kma_internal.h mod_sample, exactly
+        w = k - m + 1
+        best = np.full(len(keys), 0xFFFFFFFF, U32)
+        for i in range(k - s + 1):
+            t3 = sub_at(keys, k, s, i)
+            best = np.minimum(best, (mul32(t3, 0x9E3779) & U32(0xFFFFFFF8)) | U32(i))
+        p = ((best & U32(7)) % U32(w)).astype(np.uint64)
+        return ((keys >> (np.uint64(5) * (np.uint64(k - m) - p)))
+                & np.uint64((1 << (5 * m)) - 1)).astype(U32)
+    raise ValueError(order)
+
+
+def pair_of(v, nb):
+    return ((mix32_lite(v ^ U32(0x85EBCA77)).astype(np.uint64) * np.uint64(nb >> 1)) >> np.uint64(32))
+
+
+def parity(keys):
+    x = (keys & M32).astype(np.uint64)
+    c = np.zeros(len(keys), np.uint64)
+    while True:
+        nz = x != 0
+        if not nz.any():
+            break
+        c[nz] ^= np.uint64(1)
+        x &= x - np.uint64(1)
+    return c
+
+
+def random_kmers(rng, n, k=8):
+    key = np.zeros(n, np.uint64)
+    codes = (np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8).astype(np.uint64) - 64)
+    for _ in range(k):
+        key = (key << np.uint64(5)) | codes[rng.integers(0, 20, n)]
+    return key
+
+
+def main():
+    T = int(float(sys.argv[1])) if len(sys.argv) > 1 else 100_000_000
+    n_prot = int(sys.argv[2]) if len(sys.argv) > 2 else 20_000
+    nb = (T + 3) // 4  # 8 slots, load factor 0.5
+    nb += nb & 1
+    rng = np.random.default_rng(5)
+    sys.path.insert(0, "kmers.anno_amd/python")
+    from kmeranno import synth
+    lens = rng.choice(synth.cds_lengths(), n_prot)
+    aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+    qkeys = [synth.window_keys(aa[rng.integers(0, 20, int(L))]) for L in lens]
+    for order in ("random", "syncmer", "mod", "m5"):
+        counts = np.zeros(nb, np.int64)
+        chunk = 10_000_000
+        krng = np.random.default_rng(55)
+        for a in range(0, T, chunk):
+            keys = random_kmers(krng, min(chunk, T - a))
+            b = 2 * pair_of(order_value(keys, order), nb) + parity(keys)
+            counts += np.bincount(b.astype(np.int64), minlength=nb)
+        over = np.maximum(counts - 8, 0).sum() / T
+        changes = windows = 0
+        for q in qkeys:
+            pr = pair_of(order_value(q, order), nb)
+            changes += 1 + int((pr[1:] != pr[:-1]).sum())
+            windows += len(pr)
+        print(f"{order:8s} density {changes / windows:.4f}  overflow {over:.4f}  "
+              f"max keys per bucket {counts.max()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

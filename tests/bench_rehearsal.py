@@ -137,7 +137,8 @@ class _Info:
         self.n_buckets = nb
         self.bytes = nb * 8 * 8
         self.device = 0 if device is None else device
-        self.minimizer_len = m & 0xFF
+        self.minimizer_len = m & 0x3F
+        self.minimizer_order = 1 if m & 0x40 else 0
         self.two_choice = 1 if m & 0x100 else 0
         self.k = K
 
@@ -183,6 +184,7 @@ class StubKmerAnno(types.ModuleType):
     OPT_PACKED_INPUT = 6
     OPT_PLACEMENT = 9
     LAYOUT_TWO_CHOICE = 0x100
+    LAYOUT_MOD_SAMPLING = 0x40
     HIT_DTYPE = np.dtype([("contig", "<u4"), ("left", "<i4"), ("fid", "<u4"), ("strand", "u1"),
                           ("frame", "u1"), ("pad", "<u2")])
 

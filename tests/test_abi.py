@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(native_lib):
 
 
 def test_abi_version_and_error_string(native_lib):
-    assert native_lib.kma_abi_version() == 6
+    assert native_lib.kma_abi_version() == 7
     assert isinstance(native_lib.kma_last_error(), bytes)
 
 
@@ -40,15 +40,21 @@ def test_options_set_get_validate_restore(native_lib):
     for o, bad in ((k.OPT_LAYOUT, 5), (k.OPT_BLOCK_PROTEINS, 9), (k.OPT_DEFER, 65),
                    (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 3),
                    (k.OPT_HOST_THREADS, 65), (k.OPT_HOST_SLICE, -1), (k.OPT_PLACEMENT, 2),
+                   (k.OPT_HOST_SLICE, 1 << 32), (k.OPT_HOST_PIECE_MIN, -1), (k.OPT_LAYOUT, 7 | 0x40),
                    (99, 0)):
         with pytest.raises(k.KmerAnnoError) as e:
             k.set_option(o, bad)
         assert e.value.code == k.E_INVALID
+    with k.options(layout=6 | k.LAYOUT_MOD_SAMPLING):
+        assert k.layout_for(8, 1000) == 6 | k.LAYOUT_MOD_SAMPLING | k.LAYOUT_TWO_CHOICE
+        assert k.layout_for(7, 1000) == 6 | k.LAYOUT_TWO_CHOICE  # mod-sampling: K = 8 only
     with k.options(layout=7, block_proteins=1, defer=0, host_pieces=3, hash_slice=1000,
-                   packed_input=0, host_threads=4, host_slice=12345, placement=0):
-        assert [k.get_option(o) for o in range(1, 10)] == [7, 1, 0, 3, 1000, 0, 4, 12345, 0]
+                   packed_input=0, host_threads=4, host_slice=12345, placement=0,
+                   host_piece_min=1 << 20):
+        assert [k.get_option(o) for o in range(1, 11)] == [7, 1, 0, 3, 1000, 0, 4, 12345, 0,
+                                                           1 << 20]
         assert k.layout_for(8, 1000) == 7
-    assert [k.get_option(o) for o in range(1, 10)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1]
+    assert [k.get_option(o) for o in range(1, 11)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1, 0]
     assert k.layout_for(8, 1000) == 6 | k.LAYOUT_TWO_CHOICE
     src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
     assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src
@@ -81,19 +87,26 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
 
 def test_table_layout_host_helper(native_lib, monkeypatch):
     """Layout choice: minimizer m = 6 up to 134M keys at load factor 0.5 (2^28 slots), m = 7
-    beyond; the KMA_OPT_LAYOUT option forces 0 (flat), 6 or 7, read per call. Narrow tables are
-    tried with two-choice placement first (the layout code's flag) unless KMA_OPT_PLACEMENT = 0;
-    wide tables never."""
+    beyond; K = 8, m = 6 tables larger than the 256 MiB Infinity Cache in the mod-sampling order
+    (c5's 10^8 keys; c2 / c4's 10^7 stay in the random order); the KMA_OPT_LAYOUT option forces
+    0 (flat), 6, 7 or 6 | mod-sampling, read per call. Narrow tables are tried with two-choice
+    placement first (the layout code's flag) unless KMA_OPT_PLACEMENT = 0; wide tables never."""
     import kmeranno
-    tc = kmeranno.LAYOUT_TWO_CHOICE
+    tc, mod = kmeranno.LAYOUT_TWO_CHOICE, kmeranno.LAYOUT_MOD_SAMPLING
     kmeranno.set_option(kmeranno.OPT_LAYOUT, -1)
     nb6 = (1 << 28) // kmeranno.bucket_slots()
-    assert kmeranno.layout_for(8, nb6) == 6 | tc
+    cache = (256 << 20) // (8 * kmeranno.bucket_slots())  # buckets of the Infinity Cache
+    assert kmeranno.layout_for(8, nb6) == 6 | mod | tc
+    assert kmeranno.layout_for(8, cache + 1) == 6 | mod | tc
+    assert kmeranno.layout_for(8, cache) == 6 | tc
+    assert kmeranno.layout_for(8, kmeranno.buckets_for(10**7)) == 6 | tc  # c2 / c4
+    assert kmeranno.layout_for(8, kmeranno.buckets_for(10**8)) == 6 | mod | tc  # c5
+    assert kmeranno.layout_for(7, nb6) == 6 | tc  # mod-sampling: K = 8 only
     assert kmeranno.layout_for(8, nb6 + 1) == 7 | tc
     assert kmeranno.layout_for(5, 1 << 30) == 5 | tc  # m <= K
     assert kmeranno.layout_for(10, 1000) == 6  # wide: chains
     with kmeranno.options(placement=0):
-        assert kmeranno.layout_for(8, nb6) == 6
+        assert kmeranno.layout_for(8, nb6) == 6 | mod
     kmeranno.set_option(kmeranno.OPT_LAYOUT, 0)
     assert kmeranno.layout_for(8, 1000) == 0 | tc
     kmeranno.set_option(kmeranno.OPT_LAYOUT, 7)
@@ -111,13 +124,15 @@ def test_choose_layout_rule():
     import kmeranno
     tc = kmeranno.LAYOUT_TWO_CHOICE
     n = 99_821_868
+    six = 6 | kmeranno.LAYOUT_MOD_SAMPLING  # the size rule's m = 6 code at c5 (round 6)
+    assert kmeranno.layout_for(8, 25_000_000) == six | tc
     sweep = {  # load factor -> layout -> status
-        0.5: {6: [0, n, 10, int(0.0770 * n)], 7: [0, n, 7, int(0.0239 * n)], 0: [0, n, 6, int(0.0086 * n)]},
-        0.75: {6: [0, n, 24, int(0.1706 * n)], 7: [0, n, 19, int(0.0936 * n)], 0: [0, n, 17, int(0.0607 * n)]},
-        0.9: {6: [0, n, 47, int(0.2449 * n)], 7: [0, n, 39, int(0.1675 * n)], 0: [0, n, 38, int(0.1309 * n)]},
-        "adv": {6: [0, 1506982, 290, 1490000], 7: [0, 1506982, 145, 1012000], 0: [0, 1506982, 5, 13000]},
+        0.5: {six: [0, n, 10, int(0.0770 * n)], 7: [0, n, 7, int(0.0239 * n)], 0: [0, n, 6, int(0.0086 * n)]},
+        0.75: {six: [0, n, 24, int(0.1706 * n)], 7: [0, n, 19, int(0.0936 * n)], 0: [0, n, 17, int(0.0607 * n)]},
+        0.9: {six: [0, n, 47, int(0.2449 * n)], 7: [0, n, 39, int(0.1675 * n)], 0: [0, n, 38, int(0.1309 * n)]},
+        "adv": {six: [0, 1506982, 290, 1490000], 7: [0, 1506982, 145, 1012000], 0: [0, 1506982, 5, 13000]},
     }
-    want = {0.5: 6, 0.75: 7, 0.9: 7, "adv": 0}
+    want = {0.5: six, 0.75: 7, 0.9: 7, "adv": 0}
     for case, st in sweep.items():
         built = []
 
@@ -125,12 +140,12 @@ def test_choose_layout_rule():
             built.append(m)
             return [1, 0, 0, 0] if m & tc else st[m]  # the two-choice build fails
         m, s = kmeranno.choose_layout(8, 25_000_000, build)
-        assert built[0] == 6 | tc
+        assert built[0] == six | tc
         assert m == want[case] and built[-1] == m and s == st[m], (case, built)
-    two = {6 | tc: [0, n, 2, int(0.21 * n)], tc: [0, n, 2, int(0.05 * n)]}
-    for disp6, expect in ((0.21, 6 | tc), (0.45, tc), (0.45 - 1, 6 | tc)):
+    two = {six | tc: [0, n, 2, int(0.21 * n)], tc: [0, n, 2, int(0.05 * n)]}
+    for disp6, expect in ((0.21, six | tc), (0.45, tc), (0.45 - 1, six | tc)):
         built = []
-        two[6 | tc][3] = int(disp6 * n) if disp6 > 0 else int(0.45 * n)
+        two[six | tc][3] = int(disp6 * n) if disp6 > 0 else int(0.45 * n)
         if disp6 < 0:  # crowded, but flat does not halve the displaced keys
             two[tc][3] = int(0.30 * n)
 
@@ -145,9 +160,9 @@ def test_choose_layout_rule():
 
     def build3(m):
         built.append(m)
-        return [1, 0, 0, 0] if m == 6 | tc else [0, n, 2, int(0.12 * n)]
+        return [1, 0, 0, 0] if m == six | tc else [0, n, 2, int(0.12 * n)]
     m, s = kmeranno.choose_layout(8, 25_000_000, build3)
-    assert m == tc and built == [6 | tc, tc] and s[0] == 0
+    assert m == tc and built == [six | tc, tc] and s[0] == 0
 
 
 def _pack_reference(res: np.ndarray) -> np.ndarray:
@@ -226,3 +241,42 @@ def test_pack_residues_host_matches_bitwise_reference(native_lib, n):
     want = _pack_reference(res)
     assert len(got) == kmeranno.packed_bytes(n) == 40 * ((n + 63) // 64) + 16
     assert (got[:len(want)] == want).all() and not got[len(want):].any()
+
+
+@pytest.mark.parametrize("k,code,ok", [
+    (8, 6, True), (8, 7, True), (8, 0, True), (8, 6 | 0x40, True), (8, 6 | 0x40 | 0x100, True),
+    (8, -1, True), (7, 6 | 0x40, False), (8, 7 | 0x40, False), (8, 5, False), (8, 0x200, False),
+    (10, 6 | 0x100, False), (10, 6, True), (8, 0x80 | 6, False)])
+def test_layout_code_validation(native_lib, k, code, ok):
+    """kma_table_wrap_device checks its layout code before it touches a device: minimizer
+    0 / min(K, 6) / min(K, 7), the mod-sampling order only at K = 8, m = 6, two-choice only for
+    K <= 8, no unknown bits (KMA_E_INVALID); a valid code gets as far as the device (KMA_E_DEVICE
+    here, no GPU). -1 resolves to kma_table_layout_for's code (build and wrap agree)."""
+    import ctypes as C
+    import kmeranno
+    h = C.c_void_p()
+    rc = kmeranno.load().kma_table_wrap_device(C.c_void_p(4096), 1000, k, code, 0, C.byref(h))
+    if ok:
+        assert rc in (kmeranno.E_DEVICE, kmeranno.OK)
+        if rc == kmeranno.OK:
+            kmeranno.load().kma_table_destroy(h)
+    else:
+        assert rc == kmeranno.E_INVALID
+
+
+def test_host_cores_bounded_by_cgroup_quota(native_lib):
+    """The library sizes its staging jobs by the process's CPUs: the affinity mask, bounded by a
+    cgroup CPU quota when one is set (a GPU box grants a share of a machine whose every CPU the
+    mask lists)."""
+    import kmeranno
+    n = kmeranno.host_cores()
+    assert 1 <= n <= len(os.sched_getaffinity(0))
+    quota = None
+    if os.path.exists("/sys/fs/cgroup/cpu.max"):
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else -(-int(q) // int(p))
+    elif os.path.exists("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        quota = -(-q // p) if q > 0 else None
+    assert n == min(len(os.sched_getaffinity(0)), quota or 1 << 30)

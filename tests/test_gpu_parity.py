@@ -21,17 +21,20 @@ pytestmark = pytest.mark.gpu
 K = 8
 
 
-@pytest.fixture(params=["auto", "7", "0", "chained"], ids=["m-auto", "m7", "flat", "chained"])
+@pytest.fixture(params=["auto", "7", "0", "chained", "mod"],
+                ids=["m-auto", "m7", "flat", "chained", "m6-mod"])
 def layout(request, monkeypatch):
     """Table layouts: the size-derived minimizer layout (m = 6 up to 134M keys at load factor
-    0.5, c5 included), the m = 7 layout of larger tables, and the flat fallback (the KMA_OPT_LAYOUT
-    option, read per table creation), each with the default two-choice placement; and the
-    size-derived layout with overflow chains (KMA_OPT_PLACEMENT = 0: the placement of wide
-    tables and of a two-choice build that fails)."""
+    0.5), the m = 7 layout of larger tables, the flat fallback, and m = 6 in the mod-sampling
+    order (round 6: the size rule's choice for K = 8 tables beyond the Infinity Cache, c5; forced
+    here on small tables) (the KMA_OPT_LAYOUT option, read per table creation), each with the
+    default two-choice placement; and the size-derived layout with overflow chains
+    (KMA_OPT_PLACEMENT = 0: the placement of wide tables and of a two-choice build that fails)."""
     import kmeranno
     kmeranno.load()
     p = request.param
-    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1 if p in ("auto", "chained") else int(p))
+    code = {"auto": -1, "chained": -1, "mod": 6 | kmeranno.LAYOUT_MOD_SAMPLING}.get(p)
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, int(p) if code is None else code)
     kmeranno.set_option(kmeranno.OPT_PLACEMENT, 0 if p == "chained" else -1)
     return p
 
@@ -167,6 +170,8 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags, input_mode)
         assert t.info.n_entries == ot.size
         if layout in ("7", "0"):
             assert t.info.minimizer_len == int(layout)
+        elif layout == "mod" and lf == 0.5:
+            assert t.info.minimizer_len == 6 and t.info.minimizer_order == 1
         elif lf == 0.5:
             assert t.info.minimizer_len == 6  # size rule, few displaced keys
         if lf <= 0.9:
@@ -276,22 +281,27 @@ def test_adversarial_minimizer_keys_fall_back_flat(kma, oracle_c, path):
 
 
 def test_replicated_table_host_fan_out(kma, oracle_c, path):
-    """A table with two replicas (both on device 0 here: two host threads and streams, the
-    same code path as two GPUs) shards a host call by residues; outputs and the summed tally
-    equal the single-replica call. On a multi-GPU box, replicas on devices 0 and 1 too."""
+    """A table with 2 and 8 replicas (all on device 0 here: a host thread and stream per
+    replica, the same code path as 8 GPUs) shards a host call by residues; outputs and the
+    summed tally equal the single-replica call. Each replica's staging jobs get host_cores() / n
+    threads (at most 16); the copies report as same-device ones. On a multi-GPU box, replicas on
+    devices 0 and 1 too (peer copies)."""
     from kmeranno import synth
     wl = synth.make_workload(3000, 100_000, 500, seed=29)
     kmers = [synth.unpack_key(x) for x in wl.keys]
     with kma.SignatureTable.from_rows(kmers, wl.fids, K) as t1:
         ref = kma.annotate_proteins(t1, wl.residues, wl.offsets, 5, 0, n_fid=500)
-    devsets = [[0, 0]] + ([[0, 1], [1, 0, 1]] if kma.device_count() > 1 else [])
+    devsets = [[0, 0], [0] * 8] + ([[0, 1], [1, 0, 1]] if kma.device_count() > 1 else [])
     for devs in devsets:
         with kma.SignatureTable.from_rows_replicated(kmers, wl.fids, devs, K) as t:
             assert t.replicas == devs and t.info.n_replicas == len(devs)
+            assert t.info.replicate_local == sum(d == devs[0] for d in devs[1:])
             for _ in range(2):  # second call reuses the pooled host contexts
                 got = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0, n_fid=500)
                 for a, b in zip(got, ref):
                     assert (a == b).all()
+            want = max(1, min(16, kma.host_cores() // len(devs)))
+            assert all(kma.host_profile(i)["staging_threads"] == want for i in range(len(devs)))
     ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
     assert (ref[2] == est).all() and (ref[0] == efid).all() and (ref[1] == ecnt).all()
@@ -373,21 +383,32 @@ def test_config2_size_vs_oracle(kma, oracle_c, path, monkeypatch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("opts", [{}, {"host_pieces": 16, "host_threads": 1},
-                                  {"host_pieces": 3, "host_threads": 3}, {"packed_input": 0}],
-                         ids=["default", "16pieces-1thread", "3pieces-3threads", "ascii"])
-def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c, opts):
+@pytest.mark.parametrize("opts,pieces", [
+    ({}, 2), ({"host_pieces": 16, "host_threads": 1, "host_piece_min": 1 << 20}, 16),
+    ({"host_pieces": 3, "host_threads": 3, "host_piece_min": 1 << 20}, 3),
+    ({"packed_input": 0}, 2), ({"packed_input": 0, "host_piece_min": 1 << 20}, 8),
+    ({"packed_input": 0, "host_pieces": 5, "host_piece_min": 1 << 20}, 5)],
+    ids=["default", "16pieces-1thread", "3pieces-3threads", "ascii", "ascii-8pieces",
+         "ascii-5pieces"])
+def test_host_call_pipelined_pieces_vs_oracle(kma, oracle_c, opts, pieces):
     """A host call of ~48M residues runs as 2-16 pieces whose H2D overlaps the previous
     piece's kernel (kma_abi.cpp protein_shard): packed input streamed out in segments as the
     staging pool packs it (the calling thread alone with one staging thread), ASCII input piece
-    by piece: every protein, including those next to piece and segment boundaries, and the
-    tally (summed over the pieces' launches) equal the oracle's."""
+    by piece (uneven pieces, weights 1, 2, 4, ..., 4, 2, 1, at 4 pieces and more): every protein,
+    including those next to piece and segment boundaries, and the tally (summed over the pieces'
+    launches) equal the oracle's. KMA_OPT_HOST_PIECE_MIN lowers the 16 MiB piece floor so that a
+    48M-residue call runs the asked pieces; the library's host profile reports the count it ran
+    (the piece cases used to run 2 pieces each)."""
     from kmeranno import synth
     sig = synth.make_table(1_000_000, 2000, 41, K)
     res, off, _, _ = synth.make_queries(sig, 160_000, 41 * 1_000_003 + 17)
     assert off[-1] >= 2 * (16 << 20)  # at least two pieces
     with _config_table(kma, sig) as t, kma.options(**opts):
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=2000)
+        prof = kma.host_profile()
+    assert prof["pieces"] == pieces, prof
+    if "host_threads" in opts:
+        assert prof["staging_threads"] == opts["host_threads"]
     ot = restricted_oracle_table(oracle_c, sig.keys, sig.fids, res)
     efid, ecnt, est = oracle_c.apply_mt(ot, res, off, K, 5, 0, threads=8)
     assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
