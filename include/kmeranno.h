@@ -58,6 +58,7 @@ extern "C" {
 #define KMA_E_CAPACITY (-4)    /* an output buffer is too small; *needed count is reported    */
 #define KMA_E_ALPHABET (-5)    /* the table needs more than 4 non-[A-Z*] symbols               */
 #define KMA_E_TABLE_FULL (-6)  /* probe chain exhausted during build (load factor too high)    */
+#define KMA_E_IO (-7)          /* ABI 7: an input file cannot be opened or read (IOException)   */
 
 /* ---- per-protein call status (out_status) -------------------------------------------------
  * Mirrors the three outcomes of ApplyKmerProcessor.java:129-147 plus the reporting threshold:
@@ -222,6 +223,19 @@ int kma_pack_kmers(const kma_table* table, const char* text, const uint64_t* off
  * load_factor <= 0 selects the default 0.5.                                                   */
 int kma_table_create(const char* text, const uint64_t* offsets, const uint32_t* fids, uint64_t n,
                      int k, int device, double load_factor, kma_table** out);
+/* From apply's kmerdb.tbl itself (ABI 7; ApplyKmerProcessor.java:100-108, whose loop reads the
+ * file row by row into a HashMap<String,String>): the headerless tab-separated file (kmer in
+ * column 0, role id in column 1; TabbedLineReader(file, 2)) is mapped and parsed on the host's
+ * cores; a row's role becomes a dense fid in first-seen row order; then as
+ * kma_table_create_replicated on device_ids[0 .. n_devices) (last row of a kmer wins, rows not
+ * of length K never match). Outputs (each optional): *role_names = the role ids in fid order,
+ * each followed by a NUL byte, in one buffer of *role_bytes bytes that the caller releases with
+ * kma_free; *n_roles; *last_kmer_len = the last row's kmer length (what :108 passes to
+ * KmerReference.setKmerSize). KMA_E_IO if the file cannot be opened or mapped.                */
+int kma_table_create_from_tsv(const char* path, int k, int n_devices, const int* device_ids,
+                              double load_factor, kma_table** out, char** role_names,
+                              uint64_t* role_bytes, uint32_t* n_roles, int* last_kmer_len);
+void kma_free(void* p);
 /* Same from pre-packed keys (standard alphabet only; key 0 rows are skipped).               */
 int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t n, int k,
                             int device, double load_factor, kma_table** out);

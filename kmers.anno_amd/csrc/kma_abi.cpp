@@ -32,6 +32,7 @@
 #include "kma_hashanno.h"
 #include "kma_internal.h"
 #include "kma_pack.h"
+#include "kma_tsv.h"
 
 namespace {
 // ---- options (kma_option_set; include/kmeranno.h) ----------------------------------------------
@@ -1072,6 +1073,64 @@ int kma_table_create(const char* text, const uint64_t* offsets, const uint32_t* 
   for (uint64_t r = 0; r < n; ++r) skipped += offsets[r + 1] - offsets[r] != (uint64_t)k;
   return create_from_keys(keys, fids, n, k, device, load_factor, lut, skipped, out);
 }
+
+int kma_table_create_from_tsv(const char* path, int k, int n_devices, const int* device_ids,
+                              double load_factor, kma_table** out, char** role_names,
+                              uint64_t* role_bytes, uint32_t* n_roles, int* last_kmer_len) {
+  if (!path || !out || n_devices < 1 || !device_ids) return fail(KMA_E_INVALID, "null argument");
+  *out = nullptr;
+  if (role_names) *role_names = nullptr;
+  if (int rc = check_k(k)) return rc;
+  // the alphabet rule of kma_table_create: A-Z and '*', then up to four other bytes of K-length
+  // kmers in byte order
+  auto make_lut = [](const bool* seen, uint8_t* lut) {
+    standard_lut(lut);
+    int extra = 0;
+    for (int c = 0; c < 256; ++c)
+      if (seen[c] && !lut[c]) {
+        if (extra == 4) return KMA_E_ALPHABET;
+        lut[c] = (uint8_t)(28 + extra++);
+      }
+    return KMA_OK;
+  };
+  kma::KmerTsv tsv;
+  std::string err;
+  if (int rc = kma::read_kmer_tsv(path, k, (unsigned)std::min<size_t>(16, host_cores()), make_lut,
+                                  &tsv, &err))
+    return fail(rc, "%s", err.c_str());
+  kma_table* t = nullptr;
+  if (int rc = create_from_keys(tsv.keys, tsv.fids.data(), tsv.keys.size(), k, device_ids[0],
+                                load_factor, tsv.lut, tsv.n_skipped, &t))
+    return rc;
+  if (n_devices > 1)
+    if (int rc = kma_table_replicate(t, n_devices - 1, device_ids + 1)) {
+      free_table(t);
+      return rc;
+    }
+  uint64_t bytes = 0;
+  for (const std::string& r : tsv.roles) bytes += r.size() + 1;
+  if (role_names) {
+    char* blob = static_cast<char*>(malloc(std::max<uint64_t>(bytes, 1)));
+    if (!blob) {
+      free_table(t);
+      return fail(KMA_E_NOMEM, "role names: %llu bytes", (unsigned long long)bytes);
+    }
+    char* p = blob;
+    for (const std::string& r : tsv.roles) {
+      std::memcpy(p, r.data(), r.size());
+      p += r.size();
+      *p++ = '\0';
+    }
+    *role_names = blob;
+  }
+  if (role_bytes) *role_bytes = bytes;
+  if (n_roles) *n_roles = (uint32_t)tsv.roles.size();
+  if (last_kmer_len) *last_kmer_len = tsv.last_kmer_len;
+  *out = t;
+  return KMA_OK;
+}
+
+void kma_free(void* p) { free(p); }
 
 int kma_table_create_packed(const uint64_t* keys, const uint32_t* fids, uint64_t n, int k,
                             int device, double load_factor, kma_table** out) {

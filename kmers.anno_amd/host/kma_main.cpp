@@ -398,13 +398,22 @@ class ApplyKmerProcessor {
     reporter_->initReport(goodRoleFile_);
     log_info("Loading kmer database from %s.", kmerDbFile_.c_str());
     const auto t0 = Clock::now();
-    db_ = read_kmer_db(kmerDbFile_);
+    // The library reads kmerdb.tbl itself (kma_table_create_from_tsv: the file mapped and parsed
+    // on the host's cores into packed keys and first-seen role ids), as a JNI caller would.
     // KmerReference.setKmerSize(lastKmer.length()) (:108) only affects the 6-frame code; the
     // protein extractor (ProteinKmers) keeps its own K = 8, so the table is built for K = 8.
-    log_info("Kmer size is %zu.", db_.last_kmer.size());
-    check(kma_table_create(db_.text.data(), db_.offsets.data(), db_.fids.data(), db_.fids.size(),
-                           kProteinK, device_, 0.0, &table_),
-          "kma_table_create");
+    char* names = nullptr;
+    uint64_t names_bytes = 0;
+    uint32_t n_roles = 0;
+    int last_len = 0;
+    check(kma_table_create_from_tsv(kmerDbFile_.c_str(), kProteinK, 1, &device_, 0.0, &table_,
+                                    &names, &names_bytes, &n_roles, &last_len),
+          "kma_table_create_from_tsv");
+    roles_.clear();
+    roles_.reserve(n_roles);
+    for (uint64_t o = 0; o < names_bytes; o += roles_.back().size() + 1) roles_.emplace_back(names + o);
+    kma_free(names);
+    log_info("Kmer size is %d.", last_len);
     tableLoadS_ = seconds(t0);
     kma_table_info info;
     kma_table_info_get(table_, &info);
@@ -543,7 +552,7 @@ class ApplyKmerProcessor {
       reporter_->openGenome(genome);
       for (size_t j = 0; j < pg.pegs.size(); ++j)
         if (pg.status[j] == KMA_STATUS_CALLED)  // role != null && !badPeg && count >= minHits
-          reporter_->recordFeature(*pg.pegs[j], (uint32_t)pg.fid[j], db_.roles[pg.fid[j]],
+          reporter_->recordFeature(*pg.pegs[j], (uint32_t)pg.fid[j], roles_[pg.fid[j]],
                                    pg.count[j]);
       reporter_->closeGenome();
       n_prot += pg.pegs.size();
@@ -702,7 +711,7 @@ class ApplyKmerProcessor {
         } else {
           for (uint32_t j = 0; j < n; ++j)
             if (s.out.status[j] == KMA_STATUS_CALLED)
-              reporter_->recordFeature(dummy, (uint32_t)s.out.fid[j], db_.roles[s.out.fid[j]],
+              reporter_->recordFeature(dummy, (uint32_t)s.out.fid[j], roles_[s.out.fid[j]],
                                        s.out.count[j]);
         }
         for (uint32_t j = 0; j < n; ++j) n_called += s.out.status[j] == KMA_STATUS_CALLED;
@@ -749,7 +758,7 @@ class ApplyKmerProcessor {
       t += '\t';
       t += s.recs.ids[j];
       t += '\t';
-      t += db_.roles[s.out.fid[j]];
+      t += roles_[s.out.fid[j]];
       t += '\t';
       t.append(num, (size_t)std::snprintf(num, sizeof num, "%d", s.out.count[j]));
       t += '\t';
@@ -799,7 +808,7 @@ class ApplyKmerProcessor {
   const bool fasta_;
   std::vector<std::string> fastaInputs_, fastaFiles_;
   std::unique_ptr<ApplyKmerReporter> reporter_;
-  KmerRows db_;
+  std::vector<std::string> roles_;  // fid -> role id (kmerdb.tbl's first-seen order)
   kma_table* table_ = nullptr;
 };
 

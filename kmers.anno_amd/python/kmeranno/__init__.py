@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("KMERANNO_LIB") or os.path.join(PKG_ROOT, "build", "li
 
 OK = 0
 E_INVALID, E_DEVICE, E_NOMEM, E_CAPACITY, E_ALPHABET, E_TABLE_FULL = -1, -2, -3, -4, -5, -6
+E_IO = -7
 STATUS_NONE, STATUS_CALLED, STATUS_AMBIGUOUS, STATUS_BELOW_MIN = 0, 1, 2, 3
 F_END_EXCLUSIVE, F_MULTISET = 0x1, 0x2
 MAX_K = 12  # K <= 8: narrow tables (8-byte slots); 9..12: wide tables (16-byte slots)
@@ -39,6 +40,7 @@ EXPORTS = (
     "kma_hash_annotate", "kma_bucket_slots_for", "kma_table_buckets_for_k",
     "kma_option_set", "kma_option_get", "kma_workspace_option_set",
     "kma_packed_bytes", "kma_pack_residues", "kma_annotate_packed_device",
+    "kma_table_create_from_tsv", "kma_free",
 )
 
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
@@ -123,6 +125,11 @@ def load(path: str | None = None):
         L.kma_table_create_replicated.argtypes = [C.c_char_p, _u64p, _u32p, _u64, _int, _int,
                                                   _i32p, C.c_double, C.POINTER(_vp)]
         L.kma_table_replicate.argtypes = [_vp, _int, _i32p]
+        L.kma_table_create_from_tsv.argtypes = [C.c_char_p, _int, _int, _i32p, C.c_double,
+                                                C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_u64),
+                                                C.POINTER(_u32), C.POINTER(_int)]
+        L.kma_free.argtypes = [_vp]
+        L.kma_free.restype = None
         L.kma_table_replicas.argtypes = [_vp, C.POINTER(_int), _vp, _int]
         L.kma_table_device_ptr.argtypes = [_vp, C.POINTER(_vp), C.POINTER(_u64)]
         L.kma_workspace_create.argtypes = [_int, C.POINTER(_vp)]
@@ -297,6 +304,23 @@ class SignatureTable:
                                                   len(off) - 1, k, len(dv), dv, load_factor,
                                                   C.byref(h)))
         return cls(h)
+
+    @classmethod
+    def from_tsv(cls, path: str, k: int = 8, devices=(0,), load_factor: float = 0.5):
+        """The table of apply's kmerdb.tbl read by the library (kma_table_create_from_tsv):
+        returns (table, role ids in fid order, the last row's kmer length)."""
+        dv = np.ascontiguousarray(devices, np.int32)
+        h, names, nb, nr, last = _vp(), _vp(), _u64(), _u32(), _int()
+        _check(load().kma_table_create_from_tsv(os.fsencode(path), k, len(dv), dv, load_factor,
+                                                C.byref(h), C.byref(names), C.byref(nb),
+                                                C.byref(nr), C.byref(last)))
+        try:
+            blob = C.string_at(names.value, nb.value) if nb.value else b""
+        finally:
+            load().kma_free(names)
+        roles = [r.decode() for r in blob.split(b"\0")[:-1]] if blob else []
+        assert len(roles) == nr.value
+        return cls(h), roles, last.value
 
     @classmethod
     def wrap_device(cls, d_slots: int, n_buckets: int, k: int = 8, device: int = 0,

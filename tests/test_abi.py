@@ -280,3 +280,21 @@ def test_host_cores_bounded_by_cgroup_quota(native_lib):
         p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
         quota = -(-q // p) if q > 0 else None
     assert n == min(len(os.sched_getaffinity(0)), quota or 1 << 30)
+
+
+def test_table_from_tsv_host_errors(native_lib, tmp_path):
+    """kma_table_create_from_tsv reads the file before any device work: a missing file is
+    KMA_E_IO (apply's FileNotFoundException), more than 4 symbols outside [A-Z*] in K-length
+    kmers KMA_E_ALPHABET (kma_table_create's rule), a bad K KMA_E_INVALID."""
+    import kmeranno
+    with pytest.raises(kmeranno.KmerAnnoError) as e:
+        kmeranno.SignatureTable.from_tsv(str(tmp_path / "missing.tbl"))
+    assert e.value.code == kmeranno.E_IO
+    bad = tmp_path / "alpha.tbl"
+    bad.write_text("".join(f"AAAAAAA{c}\tR{i}\n" for i, c in enumerate("abcde")))
+    with pytest.raises(kmeranno.KmerAnnoError) as e:
+        kmeranno.SignatureTable.from_tsv(str(bad))
+    assert e.value.code == kmeranno.E_ALPHABET
+    with pytest.raises(kmeranno.KmerAnnoError) as e:
+        kmeranno.SignatureTable.from_tsv(str(bad), k=13)
+    assert e.value.code == kmeranno.E_INVALID

@@ -102,6 +102,68 @@ def test_edge_cases_golden(kma, layout, path, input_mode):
         assert got == c["expected"], c["name"]
 
 
+def _write_tsv(path, rows, crlf=False, trailing_newline=True):
+    eol = "\r\n" if crlf else "\n"
+    text = eol.join(k if r is None else f"{k}\t{r}" for k, r in rows)
+    path.write_bytes((text + (eol if trailing_newline and rows else "")).encode())
+
+
+@pytest.mark.parametrize("crlf,trailing", [(False, True), (True, True), (False, False)])
+def test_table_from_tsv_edge_golden(kma, tmp_path, crlf, trailing):
+    """kma_table_create_from_tsv (the library reads kmerdb.tbl itself, ApplyKmerProcessor.java:
+    100-108) against the rows handed to kma_table_create: on every edge case of the golden file
+    (duplicate kmers, last row wins; kmers of other lengths; foreign symbols; first-seen role
+    order) the same roles in fid order, the same table counts and the same apply outputs
+    (equal to the golden expectations); CRLF line ends, a missing final newline and a third
+    column are read as TabbedLineReader reads them."""
+    for c in json.load(open(os.path.join(GOLDEN, "apply_edge.json"))):
+        rows = [tuple(r) for r in c["rows"]]
+        f = tmp_path / f"{c['name']}.tbl"
+        _write_tsv(f, [(k, f"{r}\tignored third column" if i % 2 else r)
+                       for i, (k, r) in enumerate(rows)], crlf, trailing)
+        t, roles, last = kma.SignatureTable.from_tsv(str(f), K)
+        ids = _roles(rows)
+        assert roles == list(ids) and last == len(rows[-1][0]), c["name"]
+        with t, kma.SignatureTable.from_rows([r[0] for r in rows], [ids[r[1]] for r in rows],
+                                             K) as ref:
+            a, b = t.info, ref.info
+            assert (a.n_rows, a.n_skipped, a.n_entries, a.n_extra_syms) == \
+                (b.n_rows, b.n_skipped, b.n_entries, b.n_extra_syms), c["name"]
+            res, off = kma.pack_strings(c["proteins"])
+            got = kma.annotate_proteins(t, res, off, c["min_hits"], c["flags"])
+            want = kma.annotate_proteins(ref, res, off, c["min_hits"], c["flags"])
+            assert all((x == y).all() for x, y in zip(got[:3], want[:3])), c["name"]
+        inv = dict(enumerate(roles))
+        assert [[int(s), inv.get(int(fi)), int(n)] for fi, n, s in zip(*got[:3])] == \
+            c["expected"], c["name"]
+
+
+def test_table_from_tsv_rows_without_role_and_replicas(kma, tmp_path):
+    """A row without a tab has the role "" (TabbedLineReader pads the missing column), empty
+    lines are rows with an empty kmer (never matched); the table is replicated over the listed
+    devices and answers like the single-device table; 100k rows parse over several chunks."""
+    from kmeranno import synth
+    wl = synth.make_workload(500, 100_000, 300, seed=43)
+    kmers = [synth.unpack_key(x) for x in wl.keys]
+    rows = [(k, f"ROLE{int(f):07d}") for k, f in zip(kmers, wl.fids)]
+    rows[5] = (rows[5][0], None)
+    rows[9] = ("", "ROLE0000001")
+    f = tmp_path / "kmerdb.tbl"
+    _write_tsv(f, rows)
+    ids = {}
+    for _, r in rows:
+        ids.setdefault(r or "", len(ids))
+    t, roles, last = kma.SignatureTable.from_tsv(str(f), K, devices=[0, 0])
+    assert roles == list(ids) and last == 8 and t.replicas == [0, 0]
+    with t, kma.SignatureTable.from_rows([r[0] for r in rows], [ids[r[1] or ""] for r in rows],
+                                         K) as ref:
+        assert t.info.n_skipped == 1 and t.info.n_entries == ref.info.n_entries
+        got = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0, n_fid=len(ids))
+        want = kma.annotate_proteins(ref, wl.residues, wl.offsets, 5, 0, n_fid=len(ids))
+        assert all((x == y).all() for x, y in zip(got, want))
+        assert (got[2] == 1).sum() > 100
+
+
 def test_table_info_and_alphabet(kma):
     rows = [("ACDEFGHI", 0), ("ACDEFGHI", 1), ("ACDEFGH", 2), ("ACDE-GHI", 1)]
     t = kma.SignatureTable.from_rows([r[0] for r in rows], [r[1] for r in rows], K)
