@@ -412,6 +412,7 @@ struct ProteinArgs {
   uint32_t packed;
   uint64_t stream_first;  // packed: stream residue index of residue offsets[0]
   uint32_t two_choice;    // table placement: 1 = a missed key's only other bucket is alt_bucket
+  uint32_t block_waves;   // waves per block: 4 (kWavesPerBlock), or 1 (wave-granular grid, K = 8)
 };
 
 struct ContigArgs {

@@ -285,6 +285,44 @@ def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path, input
     assert _gpu_apply(kma, rows, prots) == exp
 
 
+@pytest.mark.parametrize("bp", [1, 2])
+def test_one_wave_blocks_vs_oracle(kma, oracle_c, path, input_mode, bp):
+    """The wave-granular grid (KMA_OPT_BLOCK_WAVES = 1, round 6: one-wave blocks of one or two
+    proteins, a 992-entry LDS set pool each): a synthetic batch at load factors 0.5 and 0.9 and
+    long proteins whose sets go to workspace lists (deduplicated in the wave's pool, or in a
+    workspace hash set for giant ones) equal the oracle, both grids, both inputs."""
+    from kmeranno import synth
+    kma.set_option(kma.OPT_BLOCK_WAVES, 1)
+    kma.set_option(kma.OPT_BLOCK_PROTEINS, bp)
+    try:
+        wl = synth.make_workload(3000, 200_000, 2000, seed=47)
+        kmers = [synth.unpack_key(x) for x in wl.keys]
+        ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
+        for flags in (0, 1, 2):
+            efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, flags)
+            for lf in (0.5, 0.9):
+                with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
+                    fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5,
+                                                                flags, n_fid=2000)
+                assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
+                assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
+        rng = np.random.default_rng(5)
+        aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+        prots, rows = [], []
+        for L, role in ((700, "R1"), (3000, "R2"), (90, "R3"), (6000, "R4"), (40, "R5")):
+            q = aa[rng.integers(0, 20, L)].tobytes().decode()
+            q = q + q[:min(300, L)]  # duplicate windows
+            prots.append(q)
+            rows += [(q[i:i + K], role) for i in range(0, len(q) - K + 1, 1 + (L % 3))]
+        prots += [prots[2], prots[0] + prots[1][:500], prots[4]]
+        exp = _oracle_apply(oracle_c, rows, prots)
+        assert max(e[2] for e in exp) > 1000
+        assert _gpu_apply(kma, rows, prots) == exp
+    finally:
+        kma.set_option(kma.OPT_BLOCK_WAVES, 0)
+        kma.set_option(kma.OPT_BLOCK_PROTEINS, 0)
+
+
 def test_giant_proteins_any_length(kma, oracle_c, path):
     """No length limit (ABI 1 returned TOO_LONG beyond 2^16 windows): proteins of 70k and
     200k residues with repeated blocks, one role and two roles, voted exactly."""
