@@ -63,7 +63,7 @@ MALL_BYTES = 256 << 20  # Infinity Cache: a table below it is served on-die (MI3
 GATHER_BIN = os.path.join(ROOT, "kmers.anno_amd", "build", "kma_gather_bench")
 # Per-launch PMC traffic of the dominant kernels of this build (scripts/gpu_traffic.sh +
 # scripts/traffic_summary.py).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06_traffic.json")
 METRIC = "kmer lookups/s + seqs annotated/s at 1/2/4/8 GPUs; achieved HBM GB/s vs roofline"
 WORKLOADS = {
     "c2": "10k synthetic proteins (small.gto CDS length distribution) vs 10M-entry protein "
@@ -203,7 +203,8 @@ def gather_ceiling(table_bytes: int):
 def pmc_traffic(workload: str, kernel: str):
     """(traffic bytes per launch, fabric line requests per launch, source, stale) from the
     committed PMC summary, or Nones. stale: the summary was measured on other kernel sources
-    than this tree's (its source_sha16 differs): its numbers are then not reported."""
+    than this tree's (its source_sha16 differs): its numbers are then not reported. workload:
+    c2 .. c5, or an LF-sweep tag (c5_lf0.75: c5 at load factor 0.75)."""
     try:
         d = json.load(open(TRAFFIC_FILE))
         rec = d["workloads"][workload][kernel]
@@ -922,7 +923,8 @@ def main():
             "gpu_ms_per_step": gpu_ms / args.steps,
             "phases_ms": ph,
         }
-        out["roofline"] = protein_roofline(ph, args.workload, m, n_win, n_res, table.info.bytes,
+        wl_tag = args.workload if args.load_factor == 0.5 else f"{args.workload}_lf{args.load_factor:g}"
+        out["roofline"] = protein_roofline(ph, wl_tag, m, n_win, n_res, table.info.bytes,
                                            live=not args.no_extras)
         if world > 1:
             add_rank_fields(out, table, args)

@@ -6,7 +6,8 @@
 #   stats    rocprofv3 --kernel-trace --stats of the c5 and c3 bench commands
 #   bench    the bench lines: c5 (headline, with the CPU baseline), c2, c3, c4
 #   sq       SQ counters of c5 and c3 (VALU / LDS / wait split)
-# Usage: SECTIONS="traffic stats bench sq" TRAFFIC=profiles/r05_traffic.json \
+#   lf       c5 bench lines at load factors 0.75 and 0.9 (their PMC requests: WLS="... c5_lf0.75 c5_lf0.9")
+# Usage: SECTIONS="traffic stats bench sq" TRAFFIC=profiles/r06_traffic.json \
 #          bash scripts/gpu_measure.sh <out-subdir>
 # Stops at the first step that does not exit 0.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -24,8 +25,9 @@ for s in $SECTIONS; do
       for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
         tag=$(echo $c | cut -d' ' -f1)
         step pmc_gather_$tag 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_gather_$tag -o run -- $GB 1536 quad 4
-        for wl in ${WLS:-c5 c2 c3 c4}; do
-          step pmc_${wl}_$tag 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${wl}_$tag -o run -- python3 bench.py $SHORT --workload $wl
+        for wl in ${WLS:-c5 c2 c3 c4}; do  # c5_lf0.75: c5 at load factor 0.75 (LF sweep lines)
+          wa="--workload ${wl%%_lf*}"; [ "$wl" != "${wl#*_lf}" ] && wa="$wa --load-factor ${wl#*_lf}"
+          step pmc_${wl}_$tag 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${wl}_$tag -o run -- python3 bench.py $SHORT $wa
         done
       done
       step traffic 60 python3 scripts/traffic_summary.py $OUT 8388608
@@ -38,6 +40,10 @@ for s in $SECTIONS; do
       step bench_c2 300 python3 bench.py --workload c2 --no-cpu-baseline
       step bench_c3 300 python3 bench.py --workload c3 --no-cpu-baseline
       step bench_c4 300 python3 bench.py --workload c4 --no-cpu-baseline ;;
+    lf)  # c5 load-factor sweep lines (their PMC requests per window: WLS with c5_lf0.75 c5_lf0.9)
+      for lf in 0.75 0.9; do
+        step bench_c5_lf$lf 600 python3 bench.py --workload c5 --load-factor $lf --no-cpu-baseline
+      done ;;
     sq)
       P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
       P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE"

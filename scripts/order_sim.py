@@ -6,7 +6,8 @@ bucket), and for random query proteins of small.gto's CDS lengths, reports per o
   density  : fraction of probed windows whose home LINE (bucket pair) differs from the previous
              window's in the same protein (the minimizer layout's line requests per window)
   overflow : keys beyond 8 per bucket / T (the keys a two-choice build must place in their
-             alternate bucket at least; the build's evictions add to it)
+             alternate bucket at least; the build's evictions add to it); and beyond 16 per
+             bucket pair, were a pair one 128-byte home
 Orders (kma_internal.h minimizer_hash and its round-6 alternatives):
   random   : smallest multiplicative hash of the K - m + 1 m-mers (the shipped order, m = 6)
   syncmer  : closed syncmers first (an m-mer whose smallest 3-mer hash sits at its first or last
@@ -67,8 +68,8 @@ def order_value(keys, order, k=8):
             t3 = sub_at(keys, k, s, i)
             best = np.minimum(best, (mul32(t3, 0x9E3779) & U32(0xFFFFFFF8)) | U32(i))
         p = ((best & U32(7)) % U32(w)).astype(np.uint64)
-        return ((keys >> (np.uint64(5) * (np.uint64(k - m) - p)))
-                & np.uint64((1 << (5 * m)) - 1)).astype(U32)
+        return mmer_hash(((keys >> (np.uint64(5) * (np.uint64(k - m) - p)))
+                          & np.uint64((1 << (5 * m)) - 1)).astype(U32))
     raise ValueError(order)
 
 
@@ -116,13 +117,16 @@ def main():
             b = 2 * pair_of(order_value(keys, order), nb) + parity(keys)
             counts += np.bincount(b.astype(np.int64), minlength=nb)
         over = np.maximum(counts - 8, 0).sum() / T
+        pairs = counts[0::2] + counts[1::2]  # one 128-byte home of 16 slots per pair
+        over16 = np.maximum(pairs - 16, 0).sum() / T
         changes = windows = 0
         for q in qkeys:
             pr = pair_of(order_value(q, order), nb)
             changes += 1 + int((pr[1:] != pr[:-1]).sum())
             windows += len(pr)
         print(f"{order:8s} density {changes / windows:.4f}  overflow {over:.4f}  "
-              f"max keys per bucket {counts.max()}", flush=True)
+              f"overflow of 128-byte homes {over16:.4f}  max keys per bucket {counts.max()}",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -42,7 +42,10 @@ out = {"source_sha16": kmeranno.source_digest(),
        "calibration": {"kernel": gk, "lines_per_launch": lines,
                        "fetch_bytes": g[gk]["FETCH_SIZE"] * 1024, "factor": corr},
        "workloads": {}}
-for wl in ("c2", "c3", "c4", "c5"):
+# every workload tag measured: c2 .. c5, and LF-sweep tags such as c5_lf0.75 (gpu_measure.sh WLS)
+tags = sorted({os.path.basename(d)[len("pmc_"):-len("_FETCH_SIZE")]
+               for d in glob.glob(f"{root}/pmc_*_FETCH_SIZE")} - {"gather"})
+for wl in tags:
     f, w, t = (load(f"{root}/pmc_{wl}_{c}") for c in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum"))
     if not f:
         continue
