@@ -194,9 +194,6 @@ int kma_device_count(int* out_n);
  *   KMA_OPT_HOST_PIECE_MIN  host protein calls: fewest residues per pipeline piece [0: 2^24]; a
  *                           call runs min(KMA_OPT_HOST_PIECES, residues / this) pieces (ABI 7;
  *                           tests set it low to run many pieces on small batches)
- *   KMA_OPT_BLOCK_WAVES     protein kernel: waves per block [0: 4]; 1 = the wave-granular grid
- *                           (one-wave blocks of 1 or 2 proteins, KMA_OPT_BLOCK_PROTEINS; K = 8
- *                           tables only, others keep 4); 4 (ABI 7)
  * kma_workspace_option_set overrides KMA_OPT_BLOCK_PROTEINS / KMA_OPT_DEFER for the _device
  * calls made with one workspace (KMA_OPT_DEFAULT: follow the library default again).        */
 #define KMA_OPT_LAYOUT 1
@@ -209,7 +206,6 @@ int kma_device_count(int* out_n);
 #define KMA_OPT_HOST_SLICE 8
 #define KMA_OPT_PLACEMENT 9
 #define KMA_OPT_HOST_PIECE_MIN 10
-#define KMA_OPT_BLOCK_WAVES 11
 #define KMA_OPT_DEFAULT INT64_MIN
 int kma_option_set(int option, int64_t value);
 int kma_option_get(int option, int64_t* value);

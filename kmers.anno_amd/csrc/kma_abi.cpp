@@ -39,8 +39,8 @@ namespace {
 // Library-wide defaults, read per call; workspaces may override the protein-kernel ones. The
 // environment is read only by tuning builds (-DKMA_TUNING_ENV=1, the A/B scripts' variants):
 // a library a JVM loads must not change its kernel geometry because of a stray variable.
-constexpr int kNumOpts = 12;
-std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}, {-1}, {0}, {0}};
+constexpr int kNumOpts = 11;
+std::atomic<int64_t> g_opt[kNumOpts] = {{0}, {-1}, {0}, {-1}, {0}, {0}, {1}, {0}, {0}, {-1}, {0}};
 constexpr int64_t kOptUnset = INT64_MIN;  // workspace override not set: the library default
 
 bool option_valid(int opt, int64_t v) {
@@ -54,7 +54,6 @@ bool option_valid(int opt, int64_t v) {
     case KMA_OPT_HOST_THREADS: return v >= 0 && v <= 64;
     case KMA_OPT_HOST_SLICE: return v >= 0 && v <= (int64_t)((1ull << 32) - 128);  // a call's limit
     case KMA_OPT_HOST_PIECE_MIN: return v >= 0 && v <= (int64_t)(1ull << 32);
-    case KMA_OPT_BLOCK_WAVES: return v == 0 || v == 1 || v == 4;
     case KMA_OPT_PLACEMENT: return v >= -1 && v <= 1;
     default: return false;
   }
@@ -1433,11 +1432,9 @@ const char* const kContigPhases[] = {"contigs_probe_kernel", "scan_emit"};
 // single proteins, so the last blocks to start end sooner; profiles/r05/c2_taper_r05u/) 47.0 /
 // 49.3 / 54.0 / 55.1 us for tails of 1/4, 1/2, 1 and 2 resident waves: each group's fixed chain
 // (offsets, first residues, final walks, vote) costs more than the shorter tail saves.
-uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes,
-                        uint32_t waves) {
+uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_bytes) {
   const int64_t f = ws->opt_block_proteins != kOptUnset ? ws->opt_block_proteins
                                                          : opt(KMA_OPT_BLOCK_PROTEINS);
-  if (waves == 1) return f >= 1 && f <= 2 ? (uint32_t)f : 1u;  // one-wave blocks: 1 or 2
   if (f >= 1 && f <= kma::kBlockProteins) return (uint32_t)f;
   const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
   return (uint64_t)n_seq / 6 > 4 * slots && table_bytes > kInfinityCacheBytes ? 6u : 4u;
@@ -1452,9 +1449,8 @@ uint32_t block_proteins(const kma_workspace* ws, uint32_t n_seq, uint64_t table_
 // CU): measured (profiles/r02m_defer_ab.log) c2 (1.4 waves) 66 -> 54 us, 40k proteins (5.6)
 // even, 100k (14) 3% slower, c4 / c5 7% / 3% slower when forced. KMA_DEFER=0 disables it,
 // KMA_DEFER=<steps> forces it on any batch (read per call).
-uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups, uint32_t waves) {
-  const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1) *
-                         (kma::kWavesPerBlock / waves);  // resident blocks
+uint32_t defer_below(const kma_workspace* ws, uint64_t n_groups) {
+  const uint64_t slots = (uint64_t)kma::kProteinOcc * (uint64_t)std::max(ws->n_cu, 1);
   const int64_t f = ws->opt_defer != kOptUnset ? ws->opt_defer : opt(KMA_OPT_DEFER);
   if (f >= 0) return (uint32_t)std::min<int64_t>(64, f);
   return n_groups > slots && n_groups <= 4 * slots ? 3u : 0u;
@@ -1510,13 +1506,9 @@ int annotate_proteins_on(const kma_table* t, const Replica& r, kma_workspace* ws
   a.tally = d_tally;
   a.n_fid = d_tally ? n_fid : 0;
   a.gset = ws->d_gset;
-  // Waves per block (KMA_OPT_BLOCK_WAVES): 4 by default; 1 = the wave-granular grid (round 6:
-  // one-wave blocks of one or two proteins, K = 8 only), measured on small launches.
-  a.block_waves = opt(KMA_OPT_BLOCK_WAVES) == 1 && t->k == 8 ? 1u : (uint32_t)kma::kWavesPerBlock;
-  a.block_proteins = block_proteins(ws, n_seq, t->n_buckets * (uint64_t)kma::kBucketBytes,
-                                    a.block_waves);
+  a.block_proteins = block_proteins(ws, n_seq, t->n_buckets * (uint64_t)kma::kBucketBytes);
   a.n_groups = (n_seq + a.block_proteins - 1) / a.block_proteins;
-  a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups, a.block_waves) : 0u;
+  a.defer_below = a.n_groups < (1u << 30) ? defer_below(ws, a.n_groups) : 0u;
   const bool pack = input == Input::kPackOnDevice;
   PhaseClock clk(ws, s, pack ? kPackedPhases : kDirectPhases, pack ? 2 : 1);
   KMA_HIP(clk.mark());

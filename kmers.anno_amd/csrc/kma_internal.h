@@ -165,6 +165,9 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
 // The order bit rides in the minimizer length m of layout codes and kernel templates; the
 // minimizer length proper is m & kMinimizerMask.
 constexpr int kOrderMod = KMA_LAYOUT_MOD_SAMPLING;
+#ifndef KMA_MOD_OPEN
+#define KMA_MOD_OPEN 0
+#endif
 constexpr int kMinimizerMask = 0x3F;
 __host__ __device__ constexpr bool order_mod_valid(int k, int m) {
   return k == 8 && (m & kMinimizerMask) == 6;  // the instantiated kernels (kma_device.h)
@@ -185,7 +188,14 @@ __host__ __device__ inline uint32_t mod_sample(uint64_t key, int k, int m) {
   for (int i = 0; i < nt; ++i) {
     const uint32_t t3 = (uint32_t)(key >> (5 * (nt - 1 - i))) & 0x7FFFu;
     // an odd 24-bit multiplier: a bijection of the 15-bit 3-mer codes; position in the low bits
-    const uint32_t g = (mul24(t3, 0x9E3779u) & ~7u) | (uint32_t)i;
+    uint32_t g = mul24(t3, 0x9E3779u);
+#if KMA_MOD_OPEN
+    // open-closed mod-sampling (tuning variant): 3-mers whose middle residue code is below both
+    // of its neighbours' rank first (simulated density 0.410 vs 0.431, scripts/order_sim.py)
+    const uint32_t c0 = t3 >> 10, c1 = (t3 >> 5) & 31u, c2 = t3 & 31u;
+    g = (c1 < c0 && c1 < c2) ? g >> 1 : (g >> 1) | 0x80000000u;
+#endif
+    g = (g & ~7u) | (uint32_t)i;
     best = best < g ? best : g;
   }
   const int p = (int)(best & 7u) % w;
@@ -414,7 +424,6 @@ struct ProteinArgs {
   uint32_t packed;
   uint64_t stream_first;  // packed: stream residue index of residue offsets[0]
   uint32_t two_choice;    // table placement: 1 = a missed key's only other bucket is alt_bucket
-  uint32_t block_waves;   // waves per block: 4 (kWavesPerBlock), or 1 (wave-granular grid, K = 8)
 };
 
 struct ContigArgs {

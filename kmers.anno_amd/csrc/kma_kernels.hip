@@ -389,16 +389,11 @@ __device__ unsigned long long g_walk_stats[8];
 #define KMA_COUNT(i, v) ((void)0)
 #endif
 
-// Per-block protein records (LDS). The layout keeps kProteinOcc waves per SIMD resident: blocks
-// of NW waves (4: the default; 1: the wave-granular grid of small launches, round 6) hold
-// set_pool<NW>() set entries.
-template <int NW>
-constexpr int set_pool() { return NW == kWavesPerBlock ? kSetPool : 992; }
-template <int P, int NW = kWavesPerBlock>
+// Per-block protein records (LDS). The layout keeps kProteinOcc blocks per CU resident.
+template <int P>
 struct ProteinSmem {
-  static constexpr int kPool = set_pool<NW>();
-  __attribute__((aligned(16))) uint32_t pool[kPool];  // LDS sets: slot id + 1, 0 = empty
-  uint32_t chain_q[NW][2 * kChainQ];  // deferred chain walks: packed key, protein
+  __attribute__((aligned(16))) uint32_t pool[kSetPool];  // LDS sets: slot id + 1, 0 = empty
+  uint32_t chain_q[kWavesPerBlock][2 * kChainQ];  // deferred chain walks: packed key, protein
   uint32_t pbeg[P + 1];  // protein starts relative to the span start; [np..P] = span end
   uint32_t pwin[P];      // windows of the protein (ProteinKmers: L - K + 1, or L - K)
   uint32_t pset[P];      // set base in `pool`, or kGlobalSet
@@ -410,9 +405,6 @@ struct ProteinSmem {
 };
 static_assert(sizeof(ProteinSmem<kBlockProteins>) <= 163840 / kProteinOcc,
               "protein-path LDS must leave kProteinOcc blocks per CU");
-constexpr int kWaveBlockProteins = 2;  // proteins per one-wave block (its LDS: 28 blocks per CU)
-static_assert(sizeof(ProteinSmem<kWaveBlockProteins, 1>) <= 163840 / (4 * kProteinOcc),
-              "one-wave blocks' LDS must leave kProteinOcc waves per SIMD");
 
 // Insert slot id + 1 in a set of `cap` u32 entries; true if it was not there.
 __device__ __forceinline__ bool lds_set_insert(uint32_t* set, uint32_t cap, uint32_t key) {
@@ -442,8 +434,8 @@ __device__ __forceinline__ bool global_set_insert(uint32_t* set, uint32_t cap, u
 // per residue), deduplicated after the probe steps (dedupe_lists). Round 3 kept a hash set
 // there, zeroed by the block and filled by agent-scope CAS: at c5 0.23 GB of writes per launch
 // for 9 MB of outputs, the set lines being evicted from L2 between hits under the gather load.
-template <int P, int NW>
-__device__ __forceinline__ void record_hit(ProteinSmem<P, NW>& sm, const ProteinArgs& a,
+template <int P>
+__device__ __forceinline__ void record_hit(ProteinSmem<P>& sm, const ProteinArgs& a,
                                            uint64_t span_lo, bool multiset, uint32_t p,
                                            uint32_t fid, uint32_t sid) {
   atomicMin(&sm.pmin[p], fid);
@@ -473,10 +465,9 @@ __device__ __forceinline__ void record_hit(ProteinSmem<P, NW>& sm, const Protein
 // zeroed here (agent-scope stores, the CAS inserts are agent-scope). Block-uniform loop.
 // (Protein bounds from LDS: indexing the kernel's register copy pb[] by the loop counter makes
 // the compiler spill it to scratch.)
-template <int P, int NW>
-__device__ __forceinline__ void dedupe_lists(ProteinSmem<P, NW>& sm, const ProteinArgs& a,
+template <int P>
+__device__ __forceinline__ void dedupe_lists(ProteinSmem<P>& sm, const ProteinArgs& a,
                                              uint64_t span_lo) {
-  constexpr uint32_t T = 64u * NW, kPool = ProteinSmem<P, NW>::kPool;
   const int t = threadIdx.x;
   for (int p = 0; p < P; ++p) {
     if (sm.pset[p] != kGlobalSet) continue;
@@ -484,19 +475,19 @@ __device__ __forceinline__ void dedupe_lists(ProteinSmem<P, NW>& sm, const Prote
     if (h == 0) continue;
     const uint32_t* list = a.gset + 2 * (span_lo + b0);
     uint32_t fresh = 0;
-    if (h < kPool) {
+    if (h < (uint32_t)kSetPool) {
       uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
-      for (uint32_t i = t; i < kPool / 4; i += T) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+      for (uint32_t i = t; i < (uint32_t)kSetPool / 4; i += 256) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
       __syncthreads();
-      for (uint32_t i = t; i < h; i += T) fresh += lds_set_insert(sm.pool, kPool, list[i]);
+      for (uint32_t i = t; i < h; i += 256) fresh += lds_set_insert(sm.pool, kSetPool, list[i]);
     } else {
       const uint32_t L = sm.pbeg[p + 1] - b0;  // > windows >= h: the set never fills
       uint32_t* set = a.gset + 2 * (span_lo + b0) + L;
-      for (uint32_t i = t; i < L; i += T)
+      for (uint32_t i = t; i < L; i += 256)
         __hip_atomic_store(set + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence();  // (giant proteins only: an L2 writeback per such protein)
       __syncthreads();
-      for (uint32_t i = t; i < h; i += T) fresh += global_set_insert(set, L, list[i]);
+      for (uint32_t i = t; i < h; i += 256) fresh += global_set_insert(set, L, list[i]);
     }
     fresh = wave_sum(fresh);
     if ((t & 63) == 0 && fresh) atomicAdd(&sm.pcnt[p], fresh);
@@ -595,7 +586,7 @@ __device__ __forceinline__ WinWords load_win(const uint8_t* __restrict__ res, ui
 }
 // The group's first probe step's residue words (clamped to the batch, which is readable past
 // its end; windows past the span are masked in the loop).
-template <int U, bool Packed, int NW = kWavesPerBlock>
+template <int U, bool Packed>
 __device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupHead& h,
                                               uint32_t tw, WinWords (&ww)[U]) {
   uint64_t pos0;
@@ -603,7 +594,7 @@ __device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupH
   const uint64_t lim = a.n_residues - h.span_lo;
 #pragma unroll
   for (int j = 0; j < U; ++j) {
-    const uint32_t x = j * (64u * NW) + tw;
+    const uint32_t x = j * 256u + tw;
     ww[j] = load_win<Packed>(res, (x < lim ? x : 0u) + pos0);
   }
 }
@@ -612,13 +603,11 @@ __device__ __forceinline__ void head_residues(const ProteinArgs& a, const GroupH
 // residue words are in ww. pass 0 / 1: a block of the two-pass grid, which annotates its group
 // only if the group is long (pass 0) / short (pass 1: fewer than defer_below probe steps);
 // pass -1: always. sm.lut is being loaded (read after the first barrier).
-template <int K, int M, int P, bool Packed, int NW>
-__device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P, NW>& sm,
+template <int K, int M, int P, bool Packed>
+__device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem<P>& sm,
                                                const GroupHead& h, WinWords (&ww)[kProbeWin],
                                                const int pass = -1) {
   constexpr int U = kProbeWin;
-  constexpr uint32_t T = 64u * NW;  // threads per block
-  constexpr uint32_t kPool = ProteinSmem<P, NW>::kPool;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, part = t & 3;
   const bool multiset = (a.flags & KMA_F_MULTISET) != 0;
   const uint32_t tw = lane_window(t);
@@ -632,7 +621,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     const uint64_t end = __shfl_down(beg, 1, 64);
     const uint64_t lo = __shfl(beg, 0, 64), span_end = __shfl(beg, (int)np, 64);
     if (pass >= 0 && lane == 0) {  // two-pass grid: is the group this pass's?
-      const bool short_group = span_end - lo < (uint64_t)a.defer_below * T * kProbeWin;
+      const bool short_group = span_end - lo < (uint64_t)a.defer_below * 256u * kProbeWin;
       sm.skip = short_group != (pass == 1) ? 1u : 0u;
     }
     if (lane <= P) sm.pbeg[lane] = (uint32_t)((lane <= (int)np ? beg : span_end) - lo);
@@ -654,7 +643,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       uint32_t sum = 0;
       for (int p = 0; p < P; ++p) sum += sm.pcap[p];
       uint32_t top = 0;
-      if (sum <= kPool) {  // the usual case: every set in LDS, in protein order
+      if (sum <= (uint32_t)kSetPool) {  // the usual case: every set in LDS, in protein order
         for (int p = 0; p < P; ++p) {
           sm.pset[p] = top;
           top += sm.pcap[p];
@@ -669,7 +658,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
             if (!(done >> p & 1u) && (best < 0 || sm.pcap[p] > sm.pcap[best])) best = p;
           done |= 1u << best;
           const uint32_t cap = sm.pcap[best];
-          const bool fits = top + cap <= kPool;
+          const bool fits = top + cap <= (uint32_t)kSetPool;
           sm.pset[best] = fits ? top : kGlobalSet;  // (a list: appended, never zeroed)
           top += fits ? cap : 0u;
         }
@@ -689,7 +678,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   __syncthreads();  // `used` has been read by every wave
   uint4* pool4 = reinterpret_cast<uint4*>(sm.pool);
   KMA_CLK(1);
-  for (uint32_t i = t; i < used / 4; i += T) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t i = t; i < used / 4; i += 256) pool4[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 
   const uint64_t* __restrict__ slots = a.slots;
@@ -698,7 +687,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   const uint8_t* lut = sm.lut;
   uint32_t* cq = sm.chain_q[wave];
   uint32_t cn = 0;  // wave-uniform queue length
-  constexpr uint32_t stride = T * U;
+  constexpr uint32_t stride = 256u * U;
   // Deferred chain walks, 64 queued windows at a time: lane (quad g, member p) takes entry
   // 16 p + g of the chunk; the chain's first bucket of every entry is loaded and matched by a
   // quad (the probe loop's cooperative loads: 2 line requests per bucket instead of 8 dwordx4
@@ -726,7 +715,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 #else
       const bool hit = walk_chain(slots, nb, home_bucket(key, K, M, nb), key, fid, sid, two_choice);
 #endif
-      if (hit) record_hit<P, NW>(sm, a, span_lo, multiset, p, fid, sid);
+      if (hit) record_hit<P>(sm, a, span_lo, multiset, p, fid, sid);
 #ifdef KMA_TUNE_COUNT
       {
         const uint32_t s1 = chain_bucket(home_bucket(key, K, M, nb), 1u, nb);
@@ -753,7 +742,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   auto prep = [&](uint32_t xs, Prep& o) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = xs + j * T + tw;
+      const uint32_t x = xs + j * 256u + tw;
       const uint32_t p = protein_at<P>(pb, x);
       uint64_t key;
       bool ok;
@@ -790,7 +779,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   auto load_residues = [&](uint32_t xs) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const uint32_t x = xs + j * T + tw;
+      const uint32_t x = xs + j * 256u + tw;
       ww[j] = load_win<Packed>(res, (x < span ? x : 0u) + pos0);
     }
   };
@@ -830,7 +819,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
       KMA_COUNT(3, __popcll(__ballot((w & kWordHit) != 0u)));
 #endif
       if (w & kWordHit)
-        record_hit<P, NW>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, w & kFidMask,
+        record_hit<P>(sm, a, span_lo, multiset, c.bk[j] >> kBucketBits, w & kFidMask,
                       (c.bk[j] & kBucketIdx) * kSlotsPerBucket + ((w >> kSlotShift) & kSlotMask));
       // rare: the home bucket missed and the key's filter positions are set -> deferred walk
 #ifdef KMA_TUNE_NO_WALK  // tuning builds only (cost bound of the chain walks; misses keys)
@@ -868,7 +857,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   if (cn) chain_flush();
   KMA_CLK(4);
   __syncthreads();  // every LDS set is final; the lists are complete
-  if (!multiset) dedupe_lists<P, NW>(sm, a, span_lo);
+  if (!multiset) dedupe_lists<P>(sm, a, span_lo);
   if (t < (int)np) {
     const uint32_t mn = sm.pmin[t], mx = sm.pmax[t], cnt = sm.pcnt[t];
     int32_t fid_out = -1, cnt_out = 0;
@@ -894,19 +883,16 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 // of scratch.
 template <int K, int M, bool Packed>
 constexpr int protein_occ() { return M == 0 && Packed ? 6 : kProteinOcc; }
-template <int K, int M, int P, bool Packed, int NW = kWavesPerBlock>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(protein_occ<K, M, Packed>(), 8))) void annotate_kernel(
+template <int K, int M, int P, bool Packed>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(protein_occ<K, M, Packed>(), 8))) void annotate_kernel(
     ProteinArgs a) {
-  __shared__ ProteinSmem<P, NW> sm;
+  __shared__ ProteinSmem<P> sm;
   KMA_CLK(0);
   const int t = threadIdx.x;
   // The ASCII kernel's LUT: loaded now, stored to LDS once the first residue loads are issued
   // (its store right here made the block wait for it before loading the offsets: one more
   // dependent round trip per block). Read after annotate_block's first barrier.
-  constexpr int kLutPer = 256 / (64 * NW);
-  uint8_t lut_b[kLutPer];
-#pragma unroll
-  for (int i = 0; i < kLutPer; ++i) lut_b[i] = Packed ? 0 : a.lut[t + 64 * NW * i];
+  const uint8_t lut_b = Packed ? 0 : a.lut[t];
   // Two-pass grid (defer_below > 0): blocks [0, n_groups) annotate the long groups, blocks
   // [n_groups, 2 n_groups) the short ones, so that every long group starts before any short
   // one (blocks are dispatched in index order); a block whose group is the other pass's exits
@@ -917,11 +903,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(protein
   // (the two-pass grid keeps block order: its long-first order is what it is for)
   const uint32_t b = blockIdx.x - (second ? a.n_groups : 0u);
   head_offsets(a, a.defer_below ? b : xcd_group(b, a.n_groups), h);
-  head_residues<kProbeWin, Packed, NW>(a, h, lane_window(t), ww);
-  if (!Packed)
-#pragma unroll
-    for (int i = 0; i < kLutPer; ++i) sm.lut[t + 64 * NW * i] = lut_b[i];
-  annotate_block<K, M, P, Packed, NW>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
+  head_residues<kProbeWin, Packed>(a, h, lane_window(t), ww);
+  if (!Packed) sm.lut[t] = lut_b;
+  annotate_block<K, M, P, Packed>(a, sm, h, ww, a.defer_below ? (second ? 1 : 0) : -1);
   KMA_CLK(5);
   KMA_CLK_HW();
 }
@@ -1682,26 +1666,11 @@ struct AnnotateLaunch {
       return hipErrorInvalidValue;
     } else {
     constexpr int P = kBlockProteins;
-    const bool one_wave = a.block_waves == 1;
-    if (!one_wave && a.block_waves != (uint32_t)kWavesPerBlock) return hipErrorInvalidValue;
-    const uint32_t pmax = one_wave ? (uint32_t)kWaveBlockProteins : (uint32_t)P;
-    const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= pmax ? a.block_proteins : 0u;
+    const unsigned bp = a.block_proteins >= 1 && a.block_proteins <= (uint32_t)P ? a.block_proteins : 4u;
     if (bp != a.block_proteins) return hipErrorInvalidValue;
     const unsigned blocks = (a.n_seq + bp - 1) / bp;
     if (a.n_groups != blocks) return hipErrorInvalidValue;
     const dim3 grid(a.defer_below ? 2 * blocks : blocks);
-    if (one_wave) {
-      // the wave-granular grid (round 6): K = 8 only (the apply path)
-      if constexpr (K == 8) {
-        if (a.packed)
-          hipLaunchKernelGGL((annotate_kernel<K, M, kWaveBlockProteins, true, 1>), grid, dim3(64), 0, stream, a);
-        else
-          hipLaunchKernelGGL((annotate_kernel<K, M, kWaveBlockProteins, false, 1>), grid, dim3(64), 0, stream, a);
-        return hipGetLastError();
-      } else {
-        return hipErrorInvalidValue;
-      }
-    }
     if (a.packed)
       hipLaunchKernelGGL((annotate_kernel<K, M, P, true>), grid, dim3(256), 0, stream, a);
     else

@@ -46,10 +46,10 @@ EXPORTS = (
 # Tuning options (include/kmeranno.h "options"): library-wide defaults read per call.
 OPT_LAYOUT, OPT_BLOCK_PROTEINS, OPT_DEFER, OPT_HOST_PIECES, OPT_HASH_SLICE = 1, 2, 3, 4, 5
 OPT_PACKED_INPUT, OPT_HOST_THREADS, OPT_HOST_SLICE, OPT_PLACEMENT = 6, 7, 8, 9
-OPT_HOST_PIECE_MIN, OPT_BLOCK_WAVES = 10, 11
+OPT_HOST_PIECE_MIN = 10
 OPT_DEFAULTS = {OPT_LAYOUT: -1, OPT_BLOCK_PROTEINS: 0, OPT_DEFER: -1, OPT_HOST_PIECES: 0,
                 OPT_HASH_SLICE: 0, OPT_PACKED_INPUT: 1, OPT_HOST_THREADS: 0, OPT_HOST_SLICE: 0,
-                OPT_PLACEMENT: -1, OPT_HOST_PIECE_MIN: 0, OPT_BLOCK_WAVES: 0}
+                OPT_PLACEMENT: -1, OPT_HOST_PIECE_MIN: 0}
 LAYOUT_TWO_CHOICE = 0x100  # layout code flag: two-choice placement (include/kmeranno.h)
 LAYOUT_MOD_SAMPLING = 0x40  # layout code flag: the mod-sampling minimizer order (K = 8, m = 6)
 OPT_DEFAULT = -(1 << 63)  # kma_workspace_option_set: follow the library default
@@ -57,7 +57,7 @@ _OPT_NAMES = {"layout": OPT_LAYOUT, "block_proteins": OPT_BLOCK_PROTEINS, "defer
               "host_pieces": OPT_HOST_PIECES, "hash_slice": OPT_HASH_SLICE,
               "packed_input": OPT_PACKED_INPUT, "host_threads": OPT_HOST_THREADS,
               "host_slice": OPT_HOST_SLICE, "placement": OPT_PLACEMENT,
-              "host_piece_min": OPT_HOST_PIECE_MIN, "block_waves": OPT_BLOCK_WAVES}
+              "host_piece_min": OPT_HOST_PIECE_MIN}
 
 
 class KmerAnnoError(RuntimeError):

@@ -41,7 +41,7 @@ def test_options_set_get_validate_restore(native_lib):
                    (k.OPT_HOST_PIECES, 17), (k.OPT_HASH_SLICE, -1), (k.OPT_PACKED_INPUT, 3),
                    (k.OPT_HOST_THREADS, 65), (k.OPT_HOST_SLICE, -1), (k.OPT_PLACEMENT, 2),
                    (k.OPT_HOST_SLICE, 1 << 32), (k.OPT_HOST_PIECE_MIN, -1), (k.OPT_LAYOUT, 7 | 0x40),
-                   (k.OPT_BLOCK_WAVES, 2),
+                   (11, 1),
                    (99, 0)):
         with pytest.raises(k.KmerAnnoError) as e:
             k.set_option(o, bad)
@@ -51,11 +51,11 @@ def test_options_set_get_validate_restore(native_lib):
         assert k.layout_for(7, 1000) == 6 | k.LAYOUT_TWO_CHOICE  # mod-sampling: K = 8 only
     with k.options(layout=7, block_proteins=1, defer=0, host_pieces=3, hash_slice=1000,
                    packed_input=0, host_threads=4, host_slice=12345, placement=0,
-                   host_piece_min=1 << 20, block_waves=1):
-        assert [k.get_option(o) for o in range(1, 12)] == [7, 1, 0, 3, 1000, 0, 4, 12345, 0,
-                                                           1 << 20, 1]
+                   host_piece_min=1 << 20):
+        assert [k.get_option(o) for o in range(1, 11)] == [7, 1, 0, 3, 1000, 0, 4, 12345, 0,
+                                                           1 << 20]
         assert k.layout_for(8, 1000) == 7
-    assert [k.get_option(o) for o in range(1, 12)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1, 0, 0]
+    assert [k.get_option(o) for o in range(1, 11)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1, 0]
     assert k.layout_for(8, 1000) == 6 | k.LAYOUT_TWO_CHOICE
     src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
     assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src

@@ -285,44 +285,6 @@ def test_long_proteins_lds_and_workspace_sets(kma, oracle_c, layout, path, input
     assert _gpu_apply(kma, rows, prots) == exp
 
 
-@pytest.mark.parametrize("bp", [1, 2])
-def test_one_wave_blocks_vs_oracle(kma, oracle_c, path, input_mode, bp):
-    """The wave-granular grid (KMA_OPT_BLOCK_WAVES = 1, round 6: one-wave blocks of one or two
-    proteins, a 992-entry LDS set pool each): a synthetic batch at load factors 0.5 and 0.9 and
-    long proteins whose sets go to workspace lists (deduplicated in the wave's pool, or in a
-    workspace hash set for giant ones) equal the oracle, both grids, both inputs."""
-    from kmeranno import synth
-    kma.set_option(kma.OPT_BLOCK_WAVES, 1)
-    kma.set_option(kma.OPT_BLOCK_PROTEINS, bp)
-    try:
-        wl = synth.make_workload(3000, 200_000, 2000, seed=47)
-        kmers = [synth.unpack_key(x) for x in wl.keys]
-        ot = oracle_c.Table(kmers, wl.fids.astype(np.int32))
-        for flags in (0, 1, 2):
-            efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, flags)
-            for lf in (0.5, 0.9):
-                with kma.SignatureTable.from_packed(wl.keys, wl.fids, K, load_factor=lf) as t:
-                    fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5,
-                                                                flags, n_fid=2000)
-                assert (st == est).all() and (fid == efid).all() and (cnt == ecnt).all()
-                assert (tally == np.bincount(efid[est == 1], minlength=2000)).all()
-        rng = np.random.default_rng(5)
-        aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
-        prots, rows = [], []
-        for L, role in ((700, "R1"), (3000, "R2"), (90, "R3"), (6000, "R4"), (40, "R5")):
-            q = aa[rng.integers(0, 20, L)].tobytes().decode()
-            q = q + q[:min(300, L)]  # duplicate windows
-            prots.append(q)
-            rows += [(q[i:i + K], role) for i in range(0, len(q) - K + 1, 1 + (L % 3))]
-        prots += [prots[2], prots[0] + prots[1][:500], prots[4]]
-        exp = _oracle_apply(oracle_c, rows, prots)
-        assert max(e[2] for e in exp) > 1000
-        assert _gpu_apply(kma, rows, prots) == exp
-    finally:
-        kma.set_option(kma.OPT_BLOCK_WAVES, 0)
-        kma.set_option(kma.OPT_BLOCK_PROTEINS, 0)
-
-
 def test_giant_proteins_any_length(kma, oracle_c, path):
     """No length limit (ABI 1 returned TOO_LONG beyond 2^16 windows): proteins of 70k and
     200k residues with repeated blocks, one role and two roles, voted exactly."""
@@ -636,21 +598,25 @@ def test_device_api_with_torch_buffers(kma):
                      len(wl.keys), status.data_ptr(), stream)
     torch.cuda.synchronize()
     st4 = status.cpu().numpy()
-    assert st4[0] == 0 and st4[1] == len(np.unique(wl.keys)) and st4[2] >= 1
-    t = kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0)
-    assert t.info.minimizer_len == kma.layout_for(K, nb) & 0xFF and t.info.two_choice == 0
-    # the same rows with two-choice placement (the layout code's flag) into a second buffer
+    # layout -1 is kma_table_layout_for's code in both the build and the wrap (the
+    # wrap used to read -1 as chained): two-choice placement at this size
     code = kma.layout_for(K, nb)
     assert code & kma.LAYOUT_TWO_CHOICE
+    assert st4[0] == 0 and st4[1] == len(np.unique(wl.keys)) and st4[2] in (1, 2)
+    t = kma.SignatureTable.wrap_device(slots.data_ptr(), nb, K, 0)
+    assert t.info.minimizer_len == code & 0x3F and t.info.two_choice == 1
+    # the same rows with overflow chains (the code without the two-choice flag) into a second
+    # buffer, wrapped with that code
+    chained = code & ~kma.LAYOUT_TWO_CHOICE
     slots2 = torch.empty_like(slots)
     status2 = torch.zeros(4, dtype=torch.int32, device=dev)
-    kma.build_device(slots2.data_ptr(), nb, 0, keys.data_ptr(), fids.data_ptr(), len(wl.keys),
-                     status2.data_ptr(), stream, layout=code)
+    kma.build_device(slots2.data_ptr(), nb, winner.data_ptr(), keys.data_ptr(), fids.data_ptr(),
+                     len(wl.keys), status2.data_ptr(), stream, layout=chained)
     torch.cuda.synchronize()
     s2 = status2.cpu().numpy()
-    assert s2[0] == 0 and s2[1] == st4[1] and s2[2] in (1, 2)
-    t2 = kma.SignatureTable.wrap_device(slots2.data_ptr(), nb, K, 0, code)
-    assert t2.info.two_choice == 1 and t2.info.minimizer_len == code & 0xFF
+    assert s2[0] == 0 and s2[1] == st4[1] and s2[2] >= 1
+    t2 = kma.SignatureTable.wrap_device(slots2.data_ptr(), nb, K, 0, chained)
+    assert t2.info.two_choice == 0 and t2.info.minimizer_len == chained & 0x3F
     n_res = int(wl.offsets[-1])
     ws = kma.Workspace(0, n_res)
     res = torch.from_numpy(wl.residues).to(dev)
