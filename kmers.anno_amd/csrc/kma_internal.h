@@ -158,16 +158,18 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
 //          the first), the m-mer at x mod w is picked; density (2 + (m - t) / w) / (w + m - t + 1)
 //          = 3/7 = 0.43. Simulated on c5's 10^8-key table (scripts/order_sim.py): density 0.430
 //          vs 0.502, keys beyond a bucket's 8 slots 7.5% vs 6.1% (more keys in their alternate).
-//          Its ~20 more VALU per window cost the Infinity-Cache-resident configs more than they
-//          save (round 5's closed-syncmer order, density 0.454, cost c3 +9% and c2 +5% while it
-//          cut c5's kernel 1.9%: profiles/r05/syncmer_ab_r05s/), so it is a size rule: K = 8,
-//          m = 6 tables larger than the Infinity Cache (kma_abi.cpp minimizer_len).
+//          Measured (ABAB): c5 kernel 2.88 ms against 3.08 ms for the random order
+//          (profiles/r06/order_ab_r06b/); on the 10^7 table (Infinity-Cache resident) c4 2.637
+//          vs 2.688 ms, c2 even (47.1 vs 46.7 us), but the 6-frame probe, two windows per position
+//          and VALU-heavier, 77.2 vs 73.7 us (profiles/r06/order_small_tables_r06c/). The order is
+//          a table property shared by both paths, so it is a size rule: K = 8, m = 6 tables
+//          larger than the Infinity Cache (kma_abi.cpp minimizer_len), where every request goes
+//          to HBM. Not kept: the open-closed variant (3-mers whose middle residue code is below
+//          both neighbours' rank first; simulated density 0.410) at 3.03 ms, its VALU per window
+//          costing more than the 5% fewer home lines save.
 // The order bit rides in the minimizer length m of layout codes and kernel templates; the
 // minimizer length proper is m & kMinimizerMask.
 constexpr int kOrderMod = KMA_LAYOUT_MOD_SAMPLING;
-#ifndef KMA_MOD_OPEN
-#define KMA_MOD_OPEN 0
-#endif
 constexpr int kMinimizerMask = 0x3F;
 __host__ __device__ constexpr bool order_mod_valid(int k, int m) {
   return k == 8 && (m & kMinimizerMask) == 6;  // the instantiated kernels (kma_device.h)
@@ -188,14 +190,7 @@ __host__ __device__ inline uint32_t mod_sample(uint64_t key, int k, int m) {
   for (int i = 0; i < nt; ++i) {
     const uint32_t t3 = (uint32_t)(key >> (5 * (nt - 1 - i))) & 0x7FFFu;
     // an odd 24-bit multiplier: a bijection of the 15-bit 3-mer codes; position in the low bits
-    uint32_t g = mul24(t3, 0x9E3779u);
-#if KMA_MOD_OPEN
-    // open-closed mod-sampling (tuning variant): 3-mers whose middle residue code is below both
-    // of its neighbours' rank first (simulated density 0.410 vs 0.431, scripts/order_sim.py)
-    const uint32_t c0 = t3 >> 10, c1 = (t3 >> 5) & 31u, c2 = t3 & 31u;
-    g = (c1 < c0 && c1 < c2) ? g >> 1 : (g >> 1) | 0x80000000u;
-#endif
-    g = (g & ~7u) | (uint32_t)i;
+    const uint32_t g = (mul24(t3, 0x9E3779u) & ~7u) | (uint32_t)i;
     best = best < g ? best : g;
   }
   const int p = (int)(best & 7u) % w;
