@@ -6,6 +6,8 @@
  *
  *   - the signature-table load of `apply`
  *       proteins/kmers/anno/ApplyKmerProcessor.java:100-110   -> kma_table_create*
+ *                                                                 (kma_table_create_from_tsv
+ *                                                                 reads kmerdb.tbl itself)
  *   - the per-protein extraction + lookup + vote loop of `apply`
  *       proteins/kmers/anno/ApplyKmerProcessor.java:122-148   -> kma_annotate_proteins*
  *       (ProteinKmers(...) at :123 is the external org.theseed.sequence extractor)
