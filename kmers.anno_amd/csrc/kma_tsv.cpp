@@ -105,13 +105,6 @@ class RoleTable {
       }
     }
   }
-  uint32_t find(std::string_view r) const {  // r was interned
-    const uint64_t h = role_hash(r);
-    for (size_t i = h & (slots_.size() - 1);; i = (i + 1) & (slots_.size() - 1)) {
-      const Slot& s = slots_[i];
-      if (s.h == h && role(s.id) == r) return s.id;
-    }
-  }
   size_t size() const { return offs_.size(); }
   // The role of an id: its bytes live in the table's own arena (compact and cache-resident: a
   // view into the mapped file made every compare a miss to a random page, ~70 ns per row).
@@ -147,6 +140,7 @@ struct Chunk {
   uint64_t rows = 0;
   bool seen[256] = {};
   RoleTable table;               // the chunk's roles -> local ids (first-seen order)
+  std::vector<uint32_t> local;   // row -> local id (pass 2 maps it instead of a second lookup)
   std::vector<uint32_t> global;  // local id -> fid
   int last_len = -1;
 };
@@ -210,7 +204,7 @@ int read_kmer_tsv(const char* path, int k, unsigned threads,
       if (kmer.size() == (size_t)k)
         for (char x : kmer) c.seen[(uint8_t)x] = true;
       bool added;
-      c.table.intern(role, &added);
+      c.local.push_back(c.table.intern(role, &added));
     });
   });
   bool seen[256] = {};
@@ -246,7 +240,9 @@ int read_kmer_tsv(const char* path, int k, unsigned threads,
   // pass 2: packed keys (0: not a k-mer or a byte without a code) and global fids
   parallel(nt, [&](unsigned i) {
     uint64_t r = first[i], sk = 0;
-    for_rows(m, ch[i].lo, ch[i].hi, [&](std::string_view kmer, std::string_view role) {
+    const uint32_t* local = ch[i].local.data();
+    const uint32_t* global = ch[i].global.data();
+    for_rows(m, ch[i].lo, ch[i].hi, [&](std::string_view kmer, std::string_view) {
       uint64_t key = 0;
       if (kmer.size() == (size_t)k) {
         for (char x : kmer) {
@@ -261,7 +257,7 @@ int read_kmer_tsv(const char* path, int k, unsigned threads,
         ++sk;
       }
       out->keys[r] = key;
-      out->fids[r] = ch[i].global[ch[i].table.find(role)];
+      out->fids[r] = global[local[r - first[i]]];
       ++r;
     });
     skipped[i] = sk;

@@ -24,8 +24,8 @@ struct KmerTsv {
 };
 // make_lut(seen, lut): the table's residue codes given the bytes seen in the file's k-length
 // kmers (KMA_OK or a KMA_E_* code). Parsed on `threads` threads over a read-only mapping: pass 1
-// counts rows, marks bytes and collects each chunk's roles in first-seen order; the chunks'
-// roles are merged in file order into global fids; pass 2 packs the keys. Returns KMA_OK or a
+// counts rows, marks bytes and interns each chunk's roles in first-seen order (a local id per
+// row); the chunks' roles are merged in file order into global fids; pass 2 packs the keys. Returns KMA_OK or a
 // KMA_E_* code with a message in *err.
 int read_kmer_tsv(const char* path, int k, unsigned threads,
                   const std::function<int(const bool* seen, uint8_t* lut)>& make_lut,
