@@ -28,3 +28,19 @@ def test_every_loaded_global_exists(module):
                         if g not in vars(mod) and not hasattr(builtins, g):
                             missing.add((name, g))
     assert not missing, sorted(missing)
+
+
+def test_committed_traffic_summary_describes_these_kernels():
+    """bench.py's roofline.traffic / frac_requests come from the committed PMC summary; it is
+    used only when stamped with the digest of this tree's native sources (csrc + ABI header),
+    so the committed file must carry that digest and the c5 probe's kernel (the mod-sampling
+    instantiation, annotate_kernel<8, 70, 8, true>) with its line requests."""
+    import json
+    import bench
+    import kmeranno
+    d = json.load(open(bench.TRAFFIC_FILE))
+    assert d["source_sha16"] == kmeranno.source_digest()
+    rec = d["workloads"]["c5"]["annotate_kernel<8, 70, 8, true>"]
+    assert rec["read_requests"] > 0 and rec["traffic_bytes"] > 0
+    for lf in ("0.75", "0.9"):
+        assert f"c5_lf{lf}" in d["workloads"]
