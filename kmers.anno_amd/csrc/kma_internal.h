@@ -153,20 +153,27 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
 // pick differs from the previous window's) is the probe's home-line requests per window.
 //   random (default): the m-mer of smallest multiplicative hash; density 2/(w + 1) = 0.50 for
 //          K = 8, m = 6 (w = K - m + 1 = 3 m-mers per key).
-//   mod-sampling (kOrderMod; Groot Koerkamp & Pibiri, "The mod-minimizer", WABI 2024) with
-//          t = 3: x = the position of the smallest 3-mer hash among the key's K - 2 3-mers (ties:
-//          the first), the m-mer at x mod w is picked; density (2 + (m - t) / w) / (w + m - t + 1)
-//          = 3/7 = 0.43. Simulated on c5's 10^8-key table (scripts/order_sim.py): density 0.430
-//          vs 0.502, keys beyond a bucket's 8 slots 7.5% vs 6.1% (more keys in their alternate).
-//          Measured (ABAB): c5 kernel 2.88 ms against 3.08 ms for the random order
-//          (profiles/r06/order_ab_r06b/); on the 10^7 table (Infinity-Cache resident) c4 2.637
-//          vs 2.688 ms, c2 even (47.1 vs 46.7 us), but the 6-frame probe, two windows per position
-//          and VALU-heavier, 77.2 vs 73.7 us (profiles/r06/order_small_tables_r06c/). The order is
-//          a table property shared by both paths, so it is a size rule: K = 8, m = 6 tables
+//   mod-sampling (kOrderMod; Groot Koerkamp & Pibiri, "The mod-minimizer", WABI 2024) over
+//          single residues (t = 1): x = the position of the smallest rank among the key's K
+//          residues (rank 31 - code; ties: the first), and the m-mer at x mod w is picked.
+//          Simulated on c5's 10^8-key table (scripts/order_sim.py, profiles/order_sim_r06.log):
+//          density 0.420 vs 0.502, keys beyond a bucket's 8 slots 7.4% vs 6.1% (more keys in
+//          their alternate); with UniProt's residue frequencies 0.421 (identity ranks 0.422,
+//          rarest-first 0.419). The first build sampled 3-mers (t = 3, the positions of the
+//          smallest multiplicative 3-mer hash: density 0.431, 7.8% beyond 8 slots): c5 kernel
+//          2.88 ms against 3.08 ms for the random order (profiles/r06/order_ab_r06b/); t = 1 then
+//          2.855-2.873 against 2.881-2.897 ms and at load factor 0.9 3.557 vs 3.672 ms (ABAB,
+//          profiles/r06/mod_t1_r06f/): a lower density for 8 cheap ranks (shift + one bitop3
+//          each) in place of 6 hashed 3-mers, and x mod 3's shift read from a nibble table.
+//          On the 10^7 table (Infinity-Cache resident) the t = 3 order measured c4 2.637 vs
+//          2.688 ms, c2 even (47.1 vs 46.7 us), but the 6-frame probe, two windows per position
+//          and VALU-heavier, 77.2 vs 73.7 us (profiles/r06/order_small_tables_r06c/). The order
+//          is a table property shared by both paths, so it is a size rule: K = 8, m = 6 tables
 //          larger than the Infinity Cache (kma_abi.cpp minimizer_len), where every request goes
-//          to HBM. Not kept: the open-closed variant (3-mers whose middle residue code is below
-//          both neighbours' rank first; simulated density 0.410) at 3.03 ms, its VALU per window
-//          costing more than the 5% fewer home lines save.
+//          to HBM. Not kept: the open-closed t = 3 variant (3-mers whose middle residue code is
+//          below both neighbours' rank first; simulated density 0.410) at 3.03 ms against
+//          2.88, its VALU per window costing more than the fewer home lines save; t = 2 and 4
+//          simulate at 0.467 / 0.468.
 // The order bit rides in the minimizer length m of layout codes and kernel templates; the
 // minimizer length proper is m & kMinimizerMask.
 constexpr int kOrderMod = KMA_LAYOUT_MOD_SAMPLING;
@@ -174,30 +181,30 @@ constexpr int kMinimizerMask = 0x3F;
 __host__ __device__ constexpr bool order_mod_valid(int k, int m) {
   return k == 8 && (m & kMinimizerMask) == 6;  // the instantiated kernels (kma_device.h)
 }
-__host__ __device__ inline uint32_t mul24(uint32_t a, uint32_t b) {  // a, b < 2^24
-#ifdef __HIP_DEVICE_COMPILE__
-  return __umul24(a, b);
-#else
-  return a * b;
-#endif
-}
 // The picked m-mer's multiplicative hash is the minimizer value (home_from_min mixes it once
 // more; the raw m-mer code there loaded the buckets less evenly: 3.00% vs 2.72% of 3e7 keys past
-// a bucket's slots, scripts/order_sim.py).
-__host__ __device__ inline uint32_t mod_sample(uint64_t key, int k, int m) {
-  const int nt = k - 2, w = k - m + 1;  // 3-mers of the key (<= 6: positions fit 3 bits)
+// a bucket's slots, scripts/order_sim.py). K = 8, m = 6 only (order_mod_valid): the ranks carry
+// 4 x in their low 5 bits, so the winner's low bits index the nibble table of the m-mer's shift
+// 5 (2 - x mod 3) (x = 0..7: 10, 5, 0, 10, 5, 0, 10, 5).
+__host__ __device__ inline uint32_t mod_sample(uint64_t key) {
   uint32_t best = 0xFFFFFFFFu;
-  for (int i = 0; i < nt; ++i) {
-    const uint32_t t3 = (uint32_t)(key >> (5 * (nt - 1 - i))) & 0x7FFFu;
-    // an odd 24-bit multiplier: a bijection of the 15-bit 3-mer codes; position in the low bits
-    const uint32_t g = (mul24(t3, 0x9E3779u) & ~7u) | (uint32_t)i;
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t c = (uint32_t)(key >> (5 * (7 - i))) & 31u;
+    const uint32_t g = (31u - c) << 5 | (uint32_t)(4 * i);
     best = best < g ? best : g;
   }
-  const int p = (int)(best & 7u) % w;
-  return mmer_hash((uint32_t)(key >> (5 * (k - m - p))) & (uint32_t)((1ull << (5 * m)) - 1));
+  const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint32_t sh = __builtin_amdgcn_ubfe(0x5A05A05Au, best, 4u);  // offset: best's low 5 bits
+  const uint32_t sub = __builtin_amdgcn_alignbit(hi, lo, sh) & 0x3FFFFFFFu;
+#else
+  const uint32_t sh = (0x5A05A05Au >> (best & 31u)) & 15u;
+  const uint32_t sub = (uint32_t)(((uint64_t)hi << 32 | lo) >> sh) & 0x3FFFFFFFu;
+#endif
+  return mmer_hash(sub);
 }
 __host__ __device__ inline uint32_t minimizer_hash(uint64_t key, int k, int m) {
-  if (m & kOrderMod) return mod_sample(key, k, m & kMinimizerMask);
+  if (m & kOrderMod) return mod_sample(key);  // (k == 8, m & kMinimizerMask == 6)
   const uint32_t mask = (uint32_t)((1ull << (5 * m)) - 1);
   uint32_t best = 0xFFFFFFFFu;
   for (int p = 0; p <= k - m; ++p) {

@@ -14,8 +14,12 @@ Orders (kma_internal.h minimizer_hash and its round-6 alternatives):
              position), then by hash (round 5's measured variant)
   mod      : mod-sampling (Groot Koerkamp & Pibiri 2024): x = position of the smallest 3-mer hash
              among the key's K - 2 3-mers, the m-mer at x mod (K - m + 1) is the minimizer
+  mod1     : mod-sampling over single residues (t = 1): x = position of the smallest rank
+             31 - code among the key's K residues (ties: the first), the m-mer at x mod 3
+             (shipped); mod1id / mod1rare: the same with the codes / rarest-first as ranks
   m5       : random order with m = 5 (128-byte homes of a lower density)
-Usage: python scripts/order_sim.py [T] [n_proteins]
+Usage: python scripts/order_sim.py [T] [n_proteins] [order,order,...] [skew]
+  skew: residues drawn with UniProt's amino-acid frequencies (default: uniform, as synth.py)
 """
 import sys
 
@@ -61,13 +65,23 @@ def order_value(keys, order, k=8):
             h = mmer_hash(sub_at(keys, k, m, p)) >> U32(1)
             v = np.minimum(v, np.where(closed, h, h | U32(0x80000000)))
         return v
-    if order == "mod":  # kma_internal.h mod_sample, exactly
+    if order == "mod":  # round 6's first mod-sampling build (t = 3; replaced by mod1)
         w = k - m + 1
         best = np.full(len(keys), 0xFFFFFFFF, U32)
         for i in range(k - s + 1):
             t3 = sub_at(keys, k, s, i)
             best = np.minimum(best, (mul32(t3, 0x9E3779) & U32(0xFFFFFFF8)) | U32(i))
         p = ((best & U32(7)) % U32(w)).astype(np.uint64)
+        return mmer_hash(((keys >> (np.uint64(5) * (np.uint64(k - m) - p)))
+                          & np.uint64((1 << (5 * m)) - 1)).astype(U32))
+    if order in ("mod1", "mod1id", "mod1rare"):  # kma_internal.h mod_sample (t = 1): ranks
+        # 31 - code; mod1id: the codes themselves; mod1rare: rarest residue (UniProt) first
+        rank = {"mod1": lambda c: U32(31) - c, "mod1id": lambda c: c, "mod1rare": lambda c: RARE[c]}
+        best = np.full(len(keys), 0xFFFFFFFF, U32)
+        for i in range(k):
+            c = sub_at(keys, k, 1, i)
+            best = np.minimum(best, (rank[order](c) << U32(3)) | U32(i))
+        p = ((best & U32(7)) % U32(3)).astype(np.uint64)
         return mmer_hash(((keys >> (np.uint64(5) * (np.uint64(k - m) - p)))
                           & np.uint64((1 << (5 * m)) - 1)).astype(U32))
     raise ValueError(order)
@@ -89,15 +103,31 @@ def parity(keys):
     return c
 
 
+# UniProtKB/Swiss-Prot amino-acid composition (%), A C D E F G H I K L M N P Q R S T V W Y
+UNIPROT = np.array([8.25, 1.37, 5.45, 6.75, 3.86, 7.07, 2.27, 5.96, 5.84, 9.66, 2.42, 4.06, 4.70,
+                    3.93, 5.53, 6.56, 5.34, 6.87, 1.08, 2.92])
+PROBS = None  # None: uniform residues
+RARE = np.full(32, 31, U32)  # residue code -> rank by UniProt frequency (rarest 0)
+for _r, _i in enumerate(np.argsort(UNIPROT, kind="stable")):
+    RARE[b"ACDEFGHIKLMNPQRSTVWY"[_i] - 64] = _r
+
+
+def residues(rng, n):
+    return rng.integers(0, 20, n) if PROBS is None else rng.choice(20, n, p=PROBS)
+
+
 def random_kmers(rng, n, k=8):
     key = np.zeros(n, np.uint64)
     codes = (np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8).astype(np.uint64) - 64)
     for _ in range(k):
-        key = (key << np.uint64(5)) | codes[rng.integers(0, 20, n)]
+        key = (key << np.uint64(5)) | codes[residues(rng, n)]
     return key
 
 
 def main():
+    global PROBS
+    if len(sys.argv) > 4 and sys.argv[4] == "skew":
+        PROBS = UNIPROT / UNIPROT.sum()
     T = int(float(sys.argv[1])) if len(sys.argv) > 1 else 100_000_000
     n_prot = int(sys.argv[2]) if len(sys.argv) > 2 else 20_000
     nb = (T + 3) // 4  # 8 slots, load factor 0.5
@@ -107,8 +137,9 @@ def main():
     from kmeranno import synth
     lens = rng.choice(synth.cds_lengths(), n_prot)
     aa = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
-    qkeys = [synth.window_keys(aa[rng.integers(0, 20, int(L))]) for L in lens]
-    for order in ("random", "syncmer", "mod", "m5"):
+    qkeys = [synth.window_keys(aa[residues(rng, int(L))]) for L in lens]
+    orders = sys.argv[3].split(",") if len(sys.argv) > 3 else ("random", "syncmer", "mod", "mod1", "m5")
+    for order in orders:
         counts = np.zeros(nb, np.int64)
         chunk = 10_000_000
         krng = np.random.default_rng(55)
@@ -124,7 +155,7 @@ def main():
             pr = pair_of(order_value(q, order), nb)
             changes += 1 + int((pr[1:] != pr[:-1]).sum())
             windows += len(pr)
-        print(f"{order:8s} density {changes / windows:.4f}  overflow {over:.4f}  "
+        print(f"{order:8s} {'skew ' if PROBS is not None else ''}density {changes / windows:.4f}  overflow {over:.4f}  "
               f"overflow of 128-byte homes {over16:.4f}  max keys per bucket {counts.max()}",
               flush=True)
 
