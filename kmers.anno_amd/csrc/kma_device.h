@@ -212,13 +212,25 @@ __device__ __forceinline__ uint32_t match_part_raw(const uint4 (&v)[kBucketHalve
   uint32_t w = 0, missing = 0;
 #pragma unroll
   for (int h = 0; h < kBucketHalves; ++h) {
-    const uint32_t m0 = (uint32_t)(v[h].x == kl) & (uint32_t)((v[h].y & kKeyHiMask) == kh);
-    const uint32_t m1 = (uint32_t)(v[h].z == kl) & (uint32_t)((v[h].w & kKeyHiMask) == kh);
-    // the matching slot's fid (keys are unique: at most one of m0, m1), masked once
-    w |= ((m0 ? v[h].y : 0u) | (m1 ? v[h].w : 0u)) & kFidMask;
-    // slot within the bucket and the hit flag: a lane constant chosen by m1, kept by m0 | m1
+    // key match: (x ^ kl) | ((y ^ kh) & kKeyHiMask) == 0, two bitop3 (truth tables over
+    // (src0, src1, src2) bits, index 4 src0 + 2 src1 + src2: 0x28 = (a ^ b) & c, 0xBE = (a ^ b)
+    // | c) and a compare per slot, where the compiler's xor / xor / and_or took three, and the
+    // verdict one select per slot: with the gather's sentinel-free bucket index (annotate_block)
+    // SQ VALU per wave c5 2,458 -> 2,267, c3 1,927 -> 1,827, and (ABAB) c5 2.853-2.857 ->
+    // 2.832-2.836 ms, c2 47.0 -> 45.0-45.2 us, c3's probe 73.1-73.6 -> 72.2-72.6 us, c4 2.689 ->
+    // 2.711-2.715 ms (profiles/r06/match_gather_r06g/, r06h: the match alone costs c4 0.6%)
+    const bool m0 = __builtin_amdgcn_bitop3_b32(
+                        v[h].x, kl, __builtin_amdgcn_bitop3_b32(v[h].y, kh, kKeyHiMask, 0x28),
+                        0xBE) == 0u;
+    const bool m1 = __builtin_amdgcn_bitop3_b32(
+                        v[h].z, kl, __builtin_amdgcn_bitop3_b32(v[h].w, kh, kKeyHiMask, 0x28),
+                        0xBE) == 0u;
+    // the slot's verdict: fid | slot within the bucket | hit flag (lane constants c0, c1), one
+    // select each (keys are unique: at most one of m0, m1)
     const uint32_t c0 = ((8u * h + 2u * part) << kSlotShift) | kWordHit;
-    w |= (m0 | m1) ? (m1 ? c0 + (1u << kSlotShift) : c0) : 0u;
+    const uint32_t s0 = (v[h].y & kFidMask) | c0;
+    const uint32_t s1 = (v[h].w & kFidMask) | (c0 + (1u << kSlotShift));
+    w |= m0 ? s0 : (m1 ? s1 : 0u);
     // the lane's positions: slot 8h + 2part (bits of .y), slot 8h + 2part + 1 (bits of .w)
     const uint32_t held = ((v[h].y >> kFidBits) & ((1u << FB) - 1u)) |
                           (((v[h].w >> kFidBits) & ((1u << FB) - 1u)) << FB);
@@ -296,9 +308,8 @@ __device__ __forceinline__ bool walk_chain_wide(const uint64_t* __restrict__ slo
   return false;
 }
 
-// kNone: a window that does not probe. The protein kernel packs the block's protein index
-// above the bucket index (buckets < 2^28).
-constexpr uint32_t kNone = 0xFFFFFFFFu;
+// The protein kernel packs the block's protein index above the bucket index (buckets <
+// kMaxBuckets); a window that does not probe carries bucket 0 (its load is discarded).
 constexpr int kBucketBits = 32 - kSlotBits;  // buckets < kMaxBuckets
 constexpr uint32_t kBucketIdx = (1u << kBucketBits) - 1u;
 

@@ -734,8 +734,11 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     __builtin_amdgcn_wave_barrier();
     cn = 0;
   };
-  // A step's windows: packed keys, filter masks and home buckets (bk: protein << kBucketBits |
-  // home bucket, or kNone for a window that does not probe), from the residues in ww.
+  // A step's windows: packed keys (khi: key bits 32..39 << 24, bit 0 set for a window that
+  // does not probe; the match reads khi's top byte only), filter masks and home buckets (bk:
+  // protein << kBucketBits | home bucket, bucket 0 for a window that does not probe), from the
+  // residues in ww. (A kNone sentinel in bk cost the gather a compare and a select per bucket;
+  // a separate flag array, SGPR spills in the ASCII kernels.)
   struct Prep {
     uint32_t klo[U], khi[U], need[U], bk[U];
   };
@@ -753,9 +756,9 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
         ok = pack_window<K>(lut, win_bytes(ww[j]), key) && x < span && window_at<P>(pe, x, p);
       }
       o.klo[j] = (uint32_t)key;
-      o.khi[j] = (uint32_t)(key >> 32) << 24;
+      o.khi[j] = (uint32_t)(key >> 32) << 24 | (ok ? 0u : 1u);  // bit 0: does not probe
       o.need[j] = filter_need<kSlotsPerBucket>(o.klo[j]);
-      o.bk[j] = ok ? (p << kBucketBits | home_bucket(key, K, M, nb)) : kNone;
+      o.bk[j] = p << kBucketBits | (ok ? home_bucket(key, K, M, nb) : 0u);
     }
   };
   // Cooperative loads: the quad's four buckets, 64 bytes at a time (lane `part` reads bytes
@@ -770,7 +773,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint4* bp = reinterpret_cast<const uint4*>(slots) + part +
-                          (uint64_t)(bb[r] == kNone ? 0u : bb[r] & kBucketIdx) * kBucketQuads;
+                          (uint64_t)(bb[r] & kBucketIdx) * kBucketQuads;
 #pragma unroll
         for (int h = 0; h < kBucketHalves; ++h) q[j][r][h] = bp[4 * h];
       }
@@ -812,7 +815,7 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const bool probed = c.bk[j] != kNone;
+      const bool probed = (c.khi[j] & 1u) == 0u;
       const uint32_t w = probed ? word[j] : 0u;
 #ifdef KMA_TUNE_COUNT
       KMA_COUNT(2, __popcll(__ballot(probed)));
@@ -878,11 +881,14 @@ __device__ __forceinline__ void annotate_block(const ProteinArgs& a, ProteinSmem
   }
 }
 
-// Occupancy: kProteinOcc waves per SIMD (its LDS and VGPR budget); the flat layout's packed
-// variant (a fallback for crowded tables: two full-key mixes per window) needs 6 to stay clear
-// of scratch.
+// Occupancy: kProteinOcc waves per SIMD (its LDS and VGPR budget); the flat layout's variants
+// (a fallback for crowded tables: two full-key mixes per window) and the mod-sampling order's
+// ASCII variant (the LUT pack of a window beside the order's ranks; small device calls only,
+// larger ones pack first) need 6 to stay clear of scratch.
 template <int K, int M, bool Packed>
-constexpr int protein_occ() { return M == 0 && Packed ? 6 : kProteinOcc; }
+constexpr int protein_occ() {
+  return (M == 0 && (Packed || K < 8)) || (!Packed && (M & kOrderMod)) ? 6 : kProteinOcc;
+}
 template <int K, int M, int P, bool Packed>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(protein_occ<K, M, Packed>(), 8))) void annotate_kernel(
     ProteinArgs a) {

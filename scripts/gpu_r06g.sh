@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 6 experiment: cheaper bucket match (bitop3 key compares, one select per slot verdict) and
+# gather (no kNone select): the GPU suite with the new build, then c5 / c4 / c2 / c3 ABAB against
+# the previous build (build/base), then SQ counters of c5 and c3 with the new build.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+OUT=${1:-r06g}
+bash scripts/gpu_tests.sh $OUT; rc=$?
+[ $rc -eq 0 ] || exit $rc
+OUT=gpurun_out/$OUT
+for rep in 1 2; do
+  for wl in c5 c4 c2 c3; do
+    for arm in base new; do
+      if [ $arm = base ]; then export KMERANNO_LIB=kmers.anno_amd/build/base/libkmeranno.so; else unset KMERANNO_LIB; fi
+      timeout -k 10 300 python bench.py --workload $wl --no-cpu-baseline --no-extras > $OUT/${wl}_${arm}_r$rep.json 2> $OUT/${wl}_${arm}_r$rep.log
+      r=$?; echo "$wl $arm r$rep rc=$r" >> $OUT/steps.log; [ $r = 0 ] || exit $r
+    done
+  done
+done
+unset KMERANNO_LIB
+SECTIONS=sq SQ_WLS="c5 c3" bash scripts/gpu_measure.sh ${1:-r06g}_sq || exit $?
+python3 - "$OUT" <<'PY'
+import json, glob, sys
+for f in sorted(glob.glob(f"{sys.argv[1]}/c*.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split("/")[-1], round(d["ms_per_step"], 4), {k: round(v, 4) for k, v in d["phases_ms"].items()})
+PY
