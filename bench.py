@@ -39,8 +39,10 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import fnmatch
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -207,7 +209,9 @@ def pmc_traffic(workload: str, kernel: str):
     c2 .. c5, or an LF-sweep tag (c5_lf0.75: c5 at load factor 0.75)."""
     try:
         d = json.load(open(TRAFFIC_FILE))
-        rec = d["workloads"][workload][kernel]
+        recs = d["workloads"][workload]
+        names = [n for n in recs if fnmatch.fnmatchcase(n, kernel)]  # kernel: may hold a '*'
+        rec = recs[names[0]] if len(names) == 1 else recs[kernel]
     except (OSError, KeyError, ValueError):
         return None, None, None, False
     src = os.path.relpath(TRAFFIC_FILE, ROOT)
@@ -339,7 +343,7 @@ def roofline(kind, workload, kernel, kernel_ms, alg_bytes, table_bytes, windows,
     traffic / time / peak beside it; the request view: fabric line requests per launch (PMC)
     per second against the random-64-B ceiling measured live on a buffer of the table's size."""
     name = kernel.split(" (")[0]
-    traffic, reqs, src, stale = pmc_traffic(workload, name)
+    traffic, reqs, src, stale = pmc_traffic(workload, re.sub(r"<(\d+), (\d+), \d+, ", r"<\1, \2, *, ", name))
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     ceil = gather_ceiling(table_bytes) if live else None
     out = {"bound": "hbm" if table_bytes > MALL_BYTES else "infinity-cache",
@@ -423,13 +427,23 @@ def link_rates(residues, n_res, dev):
     return out
 
 
+def kernel_capacity(k, workload):
+    """The protein kernel's template capacity P (proteins per block it holds): K = 8 kernels come
+    in P = 4 / 6 / 8, the smallest holding the call's block proteins (kma_kernels.hip
+    AnnotateLaunch; the library picks 6 per block at c5's size, 4 at c2 / c4's), other K in 8.
+    Shown in the kernel name; the PMC summary's record is matched on any P."""
+    if k != 8:
+        return 8
+    return 6 if workload.split("_lf")[0] == "c5" else 4 if workload in ("c2", "c4") else "*"
+
+
 def protein_roofline(ph, workload, m, n_win, n_res, table_bytes, live=True):
     """Roofline of the protein path's probe kernel (rank 0's shard, times max over ranks)."""
     packed = "pack_kernel" in ph
     return roofline("windows x 64 B + residues (" + ("packed: 0.625 B" if packed else "1 B") +
                     " each)", workload,
-                    f"annotate_kernel<{K}, {m}, 8, {'true' if packed else 'false'}> "
-                    "(probe + sets + vote)",
+                    f"annotate_kernel<{K}, {m}, {kernel_capacity(K, workload)}, "
+                    f"{'true' if packed else 'false'}> (probe + sets + vote)",
                     ph["annotate_kernel"], n_win * BYTES_PER_LOOKUP +
                     (n_res * 5 + 7) // 8 if packed else n_win * BYTES_PER_LOOKUP + n_res,
                     table_bytes, n_win, live=live)

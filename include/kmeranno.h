@@ -102,9 +102,10 @@ extern "C" {
 /* Layout codes (kma_table_build_device, kma_table_wrap_device, kma_table_layout_for): the
  * minimizer length m (0 = flat) | KMA_LAYOUT_TWO_CHOICE for two-choice placement (ABI 6)
  * | KMA_LAYOUT_MOD_SAMPLING for the mod-sampling minimizer order (ABI 7; K = 8, m = 6 only: a
- * key's minimizer is its m-mer at the position of its smallest 3-mer hash modulo K - m + 1,
- * where the default order takes the m-mer of smallest hash; the creators use it for tables
- * larger than the 256 MiB Infinity Cache, where it cuts the probe's bucket requests).         */
+ * key's minimizer is its m-mer at the position, modulo K - m + 1, of its smallest residue
+ * (rank 31 - code, the first on ties), where the default order takes the m-mer of smallest
+ * hash; the creators use it for tables larger than the 256 MiB Infinity Cache, where it cuts
+ * the probe's bucket requests).                                                              */
 #define KMA_LAYOUT_TWO_CHOICE 0x100
 #define KMA_LAYOUT_MOD_SAMPLING 0x40
 #define KMA_MAX_FID ((1u << 22) - 1u)
@@ -137,8 +138,8 @@ typedef struct kma_table_info {
                             most 2 buckets); 0 = overflow chains                            */
   int32_t minimizer_order; /* ABI 7: how a key's minimizer is chosen among its m-mers (layout
                             code bit KMA_LAYOUT_MOD_SAMPLING): 0 = smallest m-mer hash;
-                            1 = mod-sampling (the m-mer at the position of the smallest 3-mer
-                            hash modulo K - m + 1)                                           */
+                            1 = mod-sampling (the m-mer at the position, modulo K - m + 1,
+                            of the smallest residue: rank 31 - code, the first on ties)      */
   int32_t replicate_peer;  /* ABI 7: copies of the last kma_table_replicate made with peer
                             access enabled (the destination GPU reads replica 0 over xGMI)  */
   int32_t replicate_local; /* ABI 7: copies of that call on replica 0's own device; the rest

@@ -1665,6 +1665,17 @@ hipError_t launch_build_two_choice(uint64_t* slots, uint32_t n_buckets, int k, i
   return hipGetLastError();
 }
 
+// The kernel's protein capacity P (its compare chains, protein records and SGPRs scale with
+// it): K = 8 kernels come in P = 4 / 6 / 8 and take the smallest that holds the call's block
+// proteins (the defaults: 6 at c5, 4 at c2 / c4); other K use P = kBlockProteins.
+template <int K, int M, int P>
+hipError_t launch_annotate_p(const ProteinArgs& a, dim3 grid, hipStream_t stream) {
+  if (a.packed)
+    hipLaunchKernelGGL((annotate_kernel<K, M, P, true>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((annotate_kernel<K, M, P, false>), grid, dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
 template <int K, int M>
 struct AnnotateLaunch {
   static hipError_t run(const ProteinArgs& a, hipStream_t stream) {
@@ -1677,11 +1688,11 @@ struct AnnotateLaunch {
     const unsigned blocks = (a.n_seq + bp - 1) / bp;
     if (a.n_groups != blocks) return hipErrorInvalidValue;
     const dim3 grid(a.defer_below ? 2 * blocks : blocks);
-    if (a.packed)
-      hipLaunchKernelGGL((annotate_kernel<K, M, P, true>), grid, dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((annotate_kernel<K, M, P, false>), grid, dim3(256), 0, stream, a);
-    return hipGetLastError();
+    if constexpr (K == 8 && P > 6) {
+      if (bp <= 4) return launch_annotate_p<K, M, 4>(a, grid, stream);
+      if (bp <= 6) return launch_annotate_p<K, M, 6>(a, grid, stream);
+    }
+    return launch_annotate_p<K, M, P>(a, grid, stream);
     }
   }
 };

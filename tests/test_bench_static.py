@@ -34,13 +34,17 @@ def test_committed_traffic_summary_describes_these_kernels():
     """bench.py's roofline.traffic / frac_requests come from the committed PMC summary; it is
     used only when stamped with the digest of this tree's native sources (csrc + ABI header),
     so the committed file must carry that digest and the c5 probe's kernel (the mod-sampling
-    instantiation, annotate_kernel<8, 70, 8, true>) with its line requests."""
+    instantiation at 6 proteins per block, annotate_kernel<8, 70, 6, true>) with its line
+    requests, and bench.py's lookup resolves that record from the name it prints."""
     import json
     import bench
     import kmeranno
     d = json.load(open(bench.TRAFFIC_FILE))
     assert d["source_sha16"] == kmeranno.source_digest()
-    rec = d["workloads"]["c5"]["annotate_kernel<8, 70, 8, true>"]
+    rec = d["workloads"]["c5"]["annotate_kernel<8, 70, 6, true>"]
     assert rec["read_requests"] > 0 and rec["traffic_bytes"] > 0
+    assert bench.kernel_capacity(8, "c5") == 6 and bench.kernel_capacity(8, "c4") == 4
+    traffic, reqs, src, stale = bench.pmc_traffic("c5", "annotate_kernel<8, 70, *, true>")
+    assert (traffic, reqs, stale) == (rec["traffic_bytes"], rec["read_requests"], False)
     for lf in ("0.75", "0.9"):
         assert f"c5_lf{lf}" in d["workloads"]
