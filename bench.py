@@ -480,7 +480,9 @@ def bench_contigs(args, rank, world, dev, stream, sp):
     assert n_hits <= cap, "hit buffer too small"
     if rank == 0:
         value = n_win * args.steps * world / elapsed
-        kname = f"contigs_probe_quad_kernel<{K}, {table.info.minimizer_len}>"
+        m = table.info.minimizer_len | (kmeranno.LAYOUT_MOD_SAMPLING
+                                        if table.info.minimizer_order else 0)
+        kname = f"contigs_probe_quad_kernel<{K}, {m}>"  # M: the order bit rides in m
         out = {
             "metric": METRIC, "value": value, "unit": "kmer lookups/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,

@@ -103,9 +103,9 @@ extern "C" {
  * minimizer length m (0 = flat) | KMA_LAYOUT_TWO_CHOICE for two-choice placement (ABI 6)
  * | KMA_LAYOUT_MOD_SAMPLING for the mod-sampling minimizer order (ABI 7; K = 8, m = 6 only: a
  * key's minimizer is its m-mer at the position, modulo K - m + 1, of its smallest residue
- * (rank 31 - code, the first on ties), where the default order takes the m-mer of smallest
- * hash; the creators use it for tables larger than the 256 MiB Infinity Cache, where it cuts
- * the probe's bucket requests).                                                              */
+ * (rank 31 - code, the first on ties), where the other order takes the m-mer of smallest
+ * hash; the creators use it for every K = 8, m = 6 table: it cuts the probe's bucket
+ * requests).                                                                                 */
 #define KMA_LAYOUT_TWO_CHOICE 0x100
 #define KMA_LAYOUT_MOD_SAMPLING 0x40
 #define KMA_MAX_FID ((1u << 22) - 1u)
@@ -170,8 +170,9 @@ int kma_device_count(int* out_n);
  * variables; tuning builds compiled with -DKMA_TUNING_ENV=1 seed these from KMA_MINIMIZER,
  * KMA_BLOCK_PROTEINS, KMA_DEFER, KMA_HOST_PIECES and KMA_HASH_SLICE). Defaults in brackets.
  *   KMA_OPT_LAYOUT          table creators' layout [-1: size rule + measurement, see
- *                           kma_table_layout_for]; 0 = flat, 6 / 7 = minimizer m = min(K, value);
- *                           6 | KMA_LAYOUT_MOD_SAMPLING = m 6 in the mod-sampling order (K = 8)
+ *                           kma_table_layout_for]; 0 = flat, 6 / 7 = minimizer m = min(K, value)
+ *                           in the smallest-hash order; 6 | KMA_LAYOUT_MOD_SAMPLING = m 6 in the
+ *                           mod-sampling order (K = 8; the size rule's m = 6 code at K = 8)
  *   KMA_OPT_BLOCK_PROTEINS  proteins per annotate_kernel block [0: by batch and table size];
  *                           1..8
  *   KMA_OPT_DEFER           the protein kernel's two-pass grid [-1: automatic for grids of 1-4

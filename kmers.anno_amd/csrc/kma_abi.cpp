@@ -291,9 +291,12 @@ void pool_memcpy(void* dst, const void* src, size_t n) {
 }  // namespace
 
 // The size rule's minimizer code (m | order): m = min(K, 6) up to kMinimizer6Buckets buckets,
-// else min(K, 7); K = 8, m = 6 tables larger than the Infinity Cache take the mod-sampling order
-// (kma_internal.h kOrderMod: fewer home-line requests per window where every request goes to
-// HBM; its extra VALU per window slows the cache-resident configs). KMA_OPT_LAYOUT forces a code.
+// else min(K, 7); K = 8, m = 6 tables take the mod-sampling order (kma_internal.h kOrderMod:
+// fewer home-line requests per window). Until the order's single-residue form and the cheaper
+// bucket match it was kept to tables beyond the Infinity Cache (its VALU slowed the 6-frame
+// probe on the cache-resident 10^7 table); since then the 10^7 table measures c4 2.284 vs
+// 2.763 ms, c2 42.4-42.8 vs 43.4-43.6 us, c3's probe 72.7-72.8 vs 72.9-73.2 us in it
+// (profiles/r06/order_small_tables_r06j/). KMA_OPT_LAYOUT forces a code (6: the random order).
 int kma::minimizer_len(int k, uint64_t n_buckets) {
   const int m6 = k < 6 ? k : 6, m7 = k < 7 ? k : 7;
   const int f = forced_layout();
@@ -303,9 +306,7 @@ int kma::minimizer_len(int k, uint64_t n_buckets) {
   if (f == (6 | kma::kOrderMod)) return kma::order_mod_valid(k, 6) ? 6 | kma::kOrderMod : m6;
   const uint64_t lim = kma::wide_k(k) ? kma::kMinimizer6BucketsWide : kma::kMinimizer6Buckets;
   const int m = n_buckets <= lim ? m6 : m7;
-  const uint64_t bb = kma::wide_k(k) ? 64u : (uint64_t)kma::kBucketBytes;
-  const bool beyond_cache = n_buckets * bb > kInfinityCacheBytes;
-  return kma::order_mod_valid(k, m) && beyond_cache ? m | kma::kOrderMod : m;
+  return kma::order_mod_valid(k, m) ? m | kma::kOrderMod : m;
 }
 
 namespace {

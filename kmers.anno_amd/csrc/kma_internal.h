@@ -167,10 +167,11 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t sub) {
 //          each) in place of 6 hashed 3-mers, and x mod 3's shift read from a nibble table.
 //          On the 10^7 table (Infinity-Cache resident) the t = 3 order measured c4 2.637 vs
 //          2.688 ms, c2 even (47.1 vs 46.7 us), but the 6-frame probe, two windows per position
-//          and VALU-heavier, 77.2 vs 73.7 us (profiles/r06/order_small_tables_r06c/). The order
-//          is a table property shared by both paths, so it is a size rule: K = 8, m = 6 tables
-//          larger than the Infinity Cache (kma_abi.cpp minimizer_len), where every request goes
-//          to HBM. Not kept: the open-closed t = 3 variant (3-mers whose middle residue code is
+//          and VALU-heavier, 77.2 vs 73.7 us (profiles/r06/order_small_tables_r06c/), so it
+//          began as a size rule (tables beyond the Infinity Cache); with t = 1 and the cheaper
+//          bucket match the 10^7 table measures c4 2.284 vs 2.763 ms, c2 -2%, c3 even
+//          (profiles/r06/order_small_tables_r06j/), and every K = 8, m = 6 table takes it
+//          (kma_abi.cpp minimizer_len). Not kept: the open-closed t = 3 variant (3-mers whose middle residue code is
 //          below both neighbours' rank first; simulated density 0.410) at 3.03 ms against
 //          2.88, its VALU per window costing more than the fewer home lines save; t = 2 and 4
 //          simulate at 0.467 / 0.468.

@@ -56,7 +56,8 @@ def test_options_set_get_validate_restore(native_lib):
                                                            1 << 20]
         assert k.layout_for(8, 1000) == 7
     assert [k.get_option(o) for o in range(1, 11)] == [-1, 0, -1, 0, 0, 1, 0, 0, -1, 0]
-    assert k.layout_for(8, 1000) == 6 | k.LAYOUT_TWO_CHOICE
+    assert k.layout_for(8, 1000) == 6 | k.LAYOUT_MOD_SAMPLING | k.LAYOUT_TWO_CHOICE
+    assert k.layout_for(7, 1000) == 6 | k.LAYOUT_TWO_CHOICE
     src = open(os.path.join(ROOT, "kmers.anno_amd", "csrc", "kma_abi.cpp")).read()
     assert src.count("getenv(") == 1 and "#if KMA_TUNING_ENV" in src
 
@@ -88,10 +89,11 @@ def test_contig_window_count_matches_oracle(native_lib, oracle_c, small_gto):
 
 def test_table_layout_host_helper(native_lib, monkeypatch):
     """Layout choice: minimizer m = 6 up to 134M keys at load factor 0.5 (2^28 slots), m = 7
-    beyond; K = 8, m = 6 tables larger than the 256 MiB Infinity Cache in the mod-sampling order
-    (c5's 10^8 keys; c2 / c4's 10^7 stay in the random order); the KMA_OPT_LAYOUT option forces
-    0 (flat), 6, 7 or 6 | mod-sampling, read per call. Narrow tables are tried with two-choice
-    placement first (the layout code's flag) unless KMA_OPT_PLACEMENT = 0; wide tables never."""
+    beyond; K = 8, m = 6 tables in the mod-sampling order (round 6: first only beyond the 256
+    MiB Infinity Cache, then every size); the KMA_OPT_LAYOUT option forces 0 (flat), 6 / 7 (the
+    smallest-hash order) or 6 | mod-sampling, read per call. Narrow tables are tried with
+    two-choice placement first (the layout code's flag) unless KMA_OPT_PLACEMENT = 0; wide
+    tables never."""
     import kmeranno
     tc, mod = kmeranno.LAYOUT_TWO_CHOICE, kmeranno.LAYOUT_MOD_SAMPLING
     kmeranno.set_option(kmeranno.OPT_LAYOUT, -1)
@@ -99,9 +101,10 @@ def test_table_layout_host_helper(native_lib, monkeypatch):
     cache = (256 << 20) // (8 * kmeranno.bucket_slots())  # buckets of the Infinity Cache
     assert kmeranno.layout_for(8, nb6) == 6 | mod | tc
     assert kmeranno.layout_for(8, cache + 1) == 6 | mod | tc
-    assert kmeranno.layout_for(8, cache) == 6 | tc
-    assert kmeranno.layout_for(8, kmeranno.buckets_for(10**7)) == 6 | tc  # c2 / c4
+    assert kmeranno.layout_for(8, cache) == 6 | mod | tc
+    assert kmeranno.layout_for(8, kmeranno.buckets_for(10**7)) == 6 | mod | tc  # c2 / c4
     assert kmeranno.layout_for(8, kmeranno.buckets_for(10**8)) == 6 | mod | tc  # c5
+    assert kmeranno.layout_for(8, 1000) == 6 | mod | tc
     assert kmeranno.layout_for(7, nb6) == 6 | tc  # mod-sampling: K = 8 only
     assert kmeranno.layout_for(8, nb6 + 1) == 7 | tc
     assert kmeranno.layout_for(5, 1 << 30) == 5 | tc  # m <= K
@@ -112,6 +115,9 @@ def test_table_layout_host_helper(native_lib, monkeypatch):
     assert kmeranno.layout_for(8, 1000) == 0 | tc
     kmeranno.set_option(kmeranno.OPT_LAYOUT, 7)
     assert kmeranno.layout_for(8, 1000) == 7 | tc
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, 6)  # the smallest-hash order, forced
+    assert kmeranno.layout_for(8, 1000) == 6 | tc
+    kmeranno.set_option(kmeranno.OPT_LAYOUT, -1)
 
 
 def test_choose_layout_rule():
@@ -125,7 +131,7 @@ def test_choose_layout_rule():
     import kmeranno
     tc = kmeranno.LAYOUT_TWO_CHOICE
     n = 99_821_868
-    six = 6 | kmeranno.LAYOUT_MOD_SAMPLING  # the size rule's m = 6 code at c5 (round 6)
+    six = 6 | kmeranno.LAYOUT_MOD_SAMPLING  # the size rule's m = 6 code at K = 8 (round 6)
     assert kmeranno.layout_for(8, 25_000_000) == six | tc
     sweep = {  # load factor -> layout -> status
         0.5: {six: [0, n, 10, int(0.0770 * n)], 7: [0, n, 7, int(0.0239 * n)], 0: [0, n, 6, int(0.0086 * n)]},

@@ -76,7 +76,7 @@ def test_config5_size_sample_and_properties(kma, oracle_c, c5data, monkeypatch):
     dev = torch.device("cuda", 0)
     with kma.SignatureTable.from_packed(sig.keys, sig.fids, K) as t:
         assert t.info.minimizer_len == 6 and t.info.n_buckets == 200_000_000 // kma.bucket_slots()
-        assert t.info.minimizer_order == 1  # round 6: mod-sampling beyond the Infinity Cache
+        assert t.info.minimizer_order == 1  # round 6: mod-sampling (K = 8, m = 6)
         assert t.info.n_entries > 0.99 * len(sig.keys)
         fid, cnt, st, tally = kma.annotate_proteins(t, res, off, 5, 0, n_fid=n_fid)
         # property 0: the two-pass grid gives the same outputs on the whole batch

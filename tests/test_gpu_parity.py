@@ -21,19 +21,20 @@ pytestmark = pytest.mark.gpu
 K = 8
 
 
-@pytest.fixture(params=["auto", "7", "0", "chained", "mod"],
-                ids=["m-auto", "m7", "flat", "chained", "m6-mod"])
+@pytest.fixture(params=["auto", "7", "0", "chained", "6"],
+                ids=["m-auto", "m7", "flat", "chained", "m6-random"])
 def layout(request, monkeypatch):
     """Table layouts: the size-derived minimizer layout (m = 6 up to 134M keys at load factor
-    0.5), the m = 7 layout of larger tables, the flat fallback, and m = 6 in the mod-sampling
-    order (round 6: the size rule's choice for K = 8 tables beyond the Infinity Cache, c5; forced
-    here on small tables) (the KMA_OPT_LAYOUT option, read per table creation), each with the
-    default two-choice placement; and the size-derived layout with overflow chains
-    (KMA_OPT_PLACEMENT = 0: the placement of wide tables and of a two-choice build that fails)."""
+    0.5; at K = 8 in the mod-sampling order, round 6), the m = 7 layout of larger tables, the
+    flat fallback, and m = 6 in the smallest-hash order (the size rule's choice for K < 8, and
+    before round 6 for every table; forced here) (the KMA_OPT_LAYOUT option, read per table
+    creation), each with the default two-choice placement; and the size-derived layout with
+    overflow chains (KMA_OPT_PLACEMENT = 0: the placement of wide tables and of a two-choice
+    build that fails)."""
     import kmeranno
     kmeranno.load()
     p = request.param
-    code = {"auto": -1, "chained": -1, "mod": 6 | kmeranno.LAYOUT_MOD_SAMPLING}.get(p)
+    code = {"auto": -1, "chained": -1}.get(p)
     kmeranno.set_option(kmeranno.OPT_LAYOUT, int(p) if code is None else code)
     kmeranno.set_option(kmeranno.OPT_PLACEMENT, 0 if p == "chained" else -1)
     return p
@@ -232,10 +233,10 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags, input_mode)
         assert t.info.n_entries == ot.size
         if layout in ("7", "0"):
             assert t.info.minimizer_len == int(layout)
-        elif layout == "mod" and lf == 0.5:
+        elif layout == "6" and lf == 0.5:
+            assert t.info.minimizer_len == 6 and t.info.minimizer_order == 0
+        elif lf == 0.5:  # size rule, few displaced keys: m = 6, mod-sampling at K = 8
             assert t.info.minimizer_len == 6 and t.info.minimizer_order == 1
-        elif lf == 0.5:
-            assert t.info.minimizer_len == 6  # size rule, few displaced keys
         if lf <= 0.9:
             assert t.info.two_choice == (0 if layout == "chained" else 1)
         if lf == 0.9:
