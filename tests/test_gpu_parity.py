@@ -249,7 +249,9 @@ def test_synthetic_vs_oracle(kma, oracle_c, layout, path, lf, flags, input_mode)
 @pytest.mark.parametrize("defer", ["64", "3", "1"])
 def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defer):
     """The direct kernel's two-pass grid: every group deferred to the second pass (64 steps),
-    the automatic threshold (3) and none (1 step); four calls in a row, block sizes 4 and 1."""
+    the automatic threshold (3) and none (1 step); calls in a row at block sizes 4, 1, 5, 7, 8
+    and 6: each kernel capacity (K = 8: P = 4 for 1-4, 6 for 5-6, 8 for 7-8) with full and
+    partial blocks."""
     from kmeranno import synth
     wl = synth.make_workload(9000, 200_000, 2000, seed=23)
     kmers = [synth.unpack_key(x) for x in wl.keys]
@@ -257,7 +259,7 @@ def test_deferral_thresholds_and_repeated_calls(kma, oracle_c, monkeypatch, defe
     efid, ecnt, est = oracle_c.apply(ot, wl.residues, wl.offsets, K, 5, 0)
     kma.set_option(kma.OPT_DEFER, int(defer))
     with kma.SignatureTable.from_packed(wl.keys, wl.fids, K) as t:
-        for bp in ("4", "1", "4", "1"):
+        for bp in ("4", "1", "5", "7", "8", "6"):
             kma.set_option(kma.OPT_BLOCK_PROTEINS, int(bp))
             fid, cnt, st, tally = kma.annotate_proteins(t, wl.residues, wl.offsets, 5, 0,
                                                         n_fid=2000)
